@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Diarized frames/sec (10 ms hop) of the MI355X TS-VAD path — BASELINE.json metric.
+
+Default workload (N=1): config C2 — AliMeeting-shaped 10-min 4-speaker meeting
+(synthetic 16 kHz audio, seeded random weights of the reference architecture),
+TS-VAD CAM++_ots_vad + 6-layer Conformer + BiLSTM (ots_vad_style v1), rs_len 6 s,
+segment_shift 1 s, 64 windows per batch, bf16 MFMA.  One step = the whole hot
+path over one meeting: wav already in HBM -> kaldi fbank -> window CMN -> model
+-> sigmoid + overlap-average posteriors (NS, 25 Hz frames).
+
+N GPUs (torchrun, one process per GPU, RCCL): weak scaling — the meeting is N x
+the per-rank length, windows are sharded by contiguous batch ranges and the
+per-window logits are all-gathered (the only exchange) before averaging.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+WORKLOADS = {
+    "c2": dict(variant=1, rs_len=6, minutes=10.0, desc="C2: AliMeeting-shaped 4-spk meeting, TS-VAD "
+               "CAM++_ots_vad + 6-layer Conformer + BiLSTM (ots_vad_style v1), rs_len 6 s, shift 1 s"),
+    "c4": dict(variant=0, rs_len=4, minutes=60.0, desc="C4: 4-spk long-form meeting, TS-VAD CAM++ + "
+               "transformer (default TSVADConfig), rs_len 4 s, shift 1 s"),
+}
+
+PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK = 8000.0                        # GB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--minutes", type=float, default=None, help="meeting minutes per GPU")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, sd_np, meeting, ts, target_s):
+    """The CPU oracle (PyTorch-CPU restatement of the reference inference loop,
+    parity-pinned by tests/golden) on a bounded sample of the same meeting."""
+    import torch
+    from oracle.pipeline_ref import meeting_posteriors
+    from speaker_diarization_amd.weights import to_torch
+    sd = to_torch(sd_np)
+    threads = torch.get_num_threads()
+    n_lab = meeting.labels.shape[1]
+    probe = 8
+    t0 = time.perf_counter()
+    meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=probe, max_windows=probe)
+    per_win = (time.perf_counter() - t0) / probe
+    n = int(max(probe, min(256, target_s / max(per_win, 1e-6))))
+    n = max(probe, (n // probe) * probe)
+    t0 = time.perf_counter()
+    meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=min(64, n), max_windows=n)
+    dt = time.perf_counter() - t0
+    frames = n * 100 * 1   # each window advances the meeting by segment_shift (1 s) = 100 frames
+    return dict(value=frames / dt, unit="frames/s", cores=threads, kind="port",
+                sample=f"first {n} windows ({n} s of meeting, fp32, batch {min(64, n)}) of the same meeting "
+                       f"through oracle/pipeline_ref.py on {threads} host threads: {dt:.1f} s")
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from speaker_diarization_amd import _lib
+    from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
+    from speaker_diarization_amd.ts_vad.model import TSVADModel
+    from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    from speaker_diarization_amd.weights import TSVADConfig, to_torch, tsvad_state_dict
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    wl = WORKLOADS[a.workload]
+    minutes = a.minutes if a.minutes is not None else wl["minutes"]
+    cfg = TSVADConfig(rs_len=wl["rs_len"]) if wl["variant"] == 0 else TSVADConfig.ots_vad_v1(rs_len=wl["rs_len"])
+    sd_np = tsvad_state_dict(cfg, seed=777)
+    model = TSVADModel(cfg, device=dev, precision=a.precision, max_batch=a.batch)
+    model.load_state_dict(to_torch(sd_np))
+    pipe = TSVADPipeline(model, segment_shift=1, batch_size=a.batch)
+
+    total_s = minutes * 60.0 * world
+    meeting = make_meeting(total_s, n_spk=4, seed=777)
+    ts_np = speaker_embeddings(4, seed=777)
+    wav = torch.from_numpy(meeting.wav).to(dev)
+    ts = torch.from_numpy(ts_np).to(dev)
+    n_lab = meeting.labels.shape[1]
+    frames_per_step = meeting.wav.size // 160     # 10 ms frames of the whole meeting
+
+    def step():
+        return pipe.posteriors(wav, ts, n_lab)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        post = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / a.steps * 1000.0
+    value = frames_per_step * a.steps / elapsed
+
+    # Live kernel timing (HIP events on the launch stream) over one extra step.
+    roofline, kernels = None, None
+    if not a.no_kernel_timing:
+        lib = _lib.load()
+        lib.sd_prof_reset()
+        lib.sd_prof_enable(1)
+        step()
+        torch.cuda.synchronize()
+        lib.sd_prof_enable(0)
+        kernels = _lib.prof_stats()
+        lib.sd_prof_reset()
+        dom = max(kernels, key=lambda k: kernels[k]["ms"])
+        st = kernels[dom]
+        avg_ms = st["ms"] / st["launches"]
+        if st["flops"] > 0 and ("gemm" in dom or "attention" in dom):
+            dt = "bf16" if dom.endswith("bf16") else "f32"
+            ach = st["flops"] / (st["ms"] * 1e-3) / 1e12
+            roofline = dict(bound="mfma", achieved=round(ach, 2), peak=PEAKS[dt], unit="TFLOP/s",
+                            frac=round(ach / PEAKS[dt], 4), traffic=None, kernel=dom,
+                            launches=st["launches"], avg_launch_ms=round(avg_ms, 4),
+                            flops_per_launch=st["flops"] / st["launches"])
+        else:
+            ach = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+            roofline = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK, unit="GB/s",
+                            frac=round(ach / HBM_PEAK, 4), traffic=None, kernel=dom,
+                            launches=st["launches"], avg_launch_ms=round(avg_ms, 4))
+        pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                tr = json.load(open(pmc)).get(a.workload, {}).get(dom)
+                if tr:
+                    roofline["traffic"] = tr
+            except Exception:
+                pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, sd_np, meeting, ts_np, a.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "diarized frames/sec (10 ms hop)",
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic 16 kHz 4-speaker meeting (speaker_diarization_amd/synth.py), seeded random "
+                    "weights of the reference architecture",
+            "config": {"workload": wl["desc"], "meeting_minutes": minutes * world,
+                       "minutes_per_gpu": minutes, "windows": pipe.plan(n_lab).n_win,
+                       "global_batch": a.batch * world, "batch_per_gpu": a.batch,
+                       "parallelism": f"window-shard x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if kernels:
+            tot = sum(v["ms"] for v in kernels.values())
+            line["kernel_ms_share"] = {k: round(v["ms"] / tot, 3) for k, v in
+                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

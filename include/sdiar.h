@@ -1,0 +1,124 @@
+/*
+ * sdiar.h — C ABI of the MI355X (gfx950) diarization inference engine.
+ *
+ * Plain pointers, sizes and a hipStream_t passed as void*.  Device pointers are
+ * caller-owned (torch tensors, hipMalloc); weights are copied from host arrays
+ * into a handle-owned device arena.  Every call returns 0 (SD_OK) or a negative
+ * status; sd_last_error() returns the message of the last failure on the
+ * calling thread.  All compute calls are stream-ordered and do not allocate,
+ * so they can be captured into a hipGraph.
+ *
+ * The reference has no FFI: its boundary is the PyTorch nn.Module surface.
+ * Each entry point below names the reference callable it replaces; the Python
+ * mirror (speaker_diarization_amd/) binds them with ctypes.
+ */
+#ifndef SDIAR_H_
+#define SDIAR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SD_OK 0
+#define SD_ERR_INVALID (-1)  /* ValueError in the reference                       */
+#define SD_ERR_SHAPE (-2)    /* AssertionError (label / feature length mismatch)  */
+#define SD_ERR_PARAM (-3)    /* load_state_dict missing/unexpected key            */
+#define SD_ERR_HIP (-4)      /* HIP runtime failure                               */
+#define SD_ERR_STATE (-5)    /* handle used before finalize                       */
+
+const char* sd_last_error(void);
+int sd_version(void);
+
+/* Opt-in kernel-family timing (HIP events on the launch stream) with
+ * algorithmic FLOP/byte counts; used by bench.py for the live roofline.
+ * sd_prof_query fills family i and returns 1, or returns 0 past the end. */
+void sd_prof_enable(int on);
+void sd_prof_reset(void);
+int sd_prof_query(int i, char* name, int name_len, int64_t* launches, double* flops, double* bytes,
+                  double* ms);
+
+/* ------------------------------------------------------------------ TS-VAD
+ * Replaces TSVADModel (egs/alimeeting/ts_vad2/model.py:179-1142):
+ *   construction  model.py:180-225 (TSVADConfig model.py:40-110)
+ *   load_state_dict  (infer.py:184 loads checkpoint["model"])
+ *   forward(ref_speech, target_speech, labels, num_updates)  model.py:899-921
+ */
+typedef struct sd_tsvad sd_tsvad;
+
+typedef struct {
+  int variant;                    /* 0: speech_encoder_type "CAM++", single/multi_backend "transformer"
+                                     1: "CAM++_ots_vad", "conformer_ots_vad", "lstm_ots_vad", ots_vad_style "v1" */
+  int max_num_speaker;            /* TSVADDataConfig.max_num_speaker (4)                     */
+  int rs_len;                     /* seconds; PositionalEncoding max_len = rs_len * 25       */
+  int max_batch;                  /* workspace sizing                                        */
+  int max_fbank_frames;           /* workspace sizing: 1 + (rs_len*16000 - 400) / 160        */
+  int precision;                  /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate */
+  int num_transformer_layer;      /* TSVADConfig defaults: 2, 4, 384, 1536, 192              */
+  int num_attention_head;
+  int transformer_embed_dim;
+  int transformer_ffn_embed_dim;
+  int speaker_embed_dim;
+} sd_tsvad_config;
+
+int sd_tsvad_create(const sd_tsvad_config* cfg, sd_tsvad** out);
+/* One state_dict entry by its reference key name (fp32 host data, torch shape). */
+int sd_tsvad_set_param(sd_tsvad* h, const char* name, const float* host_data, const int64_t* shape,
+                       int ndim);
+/* Folds BatchNorms, packs/uploads weights, allocates the workspace.  Fails with
+ * SD_ERR_PARAM listing missing or unexpected keys (strict load_state_dict). */
+int sd_tsvad_finalize(sd_tsvad* h);
+/* ref_speech: device (B, T_fbank, 80) fbank after per-window CMN + batch pad;
+ * target_speech: device (B, max_num_speaker, speaker_embed_dim);
+ * logits: device (B, max_num_speaker, T_label) — pre-sigmoid, like forward(). */
+int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_speech, int B,
+                     int T_fbank, int T_label, float* logits, void* stream);
+int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
+int sd_tsvad_destroy(sd_tsvad* h);
+
+/* ------------------------------------------------------------------ frontend
+ * FBank.__call__ (ts_vad2/ts_vad_dataset.py:29-56) over a whole recording at
+ * dither 0: wav (n_samples) device fp32 in [-1,1), in_scale = 32768.
+ * mel_fb: device (n_mels, 257) HTK banks (host-built, see frontend.py).
+ * out: device (n_frames, n_mels), n_frames = 1 + (n_samples - 400) / 160. */
+int sd_fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
+                   const float* mel_fb, int n_mels, float* out, void* stream);
+/* Window slicing + per-window mean normalisation (mean_nor=True, :55) + the
+ * collater's zero pad to the batch max (ts_vad_dataset.py:664-701).
+ * win_start / win_n: device int32 (n_win). out: device (n_win, T_out, n_mels). */
+int sd_window_cmn(const float* feats, int n_mels, const int* win_start, const int* win_n, int n_win,
+                  int T_out, float* out, void* stream);
+
+/* ------------------------------------------------------------------ posteriors
+ * sigmoid (model.py:945-946) + mean over the overlapping windows covering each
+ * label frame, in window order (ts_vad2/infer.py:90-94).  logits: device
+ * (n_win, NS, Tw); start/len: device int32 (n_win) in label frames; windows start
+ * every `dis` frames and span at most `chunk`.  out: device (NS, n_frames). */
+int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start,
+                       const int* len, int dis, int chunk, int n_frames, float* out, void* stream);
+
+/* ------------------------------------------------------------------ ops (parity tests)
+ * precision: 0 fp32, 1 bf16.  Weights are fp32 device arrays in torch layout. */
+/* nn.Linear: out (M, N) = act(x (M, K) · w (N, K)ᵀ + b). act: 0 none 1 relu 2 sigmoid 3 silu */
+int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, int N, int act,
+                 float* out, int precision, void* stream);
+/* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
+int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
+                 int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);
+/* nn.Conv2d (Cin % 32 == 0) on NHWC x (B, H, W, Cin), weight (Cout, Cin, kh, kw) -> NHWC out. */
+int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int kh,
+                 int kw, int sh, int sw, int ph, int pw, float* out, int precision, void* stream);
+/* Attention core on packed qkv (S*T, 3D) -> out (S*T, D). */
+int sd_op_attention(const float* qkv, int S, int T, int D, int nh, int causal, int causal_delay,
+                    const int* key_len, float* out, int precision, void* stream);
+int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
+                    float* y, void* stream);
+/* LSTM recurrence on precomputed gx (B, T, ndir*4H) (biases included); whh (ndir, 4H, H). */
+int sd_op_lstm(const float* gx, int B, int T, int H, int ndir, const float* whh, const int* lengths,
+               float* out, float* hT, float* cT, float* work, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDIAR_H_ */

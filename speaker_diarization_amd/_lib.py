@@ -1,0 +1,139 @@
+"""ctypes binding of libsdiar.so (include/sdiar.h).
+
+The HIP library is the only compute path: if it is missing or fails to load,
+every entry point raises immediately — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SDIAR_LIB", os.path.join(_HERE, "lib", "libsdiar.so"))
+
+SD_OK = 0
+SD_ERR_INVALID = -1
+SD_ERR_SHAPE = -2
+SD_ERR_PARAM = -3
+SD_ERR_HIP = -4
+SD_ERR_STATE = -5
+
+
+class SdiarError(RuntimeError):
+    """Device / runtime failure inside libsdiar."""
+
+
+class TsvadConfig(ctypes.Structure):
+    _fields_ = [
+        ("variant", c_int),
+        ("max_num_speaker", c_int),
+        ("rs_len", c_int),
+        ("max_batch", c_int),
+        ("max_fbank_frames", c_int),
+        ("precision", c_int),
+        ("num_transformer_layer", c_int),
+        ("num_attention_head", c_int),
+        ("transformer_embed_dim", c_int),
+        ("transformer_ffn_embed_dim", c_int),
+        ("speaker_embed_dim", c_int),
+    ]
+
+
+_SIGS = {
+    "sd_last_error": (c_char_p, []),
+    "sd_version": (c_int, []),
+    "sd_prof_enable": (None, [c_int]),
+    "sd_prof_reset": (None, []),
+    "sd_prof_query": (c_int, [c_int, c_char_p, c_int, POINTER(c_int64), POINTER(ctypes.c_double),
+                              POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
+    "sd_tsvad_create": (c_int, [POINTER(TsvadConfig), POINTER(c_void_p)]),
+    "sd_tsvad_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_tsvad_finalize": (c_int, [c_void_p]),
+    "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
+    "sd_tsvad_destroy": (c_int, [c_void_p]),
+    "sd_fbank_kaldi": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "sd_window_cmn": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sd_overlap_average": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                   c_void_p, c_void_p]),
+    "sd_op_linear": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "sd_op_conv1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                             c_int, c_int, c_void_p, c_int, c_void_p]),
+    "sd_op_conv2d": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                             c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "sd_op_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                c_void_p]),
+    "sd_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
+    "sd_op_lstm": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """Load libsdiar.so (raises if it is missing: the product has no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libsdiar.so not found at {LIB_PATH}; build it with "
+            "`python -m speaker_diarization_amd.build` (HIP extension is required)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = ""):
+    if status == SD_OK:
+        return
+    msg = load().sd_last_error().decode(errors="replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if status == SD_ERR_INVALID:
+        raise ValueError(msg)
+    if status == SD_ERR_SHAPE:
+        raise AssertionError(msg)
+    if status == SD_ERR_PARAM:
+        raise RuntimeError(f"Error(s) in loading state_dict: {msg}")
+    raise SdiarError(msg)
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(t) -> int:
+    """Raw device/host pointer of a contiguous torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), "sdiar expects contiguous tensors"
+    return t.data_ptr()
+
+
+def prof_stats():
+    """{family: dict(launches, flops, bytes, ms)} from the library's event timers."""
+    lib = load()
+    out = {}
+    i = 0
+    buf = ctypes.create_string_buffer(128)
+    while True:
+        l, f, b, ms = c_int64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        if not lib.sd_prof_query(i, buf, 128, ctypes.byref(l), ctypes.byref(f), ctypes.byref(b), ctypes.byref(ms)):
+            break
+        out[buf.value.decode()] = dict(launches=l.value, flops=f.value, bytes=b.value, ms=ms.value)
+        i += 1
+    return out
+
+
+def stream_ptr(device=None):
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

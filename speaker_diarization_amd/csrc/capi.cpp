@@ -1,0 +1,236 @@
+// extern "C" boundary (include/sdiar.h).  Exceptions never cross it: every
+// entry point maps sd::Error to a status code + thread-local message.
+#include "../../include/sdiar.h"
+
+#include <cmath>
+#include <memory>
+#include <string>
+
+#include <algorithm>
+
+#include "kernels.h"
+#include "prof.h"
+#include "tsvad.h"
+
+namespace sd {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+const char* last_error() { return g_err.c_str(); }
+}  // namespace sd
+
+struct sd_tsvad {
+  std::unique_ptr<sd::TsvadModel> model;
+};
+
+namespace {
+
+template <typename F>
+int guard(F&& f) {
+  try {
+    f();
+    return SD_OK;
+  } catch (const sd::Error& e) {
+    sd::set_error(e.msg);
+    return e.code;
+  } catch (const std::exception& e) {
+    sd::set_error(e.what());
+    return SD_ERR_HIP;
+  } catch (...) {
+    sd::set_error("unknown error");
+    return SD_ERR_HIP;
+  }
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Scratch for test-only ops (packed weights); freed after the stream drains.
+struct Scratch {
+  void* p = nullptr;
+  hipStream_t st;
+  Scratch(size_t bytes, hipStream_t s) : st(s) { SD_HIP(hipMalloc(&p, bytes ? bytes : 4)); }
+  ~Scratch() {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* sd_last_error(void) { return sd::last_error(); }
+int sd_version(void) { return 1; }
+
+void sd_prof_enable(int on) { sd::prof_enable(on != 0); }
+void sd_prof_reset(void) { sd::prof_reset(); }
+int sd_prof_query(int i, char* name, int name_len, int64_t* launches, double* flops, double* bytes,
+                  double* ms) {
+  std::string n;
+  long long l;
+  if (!sd::prof_query(i, n, l, *flops, *bytes, *ms)) return 0;
+  *launches = l;
+  if (name && name_len > 0) {
+    size_t k = std::min<size_t>(n.size(), (size_t)name_len - 1);
+    n.copy(name, k);
+    name[k] = '\0';
+  }
+  return 1;
+}
+
+int sd_tsvad_create(const sd_tsvad_config* c, sd_tsvad** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->variant == 0 || c->variant == 1, sd::kErrInvalid, "unknown TS-VAD variant");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->max_batch > 0 && c->max_fbank_frames > 0, sd::kErrInvalid, "bad workspace sizes");
+    sd::TsvadConfig t;
+    t.variant = c->variant;
+    t.max_num_speaker = c->max_num_speaker;
+    t.rs_len = c->rs_len;
+    t.max_batch = c->max_batch;
+    t.max_fbank_frames = c->max_fbank_frames;
+    t.bf16 = c->precision == 1;
+    t.num_transformer_layer = c->num_transformer_layer;
+    t.num_attention_head = c->num_attention_head;
+    t.embed_dim = c->transformer_embed_dim;
+    t.ffn_dim = c->transformer_ffn_embed_dim;
+    t.speaker_embed_dim = c->speaker_embed_dim;
+    auto* h = new sd_tsvad;
+    h->model.reset(new sd::TsvadModel(t));
+    *out = h;
+  });
+}
+
+int sd_tsvad_set_param(sd_tsvad* h, const char* name, const float* data, const int64_t* shape,
+                       int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_tsvad_finalize(sd_tsvad* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_tsvad_forward(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl,
+                     float* logits, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
+    h->model->forward(ref, ts, B, Tf, Tl, logits, S(stream));
+  });
+}
+
+int64_t sd_tsvad_device_bytes(const sd_tsvad* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
+
+int sd_tsvad_destroy(sd_tsvad* h) {
+  return guard([&] { delete h; });
+}
+
+int sd_fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
+                   const float* mel_fb, int n_mels, float* out, void* stream) {
+  return guard([&] {
+    SD_CHECK(n_frames >= 0 && (n_frames == 0 || n_samples >= 400 + (int64_t)(n_frames - 1) * 160),
+             sd::kErrInvalid, "fbank: n_frames exceeds the samples");
+    sd::fbank_kaldi(wav, n_samples, in_scale, n_frames, mel_fb, n_mels, out, S(stream));
+  });
+}
+
+int sd_window_cmn(const float* feats, int n_mels, const int* win_start, const int* win_n, int n_win,
+                  int T_out, float* out, void* stream) {
+  return guard([&] {
+    if (n_win == 0) return;
+    sd::window_cmn(feats, n_mels, win_start, win_n, n_win, T_out, out, S(stream));
+  });
+}
+
+int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start,
+                       const int* len, int dis, int chunk, int n_frames, float* out, void* stream) {
+  return guard([&] {
+    SD_CHECK(dis > 0 && chunk > 0, sd::kErrInvalid, "overlap_average: bad window geometry");
+    sd::overlap_average(logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out, S(stream));
+  });
+}
+
+int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, int N, int act,
+                 float* out, int precision, void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    const bool bf = precision == 1;
+    Scratch wt((size_t)N * K * (bf ? 2 : 4), st);
+    sd::pack_weight(w, N, K, 1, wt.p, bf, st);
+    sd::ConvGemmArgs p = sd::linear_args(x, M, K, K, wt.p, N, out, N);
+    p.beta = b;
+    p.act = act;
+    sd::conv_gemm(p, bf, st);
+  });
+}
+
+int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
+                 int k, int stride, int pad, int dil, int act, float* out, int precision,
+                 void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    const bool bf = precision == 1;
+    Scratch wt((size_t)Cout * Cin * k * (bf ? 2 : 4), st);
+    sd::pack_weight(w, Cout, Cin, k, wt.p, bf, st);
+    sd::ConvGemmArgs p;
+    p.A = x; p.B = B; p.H = 1; p.W = T; p.Cin = Cin; p.lda = Cin;
+    p.kh = 1; p.kw = k; p.sw = stride; p.pw = pad; p.dw = dil;
+    p.Ho = 1; p.Wo = (T + 2 * pad - dil * (k - 1) - 1) / stride + 1;
+    SD_CHECK(p.Wo > 0, sd::kErrInvalid, "conv1d: empty output");
+    p.Wt = wt.p; p.N = Cout; p.K = Cin * k;
+    p.beta = b; p.act = act;
+    p.out = out; p.o_sb = (int64_t)p.Wo * Cout; p.o_sw = Cout; p.o_sn = 1;
+    sd::conv_gemm(p, bf, st);
+  });
+}
+
+int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int kh,
+                 int kw, int sh, int sw, int ph, int pw, float* out, int precision, void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    const bool bf = precision == 1;
+    Scratch wt((size_t)Cout * Cin * kh * kw * (bf ? 2 : 4), st);
+    sd::pack_weight(w, Cout, Cin, kh * kw, wt.p, bf, st);
+    sd::ConvGemmArgs p;
+    p.A = x; p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.lda = Cin;
+    p.kh = kh; p.kw = kw; p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw;
+    p.Ho = (H + 2 * ph - kh) / sh + 1;
+    p.Wo = (W + 2 * pw - kw) / sw + 1;
+    p.Wt = wt.p; p.N = Cout; p.K = Cin * kh * kw;
+    p.out = out; p.o_sb = (int64_t)p.Ho * p.Wo * Cout; p.o_sh = (int64_t)p.Wo * Cout; p.o_sw = Cout;
+    p.o_sn = 1;
+    sd::conv_gemm(p, bf, st);
+  });
+}
+
+int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, int causal_delay,
+                    const int* key_len, float* out, int precision, void* stream) {
+  return guard([&] {
+    sd::AttnArgs a;
+    a.qkv = qkv; a.S = S_; a.T = T; a.D = D; a.nh = nh; a.ld_qkv = 3 * D;
+    a.out = out; a.ldo = D; a.scale = 1.f / std::sqrt((float)(D / nh));
+    a.causal = causal; a.causal_delay = causal_delay; a.key_len = key_len;
+    sd::attention(a, precision == 1, S(stream));
+  });
+}
+
+int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
+                    float* y, void* stream) {
+  return guard([&] { sd::layernorm(x, rows, D, D, g, b, eps, y, D, S(stream)); });
+}
+
+int sd_op_lstm(const float* gx, int B, int T, int H, int ndir, const float* whh, const int* lengths,
+               float* out, float* hT, float* cT, float* work, void* stream) {
+  return guard([&] {
+    sd::lstm_recurrence(gx, B, T, H, ndir, whh, lengths, nullptr, nullptr, out, ndir * H, hT, cT,
+                        work, S(stream));
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// Shared helpers for the gfx950 diarization kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+namespace sd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Status codes (mirrored in include/sdiar.h).
+enum Status : int {
+  kOk = 0,
+  kErrInvalid = -1,   // ValueError in the reference (unknown type / bad argument)
+  kErrShape = -2,     // AssertionError in the reference (length mismatch)
+  kErrParam = -3,     // load_state_dict missing / unexpected key or wrong size
+  kErrHip = -4,       // HIP runtime failure
+  kErrState = -5,     // handle used before finalize / after destroy
+};
+
+void set_error(const std::string& msg);
+const char* last_error();
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define SD_HIP(expr)                                                              \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      throw ::sd::Error{::sd::kErrHip, std::string(#expr) + ": " + hipGetErrorString(_e)}; \
+    }                                                                             \
+  } while (0)
+
+#define SD_CHECK(cond, code, msg)                                                 \
+  do {                                                                            \
+    if (!(cond)) throw ::sd::Error{(code), (msg)};                                \
+  } while (0)
+
+#define SD_LAUNCH_CHECK() SD_HIP(hipGetLastError())
+
+__host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Round-to-nearest-even fp32 -> bf16 bits (finite inputs; NaN kept NaN by the
+// explicit check so a poisoned activation stays visible).
+__device__ __forceinline__ uint16_t f2bf_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float bf_bits2f(uint16_t b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+enum Act : int { kActNone = 0, kActRelu = 1, kActSigmoid = 2, kActSilu = 3 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case kActRelu: return fmaxf(v, 0.f);
+    case kActSigmoid: return 1.f / (1.f + expf(-v));
+    case kActSilu: return v / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+}  // namespace sd

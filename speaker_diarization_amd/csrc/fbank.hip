@@ -1,0 +1,136 @@
+// Kaldi-compatible log-mel filterbank on gfx950 (one wavefront per frame).
+//
+// Semantics follow torchaudio.compliance.kaldi.fbank as called from
+// ts_vad2/ts_vad_dataset.py:39-52 (FBank.__call__): waveform * 2^15, frames of
+// 400 samples every 160 (snip_edges=True), per-frame DC removal, pre-emphasis
+// 0.97 (first sample against itself), symmetric Hamming window, zero pad to 512,
+// |rFFT|^2, HTK-mel triangular banks (host-built, 80 x 257), log(max(e, FLT_EPS)).
+// dither is 0 here: the reference's default dither=1.0 adds fresh noise per
+// call, so parity is defined at dither 0.
+//
+// The whole meeting is framed once; windows (ts_vad_dataset.py:242-271) start
+// every 25 label frames = 400 fbank frames/s * k, so each window's frames are a
+// contiguous slice of the meeting's frames and window_cmn() only subtracts the
+// per-window mean.  That removes the 6x frame recomputation of overlapping
+// 6 s / 1 s-shift windows.
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kFrameLen = 400;
+constexpr int kShift = 160;
+constexpr int kNfft = 512;
+constexpr int kBins = kNfft / 2 + 1;
+constexpr int kFramesPerBlock = 4;
+
+__device__ __forceinline__ int bitrev9(int x) { return __brev((unsigned)x) >> (32 - 9); }
+
+__global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
+                                                    float in_scale, int n_frames,
+                                                    const float* __restrict__ mel_fb, int n_mels,
+                                                    const float2* __restrict__ twiddle,
+                                                    float* __restrict__ out) {
+  __shared__ float2 buf[kFramesPerBlock][kNfft];
+  __shared__ float pw[kFramesPerBlock][kBins + 3];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int f = blockIdx.x * kFramesPerBlock + w;
+  const bool active = f < n_frames;
+  const float* x = wav + (int64_t)(active ? f : 0) * kShift;
+
+  // Load, DC removal.
+  float v[7];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    int n = lane + i * 64;
+    int64_t gi = (int64_t)(active ? f : 0) * kShift + n;
+    v[i] = (n < kFrameLen && gi < n_samples) ? x[n] * in_scale : 0.f;
+    s += v[i];
+  }
+  s = warp_sum(s);
+  const float mean = s / (float)kFrameLen;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    int n = lane + i * 64;
+    if (n < kFrameLen) buf[w][n].x = v[i] - mean;   // scratch (real part)
+  }
+  __syncthreads();
+  // Pre-emphasis + Hamming, written bit-reversed for the DIT FFT.
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    int n = lane + i * 64;
+    float val = 0.f;
+    if (n < kFrameLen) {
+      float cur = buf[w][n].x;
+      float prev = n > 0 ? buf[w][n - 1].x : cur;
+      float win = 0.54f - 0.46f * cospif(2.f * (float)n / (float)(kFrameLen - 1));
+      val = (cur - 0.97f * prev) * win;
+    }
+    y[i] = val;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    int n = lane + i * 64;
+    buf[w][bitrev9(n)] = make_float2(y[i], 0.f);
+  }
+  __syncthreads();
+  // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
+  for (int half = 1; half < kNfft; half <<= 1) {
+    const int tstride = kNfft / (2 * half);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int bfly = lane + i * 64;
+      int grp = bfly / half, pos = bfly % half;
+      int i0 = grp * 2 * half + pos, i1 = i0 + half;
+      float2 tw = twiddle[pos * tstride];
+      float2 a = buf[w][i0], b = buf[w][i1];
+      float2 t = make_float2(b.x * tw.x - b.y * tw.y, b.x * tw.y + b.y * tw.x);
+      buf[w][i0] = make_float2(a.x + t.x, a.y + t.y);
+      buf[w][i1] = make_float2(a.x - t.x, a.y - t.y);
+    }
+    __syncthreads();
+  }
+  for (int k = lane; k < kBins; k += 64) {
+    float2 c = buf[w][k];
+    pw[w][k] = c.x * c.x + c.y * c.y;
+  }
+  __syncthreads();
+  if (!active) return;
+  const float eps = 1.1920928955078125e-07f;
+  for (int m = lane; m < n_mels; m += 64) {
+    const float* fr = mel_fb + (int64_t)m * kBins;
+    float acc = 0.f;
+    for (int k = 0; k < kBins; ++k) acc = fmaf(fr[k], pw[w][k], acc);
+    out[(int64_t)f * n_mels + m] = logf(fmaxf(acc, eps));
+  }
+}
+
+float2* g_twiddle = nullptr;
+
+}  // namespace
+
+void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
+                 const float* mel_fb, int n_mels, float* out, hipStream_t st) {
+  if (!g_twiddle) {
+    float2 h[kNfft / 2];
+    for (int k = 0; k < kNfft / 2; ++k) {
+      double ang = -2.0 * 3.14159265358979323846 * k / kNfft;
+      h[k] = make_float2((float)cos(ang), (float)sin(ang));
+    }
+    SD_HIP(hipMalloc(&g_twiddle, sizeof(h)));
+    SD_HIP(hipMemcpy(g_twiddle, h, sizeof(h), hipMemcpyHostToDevice));
+  }
+  if (n_frames <= 0) return;
+  ProfScope prof("fbank_kaldi", 0.0, 4.0 * ((double)n_frames * kShift + (double)n_frames * n_mels), st);
+  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(n_frames, kFramesPerBlock)), dim3(256), 0, st, wav,
+                     n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, out);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

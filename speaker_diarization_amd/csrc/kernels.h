@@ -1,0 +1,133 @@
+// Launchers for the gfx950 kernels (internal C++ API; the C-ABI is in capi.cpp).
+#pragma once
+#include <type_traits>
+#include "common.h"
+
+namespace sd {
+
+// ---------------------------------------------------------------- conv_gemm
+struct ConvGemmArgs {
+  // Input activation, channel-last: element (b, h, w, c) at
+  // A[((b*H + h)*W + w)*lda + a_coff + c].
+  const float* A = nullptr;
+  int B = 1, H = 1, W = 1, Cin = 0, lda = 0, a_coff = 0;
+  int Ho = 1, Wo = 1;
+  int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
+  // Packed weights Wt[N][K] (bf16 bits or fp32), K = kh*kw*Cin, tap-major.
+  const void* Wt = nullptr;
+  int N = 0, K = 0;
+  const float* pre_scale = nullptr;  // per input channel; a' = relu(a*s + h)
+  const float* pre_shift = nullptr;
+  const float* alpha = nullptr;      // per output channel scale
+  const float* beta = nullptr;       // per output channel shift
+  const float* res = nullptr;        // residual, res[m*res_ld + n]
+  int res_ld = 0;
+  int act = kActNone;
+  const float* gate = nullptr;       // gate[(b*gate_nseg + wo/gate_seg)*N + n]
+  int gate_seg = 1, gate_nseg = 1;
+  float* out = nullptr;              // out[b*o_sb + ho*o_sh + wo*o_sw + n*o_sn]
+  int64_t o_sb = 0, o_sh = 0, o_sw = 0, o_sn = 1;
+};
+void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
+
+// Plain row-major linear layer helper: out[m*ldo + o_coff + n] = act(A[m*lda+k]·W[n][k] * alpha + beta (+res)).
+ConvGemmArgs linear_args(const float* A, int M, int K, int lda, const void* Wt, int N,
+                         float* out, int ldo);
+
+// ---------------------------------------------------------------- fcm / cam++
+// First FCM conv (Cin = 1, 3x3, pad 1) + folded BN + ReLU.  fbank (B, T, F) ->
+// NHWC (B, F, T, 32).  cam_pplus_wespeaker.py:277-301.
+void fcm_conv1(const float* fbank, int B, int T, int F, const float* w /*32x9*/,
+               const float* alpha, const float* beta, float* out, hipStream_t st);
+
+// CAMLayer context gate (cam_pplus_wespeaker.py:106-123):
+// ctx[b,s,c] = mean_t x[b,t,c] + mean_{t in seg s} x[b,t,c];
+// gate[b,s,:] = sigmoid(W2·relu(W1·ctx + b1) + b2).
+void cam_context(const float* x, int B, int T, int C, int ldx, int seg_len,
+                 const float* w1, const float* b1, int C1, const float* w2, const float* b2,
+                 int C2, float* gate, hipStream_t st);
+
+// ---------------------------------------------------------------- norms
+// y = LN(x) * g + b over the last dim D; rows of x at stride ldx, y at ldy.
+void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
+               float eps, float* y, int ldy, hipStream_t st);
+
+// ---------------------------------------------------------------- attention
+// Multi-head self-attention core on a packed in-projection output.
+// qkv: (S*T, 3*D) row-major (q | k | v), heads of size hd = D/nh.
+// out: (S*T, ldo) at column h*hd.  Optional causal mask (key > query + delay is
+// masked) and per-sequence key lengths (keys >= len[s] masked).
+struct AttnArgs {
+  const float* qkv = nullptr;
+  int S = 0, T = 0, D = 0, nh = 0;
+  int ld_qkv = 0;
+  float* out = nullptr;
+  int ldo = 0;
+  float scale = 1.f;
+  int causal = 0, causal_delay = 0;
+  const int* key_len = nullptr;
+};
+void attention(const AttnArgs& a, bool bf16, hipStream_t st);
+
+// ---------------------------------------------------------------- ts-vad glue
+// rows (b, spk, t) of a (B*NS*T, 2E) buffer: [ts[b,spk,:] | mix[b,t,:]] (+ pe[t]).
+// mix rows t >= Tmix read as zeros (the pad of model.py:703-710 / :852-854).
+// model.py:862-877 (ts_embeds repeat + cat) and :876 PositionalEncoding.
+void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
+                         int T, int E, const float* pe, float* out, hipStream_t st);
+
+// x[r, :] += pe[r % T, :]  (rows of length D at stride ld)
+void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st);
+
+// Per-frame mean/std over channels then Linear(2 -> E): model.py:689-696.
+void gsp_fc(const float* x, int rows, int C, int ldx, const float* w /*E x 2*/,
+            const float* bias, int E, float* out, int ldo, hipStream_t st);
+
+// (B*NS, T, E) speaker-major rows -> (B, T, NS*E) channel-concatenated rows.
+void speakers_to_channels(const float* x, int B, int NS, int T, int E, float* out,
+                          hipStream_t st);
+
+// ---------------------------------------------------------------- conformer conv module
+// GLU over channel pairs (a = x[:, c], g = x[:, C + c]) followed by a depthwise
+// conv over time (kernel k, pad (k-1)/2, with bias).  x: (S, T, 2C); y: (S, T, C).
+// Also writes per (sequence, channel-block) partial sums for GroupNorm(1, C).
+void glu_dwconv(const float* x, int S, int T, int C, const float* w /*C x k*/,
+                const float* bias, int k, float* y, float* partial /*S x nblk x 2*/,
+                hipStream_t st);
+// GroupNorm(num_groups=1) over (T, C) of each sequence, affine, then SiLU (in place).
+void groupnorm_silu(float* y, int S, int T, int C, const float* partial, const float* g,
+                    const float* b, float eps, hipStream_t st);
+
+// ---------------------------------------------------------------- lstm
+// One bidirectional (or unidirectional) LSTM layer recurrence given the
+// precomputed input projections gx (B, T, ndir*4H) (bias_ih + bias_hh folded in).
+// whh: (ndir, 4H, H) fp32.  out: (B, T, ldo) at column dir*H.
+// h0/c0 optional (ndir, B, H); hT/cT optional outputs (ndir, B, H).
+void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
+                     const int* lengths, const float* h0, const float* c0, float* out, int ldo,
+                     float* hT, float* cT, float* work, hipStream_t st);
+
+// ---------------------------------------------------------------- frontend
+// Kaldi fbank (torchaudio.compliance.kaldi.fbank semantics used by
+// ts_vad_dataset.py:39-52): 25 ms / 10 ms frames, snip_edges, DC removal,
+// pre-emphasis 0.97, hamming, 512-point power spectrum, HTK mel, log(max(.,eps)).
+void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
+                 const float* mel_fb /*n_mels x 257*/, int n_mels, float* out,
+                 hipStream_t st);
+
+// Per-window CMN + zero pad: out[w, j, :] = feats[start_w + j, :] - mean_w for j < n_w,
+// 0 for n_w <= j < T_out (ts_vad_dataset.py:55 + collater padding :676).
+void window_cmn(const float* feats, int n_mels, const int* win_start, const int* win_n,
+                int n_win, int T_out, float* out, hipStream_t st);
+
+}  // namespace sd
+
+namespace sd {
+// Device-side weight packing (test ops): torch (N, Cin, taps) -> conv_gemm layout.
+void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16, hipStream_t st);
+}  // namespace sd
+
+namespace sd {
+void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
+                     int dis, int chunk, int n_frames, float* out, hipStream_t st);
+}  // namespace sd

@@ -1,0 +1,491 @@
+// Small fused kernels around the GEMMs: FCM stem, CAMLayer context gate,
+// LayerNorm, GroupNorm+SiLU, GLU+depthwise conv, GSP, layout glue.
+// HBM-bound; written for coalesced 64-lane access, no MFMA.
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+
+ConvGemmArgs linear_args(const float* A, int M, int K, int lda, const void* Wt, int N,
+                         float* out, int ldo) {
+  ConvGemmArgs p;
+  p.A = A; p.B = 1; p.H = 1; p.W = M; p.Cin = K; p.lda = lda; p.a_coff = 0;
+  p.Ho = 1; p.Wo = M;
+  p.Wt = Wt; p.N = N; p.K = K;
+  p.out = out; p.o_sb = 0; p.o_sh = 0; p.o_sw = ldo; p.o_sn = 1;
+  return p;
+}
+
+// ------------------------------------------------------------------ FCM stem
+__global__ __launch_bounds__(256) void fcm_conv1_kernel(const float* __restrict__ fb, int B, int T,
+                                                        int F, const float* __restrict__ w,
+                                                        const float* __restrict__ alpha,
+                                                        const float* __restrict__ beta,
+                                                        float* __restrict__ out) {
+  __shared__ float ws[32 * 9];
+  __shared__ float al[32], be[32];
+  for (int i = threadIdx.x; i < 32 * 9; i += blockDim.x) ws[i] = w[i];
+  if (threadIdx.x < 32) { al[threadIdx.x] = alpha[threadIdx.x]; be[threadIdx.x] = beta[threadIdx.x]; }
+  __syncthreads();
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)B * F * T;
+  if (idx >= total) return;
+  int t = idx % T;
+  int64_t r = idx / T;
+  int f = r % F;
+  int b = r / F;
+  float x[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      int ff = f + i - 1, tt = t + j - 1;
+      x[i * 3 + j] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? fb[((int64_t)b * T + tt) * F + ff] : 0.f;
+    }
+  float4* o = reinterpret_cast<float4*>(out + idx * 32);
+#pragma unroll
+  for (int c4 = 0; c4 < 8; ++c4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int c = c4 * 4 + u;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc = fmaf(ws[c * 9 + k], x[k], acc);
+      v[u] = fmaxf(acc * al[c] + be[c], 0.f);
+    }
+    o[c4] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+void fcm_conv1(const float* fbank, int B, int T, int F, const float* w, const float* alpha,
+               const float* beta, float* out, hipStream_t st) {
+  int64_t total = (int64_t)B * F * T;
+  ProfScope prof("fcm_conv1", 2.0 * total * 32 * 9, 4.0 * total * 33, st);
+  hipLaunchKernelGGL(fcm_conv1_kernel, dim3((unsigned)cdiv((int)total, 256)), dim3(256), 0, st,
+                     fbank, B, T, F, w, alpha, beta, out);
+  SD_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ CAM context
+constexpr int kMaxSeg = 32;
+
+__global__ __launch_bounds__(256) void cam_context_kernel(
+    const float* __restrict__ x, int T, int C, int ldx, int seg_len,
+    const float* __restrict__ w1, const float* __restrict__ b1, int C1,
+    const float* __restrict__ w2, const float* __restrict__ b2, int C2, float* __restrict__ gate) {
+  extern __shared__ float sm[];
+  const int b = blockIdx.x;
+  const int nseg = (T + seg_len - 1) / seg_len;
+  const int parts = blockDim.x / C;
+  float* psum = sm;                       // [parts][nseg][C]
+  float* ctx = psum + parts * nseg * C;   // [nseg][C]
+  float* h1 = ctx + nseg * C;             // [nseg][C1]
+  const int c = threadIdx.x % C;
+  const int part = threadIdx.x / C;
+  const float* xb = x + (int64_t)b * T * ldx;
+  if (part < parts) {
+    for (int s = 0; s < nseg; ++s) {
+      float acc = 0.f;
+      int t1 = min(T, (s + 1) * seg_len);
+      for (int t = s * seg_len + part; t < t1; t += parts) acc += xb[(int64_t)t * ldx + c];
+      psum[(part * nseg + s) * C + c] = acc;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    float tot = 0.f;
+    for (int s = 0; s < nseg; ++s) {
+      float ss = 0.f;
+      for (int q = 0; q < parts; ++q) ss += psum[(q * nseg + s) * C + threadIdx.x];
+      ctx[s * C + threadIdx.x] = ss;
+      tot += ss;
+    }
+    float mean = tot / (float)T;
+    for (int s = 0; s < nseg; ++s) {
+      int cnt = min(T, (s + 1) * seg_len) - s * seg_len;
+      ctx[s * C + threadIdx.x] = mean + ctx[s * C + threadIdx.x] / (float)cnt;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nseg * C1; i += blockDim.x) {
+    int s = i / C1, j = i % C1;
+    float acc = b1[j];
+    const float* wr = w1 + (int64_t)j * C;
+    for (int k = 0; k < C; ++k) acc = fmaf(wr[k], ctx[s * C + k], acc);
+    h1[i] = fmaxf(acc, 0.f);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nseg * C2; i += blockDim.x) {
+    int s = i / C2, o = i % C2;
+    float acc = b2[o];
+    const float* wr = w2 + (int64_t)o * C1;
+    for (int k = 0; k < C1; ++k) acc = fmaf(wr[k], h1[s * C1 + k], acc);
+    gate[((int64_t)b * nseg + s) * C2 + o] = 1.f / (1.f + expf(-acc));
+  }
+}
+
+void cam_context(const float* x, int B, int T, int C, int ldx, int seg_len, const float* w1,
+                 const float* b1, int C1, const float* w2, const float* b2, int C2, float* gate,
+                 hipStream_t st) {
+  SD_CHECK(C <= 256 && 256 % C == 0, kErrInvalid, "cam_context: C must divide 256");
+  int nseg = cdiv(T, seg_len);
+  SD_CHECK(nseg <= kMaxSeg, kErrInvalid, "cam_context: too many segments");
+  size_t smem = sizeof(float) * ((256 / C) * nseg * C + nseg * C + nseg * C1);
+  ProfScope prof("cam_context", 2.0 * B * nseg * (C * C1 + C1 * C2), 4.0 * B * T * C, st);
+  hipLaunchKernelGGL(cam_context_kernel, dim3(B), dim3(256), smem, st, x, T, C, ldx, seg_len, w1,
+                     b1, C1, w2, b2, C2, gate);
+  SD_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ LayerNorm
+template <int PER>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows, int D,
+                                                        int ldx, const float* __restrict__ g,
+                                                        const float* __restrict__ bb, float eps,
+                                                        float* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    v[i] = c < D ? xr[c] : 0.f;
+    s += v[i];
+  }
+  s = warp_sum(s);
+  const float mean = s / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    float d = c < D ? v[i] - mean : 0.f;
+    q += d * d;
+  }
+  q = warp_sum(q);
+  const float rstd = rsqrtf(q / (float)D + eps);
+  float* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    if (c < D) yr[c] = (v[i] - mean) * rstd * g[c] + bb[c];
+  }
+}
+
+void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
+               float eps, float* y, int ldy, hipStream_t st) {
+  dim3 grid(cdiv(rows, 4));
+  ProfScope prof("layernorm", 0.0, 8.0 * rows * D, st);
+  if (D <= 256)
+    hipLaunchKernelGGL((layernorm_kernel<4>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
+  else if (D <= 512)
+    hipLaunchKernelGGL((layernorm_kernel<8>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
+  else if (D <= 1024)
+    hipLaunchKernelGGL((layernorm_kernel<16>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
+  else
+    SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");
+  SD_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ TS-VAD glue
+__global__ void build_speaker_input_kernel(const float* __restrict__ ts, const float* __restrict__ mix,
+                                           int ldmix, int Tmix, int B, int NS, int T, int E,
+                                           const float* __restrict__ pe, float* __restrict__ out) {
+  const int row = blockIdx.x;  // (b, spk, t)
+  const int t = row % T;
+  const int bs = row / T;
+  const int b = bs / NS;
+  float* o = out + (int64_t)row * 2 * E;
+  const float* ts_r = ts + (int64_t)bs * E;
+  const bool mv = t < Tmix;
+  const float* mx = mix + ((int64_t)b * Tmix + (mv ? t : 0)) * ldmix;
+  const float* pr = pe ? pe + (int64_t)t * 2 * E : nullptr;
+  for (int c = threadIdx.x; c < 2 * E; c += blockDim.x) {
+    float v = c < E ? ts_r[c] : (mv ? mx[c - E] : 0.f);
+    if (pr) v += pr[c];
+    o[c] = v;
+  }
+}
+
+void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
+                         int T, int E, const float* pe, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(build_speaker_input_kernel, dim3(B * NS * T), dim3(128), 0, st, ts, mix,
+                     ldmix, Tmix, B, NS, T, E, pe, out);
+  SD_LAUNCH_CHECK();
+}
+
+__global__ void add_pe_kernel(float* __restrict__ x, int rows, int T, int D, int ld,
+                              const float* __restrict__ pe) {
+  const int row = blockIdx.x;
+  const int t = row % T;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) x[(int64_t)row * ld + c] += pe[(int64_t)t * D + c];
+}
+
+void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st) {
+  hipLaunchKernelGGL(add_pe_kernel, dim3(rows), dim3(128), 0, st, x, rows, T, D, ld, pe);
+  SD_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(256) void gsp_fc_kernel(const float* __restrict__ x, int rows, int C,
+                                                     int ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, int E,
+                                                     float* __restrict__ out, int ldo) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c];
+  s = warp_sum(s);
+  const float mean = s / (float)C;
+  float q = 0.f;
+  for (int c = lane; c < C; c += 64) { float d = xr[c] - mean; q += d * d; }
+  q = warp_sum(q);
+  const float sd = sqrtf(q / (float)(C - 1));   // torch.std default: unbiased
+  float* o = out + (int64_t)row * ldo;
+  for (int e = lane; e < E; e += 64) o[e] = fmaf(w[e * 2], mean, fmaf(w[e * 2 + 1], sd, bias[e]));
+}
+
+void gsp_fc(const float* x, int rows, int C, int ldx, const float* w, const float* bias, int E,
+            float* out, int ldo, hipStream_t st) {
+  hipLaunchKernelGGL(gsp_fc_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, C, ldx, w, bias,
+                     E, out, ldo);
+  SD_LAUNCH_CHECK();
+}
+
+__global__ void speakers_to_channels_kernel(const float* __restrict__ x, int B, int NS, int T, int E,
+                                            float* __restrict__ out) {
+  const int row = blockIdx.x;  // (b, t)
+  const int t = row % T;
+  const int b = row / T;
+  float* o = out + (int64_t)row * NS * E;
+  for (int c = threadIdx.x; c < NS * E; c += blockDim.x) {
+    int spk = c / E, e = c % E;
+    o[c] = x[(((int64_t)b * NS + spk) * T + t) * E + e];
+  }
+}
+
+void speakers_to_channels(const float* x, int B, int NS, int T, int E, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(speakers_to_channels_kernel, dim3(B * T), dim3(256), 0, st, x, B, NS, T, E, out);
+  SD_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ conformer conv module
+constexpr int kDwCB = 64;    // channels per block
+constexpr int kDwTT = 64;    // time tile
+
+__global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict__ x, int T, int C,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int k,
+                                                         float* __restrict__ y,
+                                                         float* __restrict__ partial) {
+  extern __shared__ float sm[];
+  const int pad = (k - 1) / 2;
+  const int s = blockIdx.y;
+  const int c0 = blockIdx.x * kDwCB;
+  const int nblk = gridDim.x;
+  float* g = sm;                          // [(kDwTT + k - 1)][kDwCB]
+  float* wsm = g + (kDwTT + k - 1) * kDwCB;  // [kDwCB][k]
+  __shared__ float red[2][256];
+  for (int i = threadIdx.x; i < kDwCB * k; i += blockDim.x) {
+    int cc = i / k, j = i % k;
+    wsm[i] = (c0 + cc < C) ? w[(int64_t)(c0 + cc) * k + j] : 0.f;
+  }
+  const float* xs = x + (int64_t)s * T * 2 * C;
+  float* ys = y + (int64_t)s * T * C;
+  float lsum = 0.f, lsq = 0.f;
+  const int cc = threadIdx.x % kDwCB;
+  const int tq = threadIdx.x / kDwCB;   // 0..3
+  for (int t0 = 0; t0 < T; t0 += kDwTT) {
+    __syncthreads();
+    const int span = kDwTT + k - 1;
+    for (int i = threadIdx.x; i < span * kDwCB; i += blockDim.x) {
+      int tt = i / kDwCB, c = i % kDwCB;
+      int t = t0 - pad + tt;
+      float v = 0.f;
+      if (t >= 0 && t < T && c0 + c < C) {
+        float a = xs[(int64_t)t * 2 * C + c0 + c];
+        float gg = xs[(int64_t)t * 2 * C + C + c0 + c];
+        v = a / (1.f + expf(-gg));
+      }
+      g[i] = v;
+    }
+    __syncthreads();
+    if (c0 + cc < C) {
+      const float bv = bias ? bias[c0 + cc] : 0.f;
+      for (int tt = tq; tt < kDwTT && t0 + tt < T; tt += 4) {
+        float acc = bv;
+        for (int j = 0; j < k; ++j) acc = fmaf(wsm[cc * k + j], g[(tt + j) * kDwCB + cc], acc);
+        ys[(int64_t)(t0 + tt) * C + c0 + cc] = acc;
+        lsum += acc;
+        lsq += acc * acc;
+      }
+    }
+  }
+  red[0][threadIdx.x] = lsum;
+  red[1][threadIdx.x] = lsq;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 0] = red[0][0];
+    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 1] = red[1][0];
+  }
+}
+
+void glu_dwconv(const float* x, int S, int T, int C, const float* w, const float* bias, int k,
+                float* y, float* partial, hipStream_t st) {
+  dim3 grid(cdiv(C, kDwCB), S);
+  size_t smem = sizeof(float) * ((kDwTT + k - 1) * kDwCB + kDwCB * k);
+  ProfScope prof("glu_dwconv", 2.0 * S * T * C * k, 4.0 * S * T * 3.0 * C, st);
+  hipLaunchKernelGGL(glu_dwconv_kernel, grid, dim3(256), smem, st, x, T, C, w, bias, k, y, partial);
+  SD_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(256) void groupnorm_silu_kernel(float* __restrict__ y, int T, int C,
+                                                             const float* __restrict__ partial, int nblk,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ b, float eps) {
+  const int s = blockIdx.y;
+  double sum = 0.0, sq = 0.0;
+  for (int i = 0; i < nblk; ++i) {
+    sum += partial[((int64_t)s * nblk + i) * 2];
+    sq += partial[((int64_t)s * nblk + i) * 2 + 1];
+  }
+  const double n = (double)T * C;
+  const double mean = sum / n;
+  double var = sq / n - mean * mean;
+  if (var < 0) var = 0;
+  const float fm = (float)mean;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  float* ys = y + (int64_t)s * T * C;
+  const int64_t total = (int64_t)T * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = i % C;
+    float v = (ys[i] - fm) * rstd * g[c] + b[c];
+    ys[i] = v / (1.f + expf(-v));
+  }
+}
+
+void groupnorm_silu(float* y, int S, int T, int C, const float* partial, const float* g,
+                    const float* b, float eps, hipStream_t st) {
+  int nblk = cdiv(C, kDwCB);
+  int per = cdiv(T * C, 256);
+  dim3 grid(min(per, 16), S);
+  ProfScope prof("groupnorm_silu", 0.0, 8.0 * S * T * C, st);
+  hipLaunchKernelGGL(groupnorm_silu_kernel, grid, dim3(256), 0, st, y, T, C, partial, nblk, g, b, eps);
+  SD_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ window CMN
+__global__ __launch_bounds__(256) void window_cmn_kernel(const float* __restrict__ feats, int n_mels,
+                                                         const int* __restrict__ win_start,
+                                                         const int* __restrict__ win_n, int T_out,
+                                                         float* __restrict__ out) {
+  __shared__ double part[4][128];
+  __shared__ float mean[128];
+  const int w = blockIdx.x;
+  const int start = win_start[w];
+  const int n = win_n[w];
+  const int c = threadIdx.x & 127;
+  const int q = threadIdx.x >> 7;   // 0..1
+  if (c < n_mels) {
+    double acc = 0.0;
+    for (int j = q; j < n; j += 2) acc += feats[((int64_t)start + j) * n_mels + c];
+    part[q][c] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < n_mels) mean[threadIdx.x] = (float)((part[0][threadIdx.x] + part[1][threadIdx.x]) / (double)n);
+  __syncthreads();
+  float* o = out + (int64_t)w * T_out * n_mels;
+  const int64_t total = (int64_t)T_out * n_mels;
+  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
+    int j = i / n_mels, cc = i % n_mels;
+    o[i] = j < n ? feats[((int64_t)start + j) * n_mels + cc] - mean[cc] : 0.f;
+  }
+}
+
+void window_cmn(const float* feats, int n_mels, const int* win_start, const int* win_n, int n_win,
+                int T_out, float* out, hipStream_t st) {
+  SD_CHECK(n_mels <= 128, kErrInvalid, "window_cmn: n_mels > 128");
+  hipLaunchKernelGGL(window_cmn_kernel, dim3(n_win), dim3(256), 0, st, feats, n_mels, win_start,
+                     win_n, T_out, out);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd
+
+namespace sd {
+
+// Torch conv/linear weight (N, Cin, taps) -> Wt[N][tap*Cin + c] (fp32 or bf16 bits).
+__global__ void pack_weight_kernel(const float* __restrict__ w, int N, int Cin, int taps,
+                                   void* __restrict__ out, int bf16) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)N * Cin * taps;
+  if (i >= total) return;
+  int tp = i % taps;
+  int64_t r = i / taps;
+  int c = r % Cin;
+  int n = r / Cin;
+  int64_t o = ((int64_t)n * taps + tp) * Cin + c;
+  if (bf16) reinterpret_cast<uint16_t*>(out)[o] = f2bf_bits(w[i]);
+  else reinterpret_cast<float*>(out)[o] = w[i];
+}
+
+void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16, hipStream_t st) {
+  int64_t total = (int64_t)N * Cin * taps;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w,
+                     N, Cin, taps, out, bf16 ? 1 : 0);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd
+
+namespace sd {
+
+// Overlap-average of window posteriors (ts_vad2/infer.py:90-94 np.mean over the
+// windows covering a frame, in window order) with the sigmoid of model.py:945-946
+// fused.  logits: (n_win, NS, Tw); window w covers label frames
+// [start_w, start_w + len_w).  out: (NS, n_frames); frames no window covers -> NaN.
+__global__ void overlap_average_kernel(const float* __restrict__ logits, int n_win, int NS, int Tw,
+                                       const int* __restrict__ start, const int* __restrict__ len,
+                                       int dis, int chunk, int n_frames, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)NS * n_frames) return;
+  const int t = i % n_frames;
+  const int spk = i / n_frames;
+  int w_lo = (t - chunk + 1 + dis - 1);
+  w_lo = w_lo > 0 ? w_lo / dis : 0;
+  int w_hi = min(n_win - 1, t / dis);
+  float acc = 0.f;
+  int cnt = 0;
+  for (int w = w_lo; w <= w_hi; ++w) {
+    int off = t - start[w];
+    if (off < 0 || off >= len[w]) continue;
+    float x = logits[((int64_t)w * NS + spk) * Tw + off];
+    acc += 1.f / (1.f + expf(-x));
+    ++cnt;
+  }
+  out[i] = cnt ? acc / (float)cnt : __int_as_float(0x7fc00000);
+}
+
+void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
+                     int dis, int chunk, int n_frames, float* out, hipStream_t st) {
+  int64_t total = (int64_t)NS * n_frames;
+  if (total == 0) return;
+  hipLaunchKernelGGL(overlap_average_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

@@ -1,0 +1,115 @@
+// Native TS-VAD inference runner (owns folded weights + workspace).
+#pragma once
+#include <vector>
+#include "kernels.h"
+#include "params.h"
+
+namespace sd {
+
+struct TsvadConfig {
+  int variant = 0;            // 0: CAM++ + transformer (model.py:758-897); 1: CAM++_ots_vad (669-756)
+  int max_num_speaker = 4;
+  int rs_len = 4;
+  int max_batch = 64;
+  int max_fbank_frames = 398;
+  bool bf16 = false;
+  int num_transformer_layer = 2;
+  int num_attention_head = 4;
+  int embed_dim = 384;
+  int ffn_dim = 1536;
+  int speaker_embed_dim = 192;
+  int conformer_layers = 6;
+  int conformer_heads = 8;
+  int conformer_ffn = 512;
+  int conformer_kernel = 31;
+  int lstm_hidden = 256;
+};
+
+struct ConvL {
+  PackedW w;
+  const float* alpha = nullptr;
+  const float* beta = nullptr;
+  const float* pre_s = nullptr;
+  const float* pre_h = nullptr;
+};
+
+struct DenseL {
+  ConvL bottleneck;       // nonlinear1 (prologue) -> linear1 (1x1) -> nonlinear2 (epilogue, relu)
+  ConvL local;            // cam_layer.linear_local (k3, dilation)
+  int dil = 1;
+  const float *c1w = nullptr, *c1b = nullptr, *c2w = nullptr, *c2b = nullptr;
+  int c1 = 0, c2 = 0;
+};
+
+struct TransformerL {     // nn.TransformerEncoderLayer, post-LN, ReLU FFN
+  PackedW in_proj, out_proj, l1, l2;
+  const float *in_b, *out_b, *b1, *b2, *n1g, *n1b, *n2g, *n2b;
+};
+
+struct ConformerL {       // torchaudio.models.conformer.ConformerLayer (conv after attention)
+  const float *f1_lng, *f1_lnb, *f1_b1, *f1_b2;
+  PackedW f1_w1, f1_w2;
+  const float *at_lng, *at_lnb, *in_b, *out_b;
+  PackedW in_proj, out_proj;
+  const float *cv_lng, *cv_lnb, *pw1_b, *dw_w, *dw_b, *gn_g, *gn_b, *pw2_b;
+  PackedW pw1, pw2;
+  const float *f2_lng, *f2_lnb, *f2_b1, *f2_b2;
+  PackedW f2_w1, f2_w2;
+  const float *fin_g, *fin_b;
+};
+
+class TsvadModel {
+ public:
+  explicit TsvadModel(const TsvadConfig& c) : cfg_(c) {}
+  ParamStore& params() { return ps_; }
+  void finalize();
+  // ref_speech (B, T_fb, 80) fbank, target_speech (B, NS, 192), logits out (B, NS, T_lab).
+  void forward(const float* ref_speech, const float* target_speech, int B, int T_fb, int T_lab,
+               float* logits, hipStream_t st);
+  bool finalized() const { return finalized_; }
+  size_t device_bytes() const { return arena_.total(); }
+
+ private:
+  ConvL conv_bn(const std::string& wname, const std::string& bn, const std::string& bias = "");
+  ConvL linear(const std::string& prefix, float mult = 1.f);
+  TransformerL transformer(const std::string& prefix);
+  ConformerL conformer(const std::string& prefix);
+  void run_transformer(const TransformerL& L, float* X, int S, int T, int nh, hipStream_t st);
+  void run_conformer(const ConformerL& L, float* X, int S, int T, hipStream_t st);
+  void alloc_workspace();
+  float* ws(size_t n) { return static_cast<float*>(arena_.alloc(n * sizeof(float))); }
+
+  TsvadConfig cfg_;
+  ParamStore ps_;
+  DeviceArena arena_;
+  bool finalized_ = false;
+
+  // CAM++
+  ConvL fcm_conv1_;  // fp32 3x3 Cin=1 weights (32x9) + folded bn
+  struct ResBlock { ConvL c1, c2, sc; bool has_sc; int stride; };
+  std::vector<ResBlock> fcm_blocks_;
+  ConvL fcm_conv2_;
+  ConvL tdnn_;
+  std::vector<std::vector<DenseL>> dense_;
+  std::vector<ConvL> transit_;
+  const float *out_nl_s_ = nullptr, *out_nl_h_ = nullptr;
+  ConvL down_;
+  const float *gsp_w_ = nullptr, *gsp_b_ = nullptr;
+  const float* pe_ = nullptr;
+  int pe_len_ = 0;
+  std::vector<TransformerL> single_, multi_;
+  ConvL backend_down_;
+  std::vector<ConformerL> conf_;
+  PackedW lstm_ih_;
+  const float *lstm_b_ = nullptr, *lstm_hh_ = nullptr;
+  ConvL fc_;
+
+  // Workspace.
+  float *fcmA_ = nullptr, *fcmB_ = nullptr, *fcmC_ = nullptr, *x0_ = nullptr;
+  float *d_[3] = {nullptr, nullptr, nullptr}, *x4_ = nullptr, *tmp_ = nullptr, *gate_ = nullptr;
+  float *mix_ = nullptr, *mixg_ = nullptr;
+  float *X_ = nullptr, *Y_ = nullptr, *QKV_ = nullptr, *AO_ = nullptr, *H_ = nullptr;
+  float *X2_ = nullptr, *partial_ = nullptr, *lstm_work_ = nullptr;
+};
+
+}  // namespace sd

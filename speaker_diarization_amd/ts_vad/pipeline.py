@@ -1,0 +1,105 @@
+"""Meeting-level TS-VAD inference on MI355X: wav in HBM -> per-speaker posteriors.
+
+Replaces the loop of ts_vad2/infer.py:216-285 (DataLoader of windows -> fbank on
+CPU -> model.infer -> res_dict) with: one fbank pass over the meeting (HIP) ->
+per-batch window CMN/pad (HIP) -> TSVADModel forward (HIP) -> window logits
+kept in HBM -> sigmoid + overlap average in window order (HIP).  Multi-GPU:
+windows are sharded by contiguous batch ranges (one process per GPU); the only
+exchange is an all-gather of the per-window logits (RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _lib
+from ..frontend import kaldi_fbank, window_cmn
+from .model import TSVADModel
+from .windows import WindowPlan, plan_windows, shard_batches
+
+
+class TSVADPipeline:
+    def __init__(self, model: TSVADModel, segment_shift: int = 1, batch_size: int = 64):
+        self.model = model
+        self.cfg = model.cfg
+        self.segment_shift = segment_shift
+        self.batch_size = min(batch_size, model.max_batch)
+
+    def plan(self, n_labels: int) -> WindowPlan:
+        return plan_windows(n_labels, self.cfg.rs_len, self.segment_shift, self.cfg.label_rate,
+                            self.cfg.sample_rate)
+
+    def window_logits(self, wav, ts, plan: WindowPlan, w0: int = 0, w1: int = None, out=None):
+        """Logits of windows [w0, w1) -> (w1-w0, NS, chunk) (cols >= window len unused).
+        wav: (n_samples,) CUDA float32 covering at least those windows' audio."""
+        import torch
+        dev = self.model.device
+        w1 = plan.n_win if w1 is None else w1
+        NS, chunk = self.model.max_num_speaker, plan.chunk
+        if out is None:
+            out = torch.zeros(w1 - w0, NS, chunk, device=dev, dtype=torch.float32)
+        if w1 <= w0:
+            return out
+        spl = plan.samples_per_label
+        s0 = int(plan.starts[w0]) * spl
+        s1 = min(wav.numel(), int(plan.ends[w1 - 1]) * spl)
+        feats = kaldi_fbank(wav[s0:s1])
+        f0 = int(plan.fbank_start[w0])
+        fstart = torch.from_numpy((plan.fbank_start[w0:w1] - f0).astype(np.int32)).to(dev)
+        fn = torch.from_numpy(plan.fbank_n[w0:w1].astype(np.int32)).to(dev)
+        ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
+        for b0 in range(w0, w1, self.batch_size):
+            b1 = min(w1, b0 + self.batch_size)
+            T_out = int(plan.fbank_n[b0:b1].max())
+            T_lab = int(plan.lens[b0:b1].max())
+            ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
+            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab)
+            out[b0 - w0:b1 - w0, :, :T_lab] = lg
+        return out
+
+    @staticmethod
+    def average(logits, plan: WindowPlan):
+        """(n_win, NS, chunk) logits -> (NS, n_labels) posteriors (sigmoid + overlap mean)."""
+        import torch
+        dev = logits.device
+        NS = logits.shape[1]
+        out = torch.empty(NS, plan.n_labels, device=dev, dtype=torch.float32)
+        st = torch.from_numpy(plan.starts.astype(np.int32)).to(dev)
+        ln = torch.from_numpy(plan.lens.astype(np.int32)).to(dev)
+        _lib.call("sd_overlap_average", _lib.ptr(logits.contiguous()), plan.n_win, NS, logits.shape[2],
+                  _lib.ptr(st), _lib.ptr(ln), plan.dis, plan.chunk, plan.n_labels, _lib.ptr(out),
+                  _lib.stream_ptr(dev))
+        return out
+
+    def posteriors(self, wav, ts, n_labels: int = None, group=None):
+        """wav: (n_samples,) CUDA float32 in [-1,1); ts: (NS, 192) target-speaker
+        embeddings (zeros for absent speakers, ts_vad_dataset.py:507-510).
+        Returns (NS, n_labels) frame posteriors at 25 Hz."""
+        import torch
+        import torch.distributed as dist
+        spl = self.cfg.sample_rate // self.cfg.label_rate
+        if n_labels is None:
+            n_labels = wav.numel() // spl
+        plan = self.plan(n_labels)
+        world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
+        if world == 1:
+            return self.average(self.window_logits(wav, ts, plan), plan)
+        rank = dist.get_rank(group)
+        w0, w1 = shard_batches(plan, self.batch_size, world, rank)
+        local = self.window_logits(wav, ts, plan, w0, w1)
+        logits = gather_windows(local, plan, self.batch_size, world, group)
+        return self.average(logits, plan)
+
+
+def gather_windows(local, plan: WindowPlan, batch_size: int, world: int, group=None):
+    """All-gather of per-rank window logits (RCCL over xGMI); re-assembled in
+    global window order from the deterministic shard table."""
+    import torch
+    import torch.distributed as dist
+    ranges = [shard_batches(plan, batch_size, world, r) for r in range(world)]
+    maxn = max(b - a for a, b in ranges)
+    pad = torch.zeros(maxn, *local.shape[1:], device=local.device, dtype=local.dtype)
+    pad[: local.shape[0]] = local
+    allg = torch.empty(world * maxn, *local.shape[1:], device=local.device, dtype=local.dtype)
+    dist.all_gather_into_tensor(allg, pad, group=group)
+    parts = [allg[r * maxn: r * maxn + (b - a)] for r, (a, b) in enumerate(ranges)]
+    return torch.cat(parts, 0)

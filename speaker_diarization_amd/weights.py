@@ -1,0 +1,278 @@
+"""State-dict layouts of the reference models and seeded synthetic weights.
+
+No trained checkpoints exist offline, so benchmarks and parity tests use
+seeded random weights laid out under the reference's exact key names (the
+golden-vector script loads them into the reference modules with strict=True,
+which pins the key set).  Checkpoint loading mirrors the reference loaders:
+TS-VAD `{"model": state_dict}` (ts_vad2/infer.py:184), EEND bare state_dict
+(eend_eda/infer_eda.py:88), FS-EEND Lightning `state_dict` with a `model.`
+prefix (fs_eend/train.py:183-191).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+Shape = Tuple[int, ...]
+
+
+# ----------------------------------------------------------------------------- TS-VAD
+@dataclass
+class TSVADConfig:
+    """Mirror of ts_vad2/model.py:40-110 (TSVADConfig) restricted to the fields
+    the inference path reads, plus TSVADDataConfig (build_datasets.py:10-82)
+    fields the model consumes."""
+    speech_encoder_type: str = "CAM++"
+    num_attention_head: int = 4
+    num_transformer_layer: int = 2
+    transformer_embed_dim: int = 384
+    transformer_ffn_embed_dim: int = 1536
+    speaker_embed_dim: int = 192
+    dropout: float = 0.1
+    single_backend_type: str = "transformer"
+    multi_backend_type: str = "transformer"
+    ots_vad_style: str = ""
+    # data config
+    rs_len: int = 4
+    segment_shift: int = 1
+    max_num_speaker: int = 4
+    label_rate: int = 25
+    sample_rate: int = 16000
+
+    @property
+    def variant(self) -> int:
+        if self.ots_vad_style == "v1":
+            if (self.speech_encoder_type, self.single_backend_type, self.multi_backend_type) != (
+                    "CAM++_ots_vad", "conformer_ots_vad", "lstm_ots_vad"):
+                raise ValueError("ots_vad_style v1 is built for CAM++_ots_vad + conformer_ots_vad + lstm_ots_vad")
+            return 1
+        if (self.speech_encoder_type, self.single_backend_type, self.multi_backend_type) != (
+                "CAM++", "transformer", "transformer"):
+            raise ValueError(
+                f"unsupported TS-VAD configuration {self.speech_encoder_type}/"
+                f"{self.single_backend_type}/{self.multi_backend_type} (MI355X backend builds CAM++ "
+                "with transformer or conformer_ots_vad/lstm_ots_vad)")
+        return 0
+
+    @staticmethod
+    def ots_vad_v1(**kw) -> "TSVADConfig":
+        """The C2 configuration (egs/alimeeting/run_ts_vad2.sh:8298-8356)."""
+        d = dict(speech_encoder_type="CAM++_ots_vad", single_backend_type="conformer_ots_vad",
+                 multi_backend_type="lstm_ots_vad", ots_vad_style="v1", rs_len=6)
+        d.update(kw)
+        return TSVADConfig(**d)
+
+
+def _bn(keys: list, prefix: str, c: int, affine: bool = True):
+    if affine:
+        keys.append((prefix + ".weight", (c,), "bn_w"))
+        keys.append((prefix + ".bias", (c,), "bn_b"))
+    keys.append((prefix + ".running_mean", (c,), "bn_m"))
+    keys.append((prefix + ".running_var", (c,), "bn_v"))
+    keys.append((prefix + ".num_batches_tracked", (), "nbt"))
+
+
+def campplus_layout(prefix: str = "speech_encoder.") -> list:
+    """Key layout of CAMPPlus(feat_dim=80, embedding_size=192)
+    (cam_pplus_wespeaker.py:311-386)."""
+    k: list = []
+    p = prefix + "head."
+    k.append((p + "conv1.weight", (32, 1, 3, 3), "conv2d"))
+    _bn(k, p + "bn1", 32)
+    for layer in (1, 2):
+        for blk in (0, 1):
+            q = f"{p}layer{layer}.{blk}."
+            k.append((q + "conv1.weight", (32, 32, 3, 3), "conv2d"))
+            _bn(k, q + "bn1", 32)
+            k.append((q + "conv2.weight", (32, 32, 3, 3), "conv2d"))
+            _bn(k, q + "bn2", 32)
+            if blk == 0:
+                k.append((q + "shortcut.0.weight", (32, 32, 1, 1), "conv2d"))
+                _bn(k, q + "shortcut.1", 32)
+    k.append((p + "conv2.weight", (32, 32, 3, 3), "conv2d"))
+    _bn(k, p + "bn2", 32)
+    x = prefix + "xvector."
+    k.append((x + "tdnn.linear.weight", (128, 320, 5), "kaiming"))
+    _bn(k, x + "tdnn.nonlinear.batchnorm", 128)
+    ch = 128
+    for b, n in enumerate((12, 24, 16)):
+        for i in range(n):
+            q = f"{x}block{b + 1}.tdnnd{i + 1}."
+            cin = ch + i * 32
+            _bn(k, q + "nonlinear1.batchnorm", cin)
+            k.append((q + "linear1.weight", (128, cin, 1), "kaiming"))
+            _bn(k, q + "nonlinear2.batchnorm", 128)
+            k.append((q + "cam_layer.linear_local.weight", (32, 128, 3), "kaiming"))
+            k.append((q + "cam_layer.linear1.weight", (64, 128, 1), "kaiming"))
+            k.append((q + "cam_layer.linear1.bias", (64,), "zero"))
+            k.append((q + "cam_layer.linear2.weight", (32, 64, 1), "kaiming"))
+            k.append((q + "cam_layer.linear2.bias", (32,), "zero"))
+        ch += n * 32
+        _bn(k, f"{x}transit{b + 1}.nonlinear.batchnorm", ch)
+        k.append((f"{x}transit{b + 1}.linear.weight", (ch // 2, ch, 1), "kaiming"))
+        ch //= 2
+    _bn(k, x + "out_nonlinear.batchnorm", ch)
+    k.append((x + "dense.linear.weight", (192, ch * 2, 1), "kaiming"))
+    _bn(k, x + "dense.nonlinear.batchnorm", 192, affine=False)
+    return k
+
+
+def _mha(k: list, p: str, e: int):
+    k.append((p + "in_proj_weight", (3 * e, e), "xavier"))
+    k.append((p + "in_proj_bias", (3 * e,), "small"))
+    k.append((p + "out_proj.weight", (e, e), "linear"))
+    k.append((p + "out_proj.bias", (e,), "small"))
+
+
+def _ln(k: list, p: str, e: int):
+    k.append((p + ".weight", (e,), "ln_w"))
+    k.append((p + ".bias", (e,), "small"))
+
+
+def tsvad_layout(cfg: TSVADConfig) -> list:
+    """Key layout of TSVADModel(cfg) (ts_vad2/model.py:179-367)."""
+    e, se, ns = cfg.transformer_embed_dim, cfg.speaker_embed_dim, cfg.max_num_speaker
+    k = campplus_layout()
+    if cfg.variant == 1:
+        k.append(("gsp_fc.weight", (se, 2), "linear"))
+        k.append(("gsp_fc.bias", (se,), "small"))
+    k.append(("speech_down_or_up.0.weight", (se, 512, 5), "conv1d"))
+    k.append(("speech_down_or_up.0.bias", (se,), "small"))
+    _bn(k, "speech_down_or_up.1.bn", se)
+    if cfg.variant == 0:
+        k.append(("pos_encoder.pe", (cfg.rs_len * cfg.label_rate, 1, e), "pe"))
+        for i in range(cfg.num_transformer_layer):
+            _tfm(k, f"single_backend.layers.{i}.", e, cfg.transformer_ffn_embed_dim)
+        k.append(("backend_down.0.weight", (e, e * ns, 5), "conv1d"))
+        k.append(("backend_down.0.bias", (e,), "small"))
+        _bn(k, "backend_down.1.bn", e)
+        for i in range(cfg.num_transformer_layer):
+            _tfm(k, f"multi_backend.layers.{i}.", e, cfg.transformer_ffn_embed_dim)
+        k.append(("fc.weight", (ns, e), "linear"))
+        k.append(("fc.bias", (ns,), "small"))
+    else:
+        for i in range(6):
+            p = f"single_backend.conformer_layers.{i}."
+            for f in ("ffn1", "ffn2"):
+                _ln(k, p + f + ".sequential.0", e)
+                k.append((p + f + ".sequential.1.weight", (512, e), "linear"))
+                k.append((p + f + ".sequential.1.bias", (512,), "small"))
+                k.append((p + f + ".sequential.4.weight", (e, 512), "linear"))
+                k.append((p + f + ".sequential.4.bias", (e,), "small"))
+                if f == "ffn1":
+                    _ln(k, p + "self_attn_layer_norm", e)
+                    _mha(k, p + "self_attn.", e)
+                    _ln(k, p + "conv_module.layer_norm", e)
+                    k.append((p + "conv_module.sequential.0.weight", (2 * e, e, 1), "conv1d"))
+                    k.append((p + "conv_module.sequential.0.bias", (2 * e,), "small"))
+                    k.append((p + "conv_module.sequential.2.weight", (e, 1, 31), "conv1d"))
+                    k.append((p + "conv_module.sequential.2.bias", (e,), "small"))
+                    k.append((p + "conv_module.sequential.3.weight", (e,), "ln_w"))
+                    k.append((p + "conv_module.sequential.3.bias", (e,), "small"))
+                    k.append((p + "conv_module.sequential.5.weight", (e, e, 1), "conv1d"))
+                    k.append((p + "conv_module.sequential.5.bias", (e,), "small"))
+            _ln(k, p + "final_layer_norm", e)
+        h = 256
+        for sfx in ("", "_reverse"):
+            k.append((f"multi_backend.weight_ih_l0{sfx}", (4 * h, ns * e), "lstm"))
+            k.append((f"multi_backend.weight_hh_l0{sfx}", (4 * h, h), "lstm"))
+            k.append((f"multi_backend.bias_ih_l0{sfx}", (4 * h,), "lstm"))
+            k.append((f"multi_backend.bias_hh_l0{sfx}", (4 * h,), "lstm"))
+        k.append(("fc.weight", (ns, 2 * h), "linear"))
+        k.append(("fc.bias", (ns,), "small"))
+    return k
+
+
+def _tfm(k: list, p: str, e: int, ffn: int):
+    _mha(k, p + "self_attn.", e)
+    k.append((p + "linear1.weight", (ffn, e), "linear"))
+    k.append((p + "linear1.bias", (ffn,), "small"))
+    k.append((p + "linear2.weight", (e, ffn), "linear"))
+    k.append((p + "linear2.bias", (e,), "small"))
+    _ln(k, p + "norm1", e)
+    _ln(k, p + "norm2", e)
+
+
+def sinusoid_pe(max_len: int, d: int) -> np.ndarray:
+    """PositionalEncoding.pe buffer (ts_vad2/model.py:137-150), shape (max_len, 1, d)."""
+    pos = np.arange(max_len, dtype=np.float32)[:, None]
+    div = np.exp(np.arange(0, d, 2, dtype=np.float32) * np.float32(-np.log(10000.0) / d)).astype(np.float32)
+    pe = np.zeros((max_len, 1, d), np.float32)
+    pe[:, 0, 0::2] = np.sin(pos * div)
+    pe[:, 0, 1::2] = np.cos(pos * div)
+    return pe
+
+
+def _init(rng: np.random.Generator, shape: Shape, kind: str) -> np.ndarray:
+    if kind == "nbt":
+        return np.array(0, dtype=np.int64)
+    n = int(np.prod(shape)) if shape else 1
+    fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else max(shape[0], 1)
+    if kind == "conv2d":
+        b = 1.0 / np.sqrt(fan_in)
+        v = rng.uniform(-b, b, n)
+    elif kind in ("kaiming", "conv1d"):
+        v = rng.standard_normal(n) * np.sqrt(2.0 / fan_in)
+        if kind == "conv1d":
+            v *= 0.5
+    elif kind == "linear":
+        b = 1.0 / np.sqrt(fan_in)
+        v = rng.uniform(-b, b, n)
+    elif kind == "xavier":
+        b = np.sqrt(6.0 / (shape[0] / 3 + shape[1]))
+        v = rng.uniform(-b, b, n)
+    elif kind == "lstm":
+        b = 1.0 / np.sqrt(256)
+        v = rng.uniform(-b, b, n)
+    elif kind == "bn_w":
+        v = rng.uniform(0.8, 1.2, n)
+    elif kind in ("bn_b", "small"):
+        v = rng.standard_normal(n) * 0.05
+    elif kind == "bn_m":
+        v = rng.standard_normal(n) * 0.1
+    elif kind == "bn_v":
+        v = rng.uniform(0.6, 1.4, n)
+    elif kind == "ln_w":
+        v = 1.0 + rng.standard_normal(n) * 0.05
+    elif kind == "zero":
+        v = np.zeros(n)
+    else:
+        raise ValueError(kind)
+    return v.astype(np.float32).reshape(shape)
+
+
+def synthetic_state_dict(layout: list, seed: int = 777, extras: Dict[str, np.ndarray] | None = None
+                         ) -> "OrderedDict[str, np.ndarray]":
+    """Seeded random weights (numpy PCG64: identical on every host)."""
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for name, shape, kind in layout:
+        if kind == "pe":
+            sd[name] = sinusoid_pe(shape[0], shape[2])
+        else:
+            sd[name] = _init(rng, shape, kind)
+    if extras:
+        sd.update(extras)
+    return sd
+
+
+def tsvad_state_dict(cfg: TSVADConfig, seed: int = 777):
+    return synthetic_state_dict(tsvad_layout(cfg), seed)
+
+
+def to_torch(sd):
+    import torch
+    return OrderedDict((k, torch.from_numpy(np.ascontiguousarray(v))) for k, v in sd.items())
+
+
+def unwrap_checkpoint(obj, kind: str = "tsvad"):
+    """Accept the reference's three on-disk layouts and return a flat state_dict."""
+    if isinstance(obj, dict) and "model" in obj and isinstance(obj["model"], dict):
+        return obj["model"]
+    if isinstance(obj, dict) and "state_dict" in obj:
+        sd = obj["state_dict"]
+        return OrderedDict((k[len("model."):] if k.startswith("model.") else k, v) for k, v in sd.items())
+    return obj

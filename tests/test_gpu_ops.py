@@ -1,0 +1,230 @@
+"""Kernel-level parity through the C ABI vs torch-CPU fp32 references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from speaker_diarization_amd import _lib, frontend
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = dict(atol=1e-4, rtol=1e-4)
+BF16_TOL = dict(atol=3e-2, rtol=3e-2)
+
+
+def _tol(precision):
+    return FP32_TOL if precision == 0 else BF16_TOL
+
+
+def _rel_err(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("M,K,N,act", [(1, 32, 4, 0), (257, 384, 1152, 0), (1000, 1536, 384, 1),
+                                       (64, 512, 4, 0), (333, 96, 130, 3), (4096, 256, 2048, 2)])
+def test_linear(gpu, precision, M, K, N, act):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g) * 0.1
+    ref = F.linear(x, w, b)
+    ref = [ref, F.relu(ref), torch.sigmoid(ref), F.silu(ref)][act]
+    out = torch.empty(M, N, device=gpu)
+    xd, wd, bd = x.to(gpu), w.to(gpu), b.to(gpu)
+    _lib.call("sd_op_linear", xd.data_ptr(), M, K, wd.data_ptr(), bd.data_ptr(), N, act, out.data_ptr(),
+              precision, _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("B,T,Cin,Cout,k,stride,pad,dil", [
+    (2, 299, 128, 32, 3, 1, 2, 2),     # CAM dense k3 dilation 2
+    (3, 598, 320, 128, 5, 2, 2, 1),    # TDNN
+    (2, 299, 512, 192, 5, 2, 2, 1),    # speech_down_or_up
+    (2, 100, 1536, 384, 5, 1, 2, 1),   # backend_down
+    (1, 7, 64, 40, 1, 1, 0, 1),
+])
+def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
+    g = torch.Generator().manual_seed(B * T + Cout)
+    x = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(Cout, Cin, k, generator=g) / math.sqrt(Cin * k)
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv1d(x, w, b, stride=stride, padding=pad, dilation=dil).permute(0, 2, 1)
+    xd = x.permute(0, 2, 1).contiguous().to(gpu)
+    out = torch.empty(ref.shape, device=gpu)
+    _lib.call("sd_op_conv1d", xd.data_ptr(), B, T, Cin, w.to(gpu).data_ptr(), b.to(gpu).data_ptr(), Cout, k,
+              stride, pad, dil, 0, out.data_ptr(), precision, _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("B,H,W,sh,kh,pad", [(2, 80, 50, 2, 3, 1), (1, 40, 37, 1, 3, 1), (2, 40, 21, 2, 1, 0),
+                                             (2, 20, 33, 2, 3, 1)])
+def test_conv2d(gpu, precision, B, H, W, sh, kh, pad):
+    g = torch.Generator().manual_seed(H * W)
+    x = torch.randn(B, 32, H, W, generator=g)
+    w = torch.randn(32, 32, kh, kh, generator=g) / math.sqrt(32 * kh * kh)
+    ref = F.conv2d(x, w, stride=(sh, 1), padding=pad).permute(0, 2, 3, 1)
+    out = torch.empty(ref.shape, device=gpu)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    _lib.call("sd_op_conv2d", xd.data_ptr(), B, H, W, 32, w.to(gpu).data_ptr(), 32, kh, kh, sh, 1, pad, pad,
+              out.data_ptr(), precision, _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 1e-2
+
+
+def _attn_ref(qkv, S, T, D, nh, causal=0, delay=0, key_len=None):
+    hd = D // nh
+    q, k, v = qkv.view(S, T, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / math.sqrt(hd)
+    if causal:
+        m = torch.ones(T, T).triu(1 + delay).bool()
+        s = s.masked_fill(m, float("-inf"))
+    if key_len is not None:
+        km = torch.arange(T)[None, :] >= key_len[:, None]
+        s = s.masked_fill(km[:, None, None, :], float("-inf"))
+    return (torch.softmax(s, -1) @ v).permute(0, 2, 1, 3).reshape(S * T, D)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("S,T,D,nh,causal", [(8, 100, 384, 4, 0), (6, 150, 384, 8, 0), (1, 777, 256, 4, 0),
+                                             (2, 300, 256, 4, 1), (3, 33, 512, 4, 0)])
+def test_attention(gpu, precision, S, T, D, nh, causal):
+    g = torch.Generator().manual_seed(S * T)
+    qkv = torch.randn(S * T, 3 * D, generator=g)
+    ref = _attn_ref(qkv, S, T, D, nh, causal)
+    out = torch.empty(S * T, D, device=gpu)
+    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, causal, 0, None, out.data_ptr(), precision,
+              _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 2e-2
+
+
+def test_attention_key_len(gpu):
+    S, T, D, nh = 3, 70, 384, 8
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(S * T, 3 * D, generator=g)
+    kl = torch.tensor([70, 41, 1], dtype=torch.int32)
+    ref = _attn_ref(qkv, S, T, D, nh, key_len=kl)
+    out = torch.empty(S * T, D, device=gpu)
+    kld = kl.to(gpu)
+    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, 0, 0, kld.data_ptr(), out.data_ptr(), 0,
+              _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+
+
+def test_attention_large_logits(gpu):
+    """Online-softmax rescale path: a key tile far later in the sequence dominates."""
+    S, T, D, nh = 1, 200, 256, 4
+    g = torch.Generator().manual_seed(9)
+    qkv = torch.randn(S * T, 3 * D, generator=g)
+    qkv[150, D:2 * D] *= 30.0     # spike one key
+    ref = _attn_ref(qkv, S, T, D, nh)
+    out = torch.empty(S * T, D, device=gpu)
+    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, 0, 0, None, out.data_ptr(), 0,
+              _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-4, rtol=2e-4)
+
+
+@pytest.mark.parametrize("rows,D", [(1000, 384), (7, 256), (65, 1000)])
+def test_layernorm(gpu, rows, D):
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, D, generator=g) * 3 + 1
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    ref = F.layer_norm(x, (D,), w, b, 1e-5)
+    out = torch.empty(rows, D, device=gpu)
+    _lib.call("sd_op_layernorm", x.to(gpu).data_ptr(), rows, D, w.to(gpu).data_ptr(), b.to(gpu).data_ptr(), 1e-5,
+              out.data_ptr(), _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+
+
+@pytest.mark.parametrize("B,T,H,ndir,lengths", [(64, 150, 256, 2, None), (1, 300, 256, 1, None),
+                                                (5, 40, 256, 2, [40, 17, 1, 33, 40])])
+def test_lstm(gpu, B, T, H, ndir, lengths):
+    from oracle.tsvad_ref import lstm
+    g = torch.Generator().manual_seed(B + T)
+    I = 64
+    x = torch.randn(B, T, I, generator=g)
+    sd = {}
+    for d, sfx in enumerate(("", "_reverse")[:ndir]):
+        sd[f"l.weight_ih_l0{sfx}"] = torch.randn(4 * H, I, generator=g) / 16
+        sd[f"l.weight_hh_l0{sfx}"] = torch.randn(4 * H, H, generator=g) / 16
+        sd[f"l.bias_ih_l0{sfx}"] = torch.randn(4 * H, generator=g) * 0.1
+        sd[f"l.bias_hh_l0{sfx}"] = torch.randn(4 * H, generator=g) * 0.1
+    ref, (hn, cn) = lstm(x, sd, "l.", bidirectional=ndir == 2, lengths=lengths)
+    sfxs = ("", "_reverse")[:ndir]
+    gx = torch.cat([F.linear(x, sd[f"l.weight_ih_l0{s}"], sd[f"l.bias_ih_l0{s}"] + sd[f"l.bias_hh_l0{s}"])
+                    for s in sfxs], -1).contiguous()
+    whh = torch.stack([sd[f"l.weight_hh_l0{s}"] for s in sfxs]).contiguous()
+    out = torch.zeros(B, T, ndir * H, device=gpu)
+    hT = torch.empty(ndir, B, H, device=gpu)
+    cT = torch.empty(ndir, B, H, device=gpu)
+    work = torch.empty(3 * ndir * B * H, device=gpu)
+    ld = torch.tensor(lengths, dtype=torch.int32, device=gpu) if lengths else None
+    _lib.call("sd_op_lstm", gx.to(gpu).data_ptr(), B, T, H, ndir, whh.to(gpu).data_ptr(),
+              ld.data_ptr() if ld is not None else None, out.data_ptr(), hT.data_ptr(), cT.data_ptr(),
+              work.data_ptr(), _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(hT.cpu(), hn, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(cT.cpu(), cn, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("n", [400, 16000 * 3 + 123, 16000 * 60])
+def test_fbank(gpu, n):
+    from oracle import fbank_ref
+    rng = np.random.default_rng(n)
+    wav = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    ref = fbank_ref.fbank(wav)
+    out = frontend.kaldi_fbank(torch.from_numpy(wav).to(gpu)).cpu().numpy()
+    assert out.shape == ref.shape
+    np.testing.assert_allclose(out, ref, atol=2e-3, rtol=1e-4)
+
+
+def test_window_cmn(gpu):
+    g = torch.Generator().manual_seed(3)
+    feats = torch.randn(1000, 80, generator=g) * 4 + 2
+    starts = torch.tensor([0, 100, 400, 900], dtype=torch.int32)
+    ns = torch.tensor([398, 398, 198, 100], dtype=torch.int32)
+    out = frontend.window_cmn(feats.to(gpu), starts.to(gpu), ns.to(gpu), 398).cpu()
+    for i in range(4):
+        s, n = int(starts[i]), int(ns[i])
+        w = feats[s:s + n]
+        torch.testing.assert_close(out[i, :n], w - w.mean(0, keepdim=True), atol=1e-5, rtol=1e-5)
+        assert (out[i, n:] == 0).all()
+
+
+def test_overlap_average(gpu):
+    from speaker_diarization_amd.ts_vad.windows import plan_windows
+    from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    plan = plan_windows(1000, 6, 1)
+    g = torch.Generator().manual_seed(4)
+    logits = torch.randn(plan.n_win, 4, plan.chunk, generator=g)
+    out = TSVADPipeline.average(logits.to(gpu), plan).cpu().numpy()
+    prob = torch.sigmoid(logits).numpy()
+    ref = np.zeros((4, 1000), np.float32)
+    for t in range(1000):
+        vals = [prob[w, :, t - plan.starts[w]] for w in range(plan.n_win) if plan.starts[w] <= t < plan.ends[w]]
+        ref[:, t] = np.mean(np.stack(vals), axis=0)
+    np.testing.assert_allclose(out, ref, atol=1e-6, rtol=1e-6)

@@ -1,0 +1,93 @@
+"""End-to-end TS-VAD parity on the MI355X path vs reference goldens and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from make_golden import TSVAD_CASES, tsvad_inputs
+from speaker_diarization_amd.ts_vad.model import TSVADModel
+from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
+
+pytestmark = pytest.mark.gpu
+
+# fp32: exact-f32 MFMA, the north_star bound.  bf16: bf16 operands / fp32
+# accumulate through ~70 layers; bound on the logits measured on the goldens.
+FP32_ATOL = 1e-3
+BF16_ATOL = 0.08
+
+
+def _cfg(v, rs):
+    return TSVADConfig(rs_len=rs) if v == 0 else TSVADConfig.ots_vad_v1(rs_len=rs)
+
+
+_models = {}
+
+
+def _model(v, rs, wseed, precision, gpu):
+    key = (v, rs, wseed, precision)
+    if key not in _models:
+        cfg = _cfg(v, rs)
+        m = TSVADModel(cfg, device=gpu, precision=precision, max_batch=8)
+        m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=wseed)))
+        _models[key] = m
+    return _models[key]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(TSVAD_CASES))
+def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
+    v, rs, B, T, nl, iseed, wseed = TSVAD_CASES[name]
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    m = _model(v, rs, wseed, precision, gpu)
+    x, ts = tsvad_inputs(B, T, nl, seed=iseed)
+    labels = torch.zeros(B, 4, nl)
+    out = m.forward(torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu), labels).cpu().numpy()
+    err = np.abs(out - g["logits"]).max()
+    print(f"{name} {precision}: max|logit diff| = {err:.3e} (|logit| max {np.abs(g['logits']).max():.3f})")
+    assert err < (FP32_ATOL if precision == "fp32" else BF16_ATOL)
+
+
+def test_tsvad_strict_load_errors(gpu):
+    cfg = TSVADConfig()
+    sd = to_torch(tsvad_state_dict(cfg, seed=1))
+    sd.pop("fc.bias")
+    m = TSVADModel(cfg, device=gpu, precision="fp32", max_batch=2)
+    with pytest.raises(RuntimeError, match="fc.bias"):
+        m.load_state_dict(sd)
+    sd = to_torch(tsvad_state_dict(cfg, seed=1))
+    sd["extra.weight"] = torch.zeros(3)
+    m = TSVADModel(cfg, device=gpu, precision="fp32", max_batch=2)
+    with pytest.raises(RuntimeError, match="extra.weight"):
+        m.load_state_dict(sd)
+
+
+def test_tsvad_length_assert(gpu):
+    m = _model(0, 4, 777, "fp32", gpu)
+    x = torch.zeros(1, 398, 80, device=gpu)
+    ts = torch.zeros(1, 4, 192, device=gpu)
+    with pytest.raises(AssertionError, match="diff"):
+        m.forward(x, ts, torch.zeros(1, 4, 90))
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_pipeline_vs_oracle(gpu, variant, precision):
+    """Meeting wav in HBM -> posteriors, vs the CPU restatement of the reference
+    loop (per-window fbank + CMN, batch padding, res_dict mean)."""
+    from oracle.pipeline_ref import meeting_posteriors
+    from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
+    from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    rs = 4 if variant == 0 else 6
+    cfg = _cfg(variant, rs)
+    mt = make_meeting(23.0, n_spk=3, seed=11)
+    ts = np.zeros((4, 192), np.float32)
+    ts[:3] = speaker_embeddings(3, seed=11)
+    n_lab = mt.labels.shape[1]
+    sd = tsvad_state_dict(cfg, seed=5)
+    ref = meeting_posteriors(to_torch(sd), cfg, mt.wav, ts, n_lab, shift=1, batch_size=8, n_real=3)
+    m = TSVADModel(cfg, device=gpu, precision=precision, max_batch=8)
+    m.load_state_dict(to_torch(sd))
+    pipe = TSVADPipeline(m, segment_shift=1, batch_size=8)
+    post = pipe.posteriors(torch.from_numpy(mt.wav).to(gpu), torch.from_numpy(ts).to(gpu), n_lab).cpu().numpy()
+    err = np.abs(post[:3] - ref[:3]).max()
+    print(f"pipeline v{variant} {precision}: max|post diff| = {err:.3e}")
+    assert err < (1e-3 if precision == "fp32" else 2e-2)
