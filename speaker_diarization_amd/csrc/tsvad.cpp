@@ -79,7 +79,7 @@ ConvL TsvadModel::linear(const std::string& prefix, float mult) {
   int N, Cin, kh, kw;
   auto w = ps_.pack(prefix + ".weight", N, Cin, kh, kw, mult);
   L.w = upload_packed(arena_, w, N, Cin, kh, kw, cfg_.bf16);
-  if (ps_.has(prefix + ".bias")) {
+  {  // nn.Linear / the conformer's Conv1d(bias=True): the bias key is required (strict load)
     std::vector<float> b = ps_.get(prefix + ".bias").data;
     for (auto& v : b) v *= mult;
     L.beta = arena_.upload(b);

@@ -18,6 +18,24 @@ def _tol(precision):
     return FP32_TOL if precision == 0 else BF16_TOL
 
 
+_ALIVE = []
+
+
+def _d(t, gpu):
+    """Device copy kept alive until the test ends (a temporary's block could be
+    reused by the caching allocator before the kernel reads it)."""
+    x = t.to(gpu).contiguous()
+    _ALIVE.append(x)
+    return x.data_ptr()
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    torch.cuda.synchronize()
+    _ALIVE.clear()
+
+
 def _rel_err(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
@@ -59,7 +77,7 @@ def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
     ref = F.conv1d(x, w, b, stride=stride, padding=pad, dilation=dil).permute(0, 2, 1)
     xd = x.permute(0, 2, 1).contiguous().to(gpu)
     out = torch.empty(ref.shape, device=gpu)
-    _lib.call("sd_op_conv1d", xd.data_ptr(), B, T, Cin, w.to(gpu).data_ptr(), b.to(gpu).data_ptr(), Cout, k,
+    _lib.call("sd_op_conv1d", xd.data_ptr(), B, T, Cin, _d(w, gpu), _d(b, gpu), Cout, k,
               stride, pad, dil, 0, out.data_ptr(), precision, _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     if precision == 0:
@@ -78,7 +96,7 @@ def test_conv2d(gpu, precision, B, H, W, sh, kh, pad):
     ref = F.conv2d(x, w, stride=(sh, 1), padding=pad).permute(0, 2, 3, 1)
     out = torch.empty(ref.shape, device=gpu)
     xd = x.permute(0, 2, 3, 1).contiguous().to(gpu)
-    _lib.call("sd_op_conv2d", xd.data_ptr(), B, H, W, 32, w.to(gpu).data_ptr(), 32, kh, kh, sh, 1, pad, pad,
+    _lib.call("sd_op_conv2d", xd.data_ptr(), B, H, W, 32, _d(w, gpu), 32, kh, kh, sh, 1, pad, pad,
               out.data_ptr(), precision, _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     if precision == 0:
@@ -108,7 +126,7 @@ def test_attention(gpu, precision, S, T, D, nh, causal):
     qkv = torch.randn(S * T, 3 * D, generator=g)
     ref = _attn_ref(qkv, S, T, D, nh, causal)
     out = torch.empty(S * T, D, device=gpu)
-    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, causal, 0, None, out.data_ptr(), precision,
+    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, causal, 0, None, out.data_ptr(), precision,
               _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     if precision == 0:
@@ -125,7 +143,7 @@ def test_attention_key_len(gpu):
     ref = _attn_ref(qkv, S, T, D, nh, key_len=kl)
     out = torch.empty(S * T, D, device=gpu)
     kld = kl.to(gpu)
-    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, 0, 0, kld.data_ptr(), out.data_ptr(), 0,
+    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, 0, 0, kld.data_ptr(), out.data_ptr(), 0,
               _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
@@ -139,7 +157,7 @@ def test_attention_large_logits(gpu):
     qkv[150, D:2 * D] *= 30.0     # spike one key
     ref = _attn_ref(qkv, S, T, D, nh)
     out = torch.empty(S * T, D, device=gpu)
-    _lib.call("sd_op_attention", qkv.to(gpu).data_ptr(), S, T, D, nh, 0, 0, None, out.data_ptr(), 0,
+    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, 0, 0, None, out.data_ptr(), 0,
               _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, atol=2e-4, rtol=2e-4)
@@ -153,7 +171,7 @@ def test_layernorm(gpu, rows, D):
     b = torch.randn(D, generator=g)
     ref = F.layer_norm(x, (D,), w, b, 1e-5)
     out = torch.empty(rows, D, device=gpu)
-    _lib.call("sd_op_layernorm", x.to(gpu).data_ptr(), rows, D, w.to(gpu).data_ptr(), b.to(gpu).data_ptr(), 1e-5,
+    _lib.call("sd_op_layernorm", _d(x, gpu), rows, D, _d(w, gpu), _d(b, gpu), 1e-5,
               out.data_ptr(), _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
@@ -182,7 +200,7 @@ def test_lstm(gpu, B, T, H, ndir, lengths):
     cT = torch.empty(ndir, B, H, device=gpu)
     work = torch.empty(3 * ndir * B * H, device=gpu)
     ld = torch.tensor(lengths, dtype=torch.int32, device=gpu) if lengths else None
-    _lib.call("sd_op_lstm", gx.to(gpu).data_ptr(), B, T, H, ndir, whh.to(gpu).data_ptr(),
+    _lib.call("sd_op_lstm", _d(gx, gpu), B, T, H, ndir, _d(whh, gpu),
               ld.data_ptr() if ld is not None else None, out.data_ptr(), hT.data_ptr(), cT.data_ptr(),
               work.data_ptr(), _lib.stream_ptr(gpu))
     torch.cuda.synchronize()

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 # fp32: exact-f32 MFMA, the north_star bound.  bf16: bf16 operands / fp32
 # accumulate through ~70 layers; bound on the logits measured on the goldens.
 FP32_ATOL = 1e-3
-BF16_ATOL = 0.08
+BF16_ATOL = 2e-2
 
 
 def _cfg(v, rs):
