@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--minutes", type=float, default=None, help="meeting minutes per GPU")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=64, help="reference batch (windows, zero-pad unit)")
+    ap.add_argument("--device-batch", type=int, default=256, help="windows per device launch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -98,7 +99,7 @@ def main():
     minutes = a.minutes if a.minutes is not None else wl["minutes"]
     cfg = TSVADConfig(rs_len=wl["rs_len"]) if wl["variant"] == 0 else TSVADConfig.ots_vad_v1(rs_len=wl["rs_len"])
     sd_np = tsvad_state_dict(cfg, seed=777)
-    model = TSVADModel(cfg, device=dev, precision=a.precision, max_batch=a.batch)
+    model = TSVADModel(cfg, device=dev, precision=a.precision, max_batch=max(a.batch, a.device_batch))
     model.load_state_dict(to_torch(sd_np))
     pipe = TSVADPipeline(model, segment_shift=1, batch_size=a.batch)
 
@@ -191,6 +192,7 @@ def main():
             "config": {"workload": wl["desc"], "meeting_minutes": minutes * world,
                        "minutes_per_gpu": minutes, "windows": pipe.plan(n_lab).n_win,
                        "global_batch": a.batch * world, "batch_per_gpu": a.batch,
+                       "device_batch": max(a.batch, a.device_batch),
                        "parallelism": f"window-shard x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -99,7 +99,9 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
                        const int* len, int dis, int chunk, int n_frames, float* out, void* stream);
 
 /* ------------------------------------------------------------------ ops (parity tests)
- * precision: 0 fp32, 1 bf16.  Weights are fp32 device arrays in torch layout. */
+ * precision: 0 fp32, 1 bf16 MFMA (fp32 activations), 2 bf16 MFMA on bf16 activations
+ * (the input is converted first; exercises the LDS-DMA GEMM path).
+ * Weights are fp32 device arrays in torch layout. */
 /* nn.Linear: out (M, N) = act(x (M, K) · w (N, K)ᵀ + b). act: 0 none 1 relu 2 sigmoid 3 silu */
 int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, int N, int act,
                  float* out, int precision, void* stream);

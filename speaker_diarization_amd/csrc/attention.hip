@@ -23,8 +23,9 @@ constexpr int kKT = 32;   // keys per tile
 
 constexpr int f32_stride(int hd) { return hd + (((4 - hd) % 32) + 32) % 32; }
 
-template <bool BF16, int HD>
+template <bool BF16, int HD, bool IOBF>
 __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  using io_t = act_t<IOBF>;
   constexpr int HDP = BF16 ? ((HD + 31) / 32) * 32 : HD;   // padded head dim for bf16 k-chunks
   constexpr int KS_BF = HDP + 8;                           // bf16 K row stride
   constexpr int VT_BF = kKT + 8;                           // bf16 Vᵀ row stride
@@ -49,14 +50,14 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int q0 = blockIdx.x * kQB + wid * 16;
   const int myq = q0 + l15;
   const int D = a.D;
-  const float* base = a.qkv + (int64_t)s * T * a.ld_qkv;
+  const io_t* base = reinterpret_cast<const io_t*>(a.qkv) + (int64_t)s * T * a.ld_qkv;
   const int klen = a.key_len ? min(a.key_len[s], T) : T;
 
   // Q operand (B operand of Sᵀ = K·Qᵀ), pre-scaled.
   constexpr int QN = BF16 ? HDP / 32 : HD / 4;
   typename std::conditional<BF16, bf16x8, float>::type qf[QN];
   {
-    const float* qr = base + (int64_t)min(myq, T - 1) * a.ld_qkv + h * HD;
+    const io_t* qr = base + (int64_t)min(myq, T - 1) * a.ld_qkv + h * HD;
     const bool qv = myq < T;
     if constexpr (BF16) {
 #pragma unroll
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           int d = kc * 32 + g * 8 + j;
-          float x = (qv && d < HD) ? qr[d] * a.scale : 0.f;
+          float x = (qv && d < HD) ? ld_act(qr, d) * a.scale : 0.f;
           uint16_t bits = f2bf_bits(x);
           v[j] = __builtin_bit_cast(__bf16, bits);
         }
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       }
     } else {
 #pragma unroll
-      for (int kk = 0; kk < QN; ++kk) qf[kk] = qv ? qr[kk * 4 + g] * a.scale : 0.f;
+      for (int kk = 0; kk < QN; ++kk) qf[kk] = qv ? ld_act(qr, kk * 4 + g) * a.scale : 0.f;
     }
   }
 
@@ -93,9 +94,18 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       int key = k0 + kr;
       float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
       if (key < T) {
-        const float* r = base + (int64_t)key * a.ld_qkv + h * HD + d4;
-        kv = *reinterpret_cast<const float4*>(r + D);
-        vv = *reinterpret_cast<const float4*>(r + 2 * D);
+        const io_t* r = base + (int64_t)key * a.ld_qkv + h * HD + d4;
+        if constexpr (IOBF) {
+          uint2 k2 = *reinterpret_cast<const uint2*>(r + D);
+          uint2 v2 = *reinterpret_cast<const uint2*>(r + 2 * D);
+          kv = make_float4(__uint_as_float(k2.x << 16), __uint_as_float(k2.x & 0xffff0000u),
+                           __uint_as_float(k2.y << 16), __uint_as_float(k2.y & 0xffff0000u));
+          vv = make_float4(__uint_as_float(v2.x << 16), __uint_as_float(v2.x & 0xffff0000u),
+                           __uint_as_float(v2.y << 16), __uint_as_float(v2.y & 0xffff0000u));
+        } else {
+          kv = *reinterpret_cast<const float4*>(r + D);
+          vv = *reinterpret_cast<const float4*>(r + 2 * D);
+        }
       }
       if constexpr (BF16) {
         uint2 pk;
@@ -221,29 +231,33 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     const int q = q0 + qi;
     if (q >= T) continue;
     const float inv = lr > 0.f ? 1.f / lr : 0.f;
-    float* orow = a.out + ((int64_t)s * T + q) * a.ldo + h * HD;
+    io_t* orow = reinterpret_cast<io_t*>(a.out) + ((int64_t)s * T + q) * a.ldo + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) orow[dt * 16 + l15] = o[dt][r] * inv;
+    for (int dt = 0; dt < DT; ++dt) st_act(orow, dt * 16 + l15, o[dt][r] * inv);
   }
 }
 
 template <int HD>
 void launch_hd(const AttnArgs& a, bool bf16, hipStream_t st) {
   dim3 grid(cdiv(a.T, kQB), a.S * a.nh);
-  if (bf16)
-    hipLaunchKernelGGL((attn_kernel<true, HD>), grid, dim3(256), 0, st, a);
+  if (bf16 && a.io_bf16)
+    hipLaunchKernelGGL((attn_kernel<true, HD, true>), grid, dim3(256), 0, st, a);
+  else if (bf16)
+    hipLaunchKernelGGL((attn_kernel<true, HD, false>), grid, dim3(256), 0, st, a);
+  else if (a.io_bf16)
+    hipLaunchKernelGGL((attn_kernel<false, HD, true>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((attn_kernel<false, HD>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_kernel<false, HD, false>), grid, dim3(256), 0, st, a);
 }
 
 }  // namespace
 
 void attention(const AttnArgs& a, bool bf16, hipStream_t st) {
   SD_CHECK(a.nh > 0 && a.D % a.nh == 0, kErrInvalid, "attention: D % nh != 0");
-  SD_CHECK(a.ld_qkv % 4 == 0, kErrInvalid, "attention: ld_qkv % 4 != 0");
+  SD_CHECK(a.ld_qkv % 4 == 0 && a.D % 4 == 0, kErrInvalid, "attention: ld_qkv % 4 != 0");
   const int hd = a.D / a.nh;
   const double flops = 4.0 * a.S * a.nh * (double)a.T * a.T * hd * (a.causal ? 0.5 : 1.0);
-  const double bytes = 4.0 * a.S * a.T * (3.0 * a.D + a.D);
+  const double bytes = (a.io_bf16 ? 2.0 : 4.0) * a.S * a.T * (3.0 * a.D + a.D);
   ProfScope prof(bf16 ? "attention_bf16" : "attention_f32", flops, bytes, st);
   switch (hd) {
     case 48: launch_hd<48>(a, bf16, st); break;

@@ -160,10 +160,13 @@ int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, i
                  float* out, int precision, void* stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    const bool bf = precision == 1;
+    const bool bf = precision >= 1;
     Scratch wt((size_t)N * K * (bf ? 2 : 4), st);
     sd::pack_weight(w, N, K, 1, wt.p, bf, st);
-    sd::ConvGemmArgs p = sd::linear_args(x, M, K, K, wt.p, N, out, N);
+    Scratch xb(precision == 2 ? (size_t)M * K * 2 : 4, st);   // precision 2: bf16 activations
+    if (precision == 2) sd::f32_to_bf16(x, (int64_t)M * K, xb.p, st);
+    sd::ConvGemmArgs p = sd::linear_args(precision == 2 ? xb.p : (const void*)x, M, K, K, wt.p, N, out, N);
+    p.a_bf16 = precision == 2;
     p.beta = b;
     p.act = act;
     sd::conv_gemm(p, bf, st);
@@ -175,11 +178,13 @@ int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const fl
                  void* stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    const bool bf = precision == 1;
+    const bool bf = precision >= 1;
     Scratch wt((size_t)Cout * Cin * k * (bf ? 2 : 4), st);
     sd::pack_weight(w, Cout, Cin, k, wt.p, bf, st);
+    Scratch xb(precision == 2 ? (size_t)B * T * Cin * 2 : 4, st);
+    if (precision == 2) sd::f32_to_bf16(x, (int64_t)B * T * Cin, xb.p, st);
     sd::ConvGemmArgs p;
-    p.A = x; p.B = B; p.H = 1; p.W = T; p.Cin = Cin; p.lda = Cin;
+    p.A = precision == 2 ? xb.p : (const void*)x; p.a_bf16 = precision == 2; p.B = B; p.H = 1; p.W = T; p.Cin = Cin; p.lda = Cin;
     p.kh = 1; p.kw = k; p.sw = stride; p.pw = pad; p.dw = dil;
     p.Ho = 1; p.Wo = (T + 2 * pad - dil * (k - 1) - 1) / stride + 1;
     SD_CHECK(p.Wo > 0, sd::kErrInvalid, "conv1d: empty output");
@@ -194,11 +199,13 @@ int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, i
                  int kw, int sh, int sw, int ph, int pw, float* out, int precision, void* stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    const bool bf = precision == 1;
+    const bool bf = precision >= 1;
     Scratch wt((size_t)Cout * Cin * kh * kw * (bf ? 2 : 4), st);
     sd::pack_weight(w, Cout, Cin, kh * kw, wt.p, bf, st);
+    Scratch xb(precision == 2 ? (size_t)B * H * W * Cin * 2 : 4, st);
+    if (precision == 2) sd::f32_to_bf16(x, (int64_t)B * H * W * Cin, xb.p, st);
     sd::ConvGemmArgs p;
-    p.A = x; p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.lda = Cin;
+    p.A = precision == 2 ? xb.p : (const void*)x; p.a_bf16 = precision == 2; p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.lda = Cin;
     p.kh = kh; p.kw = kw; p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw;
     p.Ho = (H + 2 * ph - kh) / sh + 1;
     p.Wo = (W + 2 * pw - kw) / sw + 1;
@@ -222,7 +229,7 @@ int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, 
 
 int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
                     float* y, void* stream) {
-  return guard([&] { sd::layernorm(x, rows, D, D, g, b, eps, y, D, S(stream)); });
+  return guard([&] { sd::layernorm(x, rows, D, D, g, b, eps, y, D, false, S(stream)); });
 }
 
 int sd_op_lstm(const float* gx, int B, int T, int H, int ndir, const float* whh, const int* lengths,

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <type_traits>
 
 namespace sd {
 
@@ -57,6 +58,15 @@ __device__ __forceinline__ float bf_bits2f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
 
+// Element access for activations stored as fp32 or bf16 (uint16 bits).
+__device__ __forceinline__ float ld_act(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float ld_act(const uint16_t* p, int64_t i) { return bf_bits2f(p[i]); }
+__device__ __forceinline__ void st_act(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st_act(uint16_t* p, int64_t i, float v) { p[i] = f2bf_bits(v); }
+
+template <bool BF>
+using act_t = typename std::conditional<BF, uint16_t, float>::type;
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -70,6 +80,15 @@ __device__ __forceinline__ float warp_max(float v) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// XCD-aware tile order (cdna_hip_programming.md T1, bijective form): workgroups
+// are dealt round-robin over the 8 XCDs, so remap the linear id such that
+// consecutive logical tiles (the N-tiles sharing one A row panel) run on the
+// same XCD and hit its L2.  Returns the logical tile id.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
 
 enum Act : int { kActNone = 0, kActRelu = 1, kActSigmoid = 2, kActSilu = 3 };
 

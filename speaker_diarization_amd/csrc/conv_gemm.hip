@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
     }
   }
 
-  const int KT = p.K / kBK;
+  const int KT = (p.K + kBK - 1) / kBK;
   float4 areg[APASS];
   // B staging registers.
   constexpr int BCHUNK = BF16 ? (BN * 4) : (BN * 8);   // 16-B chunks per tile
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
     const int tj = tap - ti * p.kw;
     const int c = c0 + kq;
     float4 s4, h4;
-    if (p.pre_scale) {
+    if (p.pre_scale && k0 + kq < p.K) {
       s4 = *reinterpret_cast<const float4*>(p.pre_scale + c);
       h4 = *reinterpret_cast<const float4*>(p.pre_shift + c);
     }
@@ -97,8 +97,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
       int hi = rh[i] + ti * p.dh;
       int wi = rw[i] + tj * p.dw;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W) {
-        const float* src = p.A + ((int64_t)(rbh[i] + hi) * p.W + wi) * p.lda + p.a_coff + c;
+      if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && k0 + kq < p.K) {
+        const float* src = reinterpret_cast<const float*>(p.A) + ((int64_t)(rbh[i] + hi) * p.W + wi) * p.lda + p.a_coff + c;
         v = *reinterpret_cast<const float4*>(src);
         if (p.pre_scale) {
           v.x = fmaxf(v.x * s4.x + h4.x, 0.f);
@@ -116,12 +116,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
       if (ch < BCHUNK) {
         if (BF16) {
           int n = ch >> 2, kc = (ch & 3) * 8;
-          if (n0 + n < p.N)
+          if (n0 + n < p.N && k0 + kc < p.K)
             v = *reinterpret_cast<const uint4*>(
                 reinterpret_cast<const uint16_t*>(p.Wt) + (int64_t)(n0 + n) * p.K + k0 + kc);
         } else {
           int n = ch >> 3, kc = (ch & 7) * 4;
-          if (n0 + n < p.N)
+          if (n0 + n < p.N && k0 + kc < p.K)
             v = *reinterpret_cast<const uint4*>(
                 reinterpret_cast<const float*>(p.Wt) + (int64_t)(n0 + n) * p.K + k0 + kc);
         }
@@ -234,10 +234,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
         float v = acc[mt][nt][r];
         if (p.alpha) v *= p.alpha[n];
         if (p.beta) v += p.beta[n];
-        if (p.res) v += p.res[(int64_t)m * p.res_ld + n];
+        if (p.res) v += reinterpret_cast<const float*>(p.res)[(int64_t)m * p.res_ld + n];
         v = apply_act(v, p.act);
         if (p.gate) v *= p.gate[((int64_t)b * p.gate_nseg + wo / p.gate_seg) * p.N + n];
-        p.out[obase + (int64_t)n * p.o_sn] = v;
+        reinterpret_cast<float*>(p.out)[obase + (int64_t)n * p.o_sn] = v;
       }
     }
   }
@@ -245,6 +245,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
 
 template <int BM, int BN>
 void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
+  SD_CHECK(!p.a_bf16 && !p.out_bf16 && !p.res_bf16, kErrInvalid, "fp32 conv_gemm takes fp32 tensors");
   const int M = p.B * p.Ho * p.Wo;
   dim3 grid(cdiv(p.N, BN), cdiv(M, BM));
   if (bf16)
@@ -257,12 +258,16 @@ void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
 
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(p.K == p.kh * p.kw * p.Cin, kErrInvalid, "conv_gemm: K != kh*kw*Cin");
-  SD_CHECK(p.K % kBK == 0, kErrInvalid, "conv_gemm: K must be a multiple of 32");
+  SD_CHECK(p.K % 4 == 0, kErrInvalid, "conv_gemm: K must be a multiple of 4");
   SD_CHECK(p.Cin % kBK == 0 || (p.kh * p.kw == 1), kErrInvalid,
            "conv_gemm: multi-tap conv needs Cin % 32 == 0");
   SD_CHECK(p.lda % 4 == 0 && p.a_coff % 4 == 0, kErrInvalid, "conv_gemm: lda/a_coff must be multiples of 4");
   SD_CHECK(p.N > 0 && p.B > 0 && p.Ho > 0 && p.Wo > 0, kErrInvalid, "conv_gemm: empty problem");
   SD_CHECK(!p.gate || p.gate_seg > 0, kErrInvalid, "conv_gemm: gate_seg must be > 0");
+  if (bf16) {
+    conv_gemm_bf16(p, st);
+    return;
+  }
   const int M = p.B * p.Ho * p.Wo;
   // Algorithmic work: 2*M*N*K flops; bytes = input activation once + weights + output (+res).
   const double flops = 2.0 * M * p.N * (double)p.K;

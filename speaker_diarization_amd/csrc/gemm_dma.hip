@@ -1,0 +1,271 @@
+// bf16 implicit GEMM fed by LDS-DMA (buffer_load_dwordx4 ... lds) — the fast path
+// of conv_gemm for bf16 activations without a BN-ReLU prologue.
+//
+// * A (activations) and B (packed weights) tiles go global -> LDS directly, 16 B
+//   per lane; each wave instruction fills 8 rows x 128 B.  Out-of-range rows
+//   (conv zero padding, M/N/K tails) use an out-of-range buffer offset, which
+//   the buffer unit returns as zeros: no branches in the k loop.
+// * LDS rows are 128 B (BK = 64 bf16) unpadded; the 16-B chunk c of row r is
+//   stored at chunk c ^ (r & 7) (swizzle applied on the SOURCE address, the
+//   DMA destination stays lane-linear), which makes the MFMA fragment reads
+//   (ds_read_b128, 16 rows x one chunk) bank-conflict free.
+// * 2 LDS stages: the DMA of tile k+1 is in flight while tile k is consumed;
+//   one vmcnt(0) + barrier per k-tile.
+// * Epilogue identical to gemm_bf16.hip (LDS-staged, coalesced, bf16/fp32 out).
+// Handles taps == 1 (linear / 1x1 conv) and multi-tap convs with Cin % 64 == 0.
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int BK = 64;
+constexpr uint32_t kOOB = 0x80000000u;   // >= num_records -> hardware returns zeros
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf_bits(a) | ((uint32_t)f2bf_bits(b) << 16);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
+  constexpr int TM = BM / 2, TN = BN / 2;
+  constexpr int MT = TM / 16, NT = TN / 16;
+  constexpr int AI = BM / 32;        // A DMA instructions per wave per k-tile (8 rows each)
+  constexpr int BI = BN / 32;
+  constexpr int STAGE = (BM + BN) * BK;   // bf16 elements per stage
+  constexpr int CLD = BN + 4;
+  constexpr int EPI = BM * CLD * 2;
+  constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) uint16_t sm[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int M = p.B * p.Ho * p.Wo;
+  const int n_nt = (p.N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / n_nt) * BM;
+  const int n0 = (tile % n_nt) * BN;
+  const int taps = p.kh * p.kw;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), (short)0,
+                                                                      (int)kOOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Wt), (short)0,
+                                                                      (int)kOOB, 0x00020000);
+  // Per-lane A rows handled by this wave's DMA instructions.
+  const int lrow = lane >> 3;          // row within an 8-row group
+  const int lch = lane & 7;            // physical chunk this lane fills
+  int a_bh[AI], a_h[AI], a_w[AI], a_lc[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int r = wid * (BM / 4) + j * 8 + lrow;
+    const int m = m0 + r;
+    a_lc[j] = lch ^ (r & 7);
+    if (m < M) {
+      const int wo = m % p.Wo;
+      const int t = m / p.Wo;
+      const int ho = t % p.Ho;
+      a_bh[j] = (t / p.Ho) * p.H;
+      a_h[j] = ho * p.sh - p.ph;
+      a_w[j] = wo * p.sw - p.pw;
+    } else {
+      a_bh[j] = 0;
+      a_h[j] = -(1 << 28);
+      a_w[j] = 0;
+    }
+  }
+  int b_row[BI], b_lc[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int r = wid * (BN / 4) + j * 8 + lrow;
+    b_row[j] = n0 + r;
+    b_lc[j] = lch ^ (r & 7);
+  }
+
+  auto issue = [&](int kt, int stg) {
+    const int k0 = kt * BK;
+    int tap = 0, c0 = k0;
+    if (taps > 1) {
+      tap = k0 / p.Cin;
+      c0 = k0 - tap * p.Cin;
+    }
+    const int ti = tap / p.kw, tj = tap - (tap / p.kw) * p.kw;
+    const int dho = ti * p.dh, dwo = tj * p.dw;
+    uint16_t* As = sm + stg * STAGE;
+    uint16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int hi = a_h[j] + dho, wi = a_w[j] + dwo;
+      const int c = c0 + a_lc[j] * 8;
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && (k0 + a_lc[j] * 8) < p.K;
+      const uint32_t off = ok ? (uint32_t)((((int64_t)(a_bh[j] + hi) * p.W + wi) * p.lda + p.a_coff + c) * 2)
+                              : kOOB;
+      lds_ptr_t dst = (lds_ptr_t)(As + (wid * (BM / 4) + j * 8) * BK);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int k = k0 + b_lc[j] * 8;
+      const bool ok = b_row[j] < p.N && k < p.K;
+      const uint32_t off = ok ? (uint32_t)(((int64_t)b_row[j] * p.K + k) * 2) : kOOB;
+      lds_ptr_t dst = (lds_ptr_t)(Bs + (wid * (BN / 4) + j * 8) * BK);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, dst, 16, off, 0, 0, 0);
+    }
+  };
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = (p.K + BK - 1) / BK;
+  const int l15 = lane & 15, lk = lane >> 4;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int stg = kt & 1;
+    if (kt + 1 < KT) issue(kt + 1, stg ^ 1);
+    const uint16_t* As = sm + stg * STAGE;
+    const uint16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MT], bfr[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int r = wm * TM + mt * 16 + l15;
+        af[mt] = *reinterpret_cast<const bf16x8*>(As + r * BK + (((ks * 4 + lk) ^ (r & 7)) * 8));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int r = wn * TN + nt * 16 + l15;
+        bfr[nt] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + (((ks * 4 + lk) ^ (r & 7)) * 8));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue (LDS-staged, row-contiguous 4-column groups)
+  float* Cs = reinterpret_cast<float*>(sm);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + l15] = acc[mt][nt][r];
+  __syncthreads();
+
+  const bool lin = p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh;
+  const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
+  constexpr int CPR = BN / 4;
+  for (int q = tid; q < BM * CPR; q += 256) {
+    const int row = q / CPR;
+    const int cc = (q % CPR) * 4;
+    const int m = m0 + row;
+    const int n = n0 + cc;
+    if (m >= M || n >= p.N) continue;
+    const float4 c4 = *reinterpret_cast<const float4*>(Cs + row * CLD + cc);
+    float v[4] = {c4.x, c4.y, c4.z, c4.w};
+    int b = 0, ho = 0, wo = m;
+    if (!lin || p.gate) {
+      wo = m % p.Wo;
+      const int t = m / p.Wo;
+      ho = t % p.Ho;
+      b = t / p.Ho;
+    }
+    const bool full = n + 3 < p.N;
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.res) {
+      const int64_t ro = (int64_t)m * p.res_ld + n;
+      if (p.res_bf16) {
+        const uint16_t* r = reinterpret_cast<const uint16_t*>(p.res) + ro;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rv[u] = (full || n + u < p.N) ? bf_bits2f(r[u]) : 0.f;
+      } else {
+        const float* r = reinterpret_cast<const float*>(p.res) + ro;
+        if (full && (p.res_ld & 3) == 0) {
+          const float4 r4 = *reinterpret_cast<const float4*>(r);
+          rv[0] = r4.x; rv[1] = r4.y; rv[2] = r4.z; rv[3] = r4.w;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rv[u] = (full || n + u < p.N) ? r[u] : 0.f;
+        }
+      }
+    }
+    const float* gr = p.gate ? p.gate + ((int64_t)b * p.gate_nseg + wo / p.gate_seg) * p.N : nullptr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int nn = n + u;
+      if (!full && nn >= p.N) break;
+      float x = v[u];
+      if (p.alpha) x *= p.alpha[nn];
+      if (p.beta) x += p.beta[nn];
+      x += rv[u];
+      x = apply_act(x, p.act);
+      if (gr) x *= gr[nn];
+      v[u] = x;
+    }
+    if (vec && full) {
+      const int64_t o = (int64_t)m * p.o_sw + n;
+      if (p.out_bf16)
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.out) + o) =
+            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      else
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      const int64_t ob = lin ? (int64_t)m * p.o_sw
+                             : (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (n + u >= p.N) break;
+        const int64_t o = ob + (int64_t)(n + u) * p.o_sn;
+        if (p.out_bf16) reinterpret_cast<uint16_t*>(p.out)[o] = f2bf_bits(v[u]);
+        else reinterpret_cast<float*>(p.out)[o] = v[u];
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+void launch(const ConvGemmArgs& p, hipStream_t st) {
+  const int M = p.B * p.Ho * p.Wo;
+  dim3 grid(cdiv(p.N, BN) * cdiv(M, BM));
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN>), grid, dim3(256), 0, st, p);
+}
+
+}  // namespace
+
+bool gemm_dma_supported(const ConvGemmArgs& p) {
+  const int taps = p.kh * p.kw;
+  const int64_t a_bytes = ((int64_t)p.B * p.H * p.W) * p.lda * 2;
+  const int64_t w_bytes = (int64_t)p.N * p.K * 2;
+  return p.a_bf16 && !p.pre_scale && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
+         p.a_coff % 8 == 0 && a_bytes < (int64_t)kOOB && w_bytes < (int64_t)kOOB;
+}
+
+void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st) {
+  const int M = p.B * p.Ho * p.Wo;
+  const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
+  const bool big = (int64_t)cdiv(M, 128) * cdiv(p.N, bn) >= 512;
+  if (bn == 128) {
+    if (big) launch<128, 128>(p, st); else launch<64, 128>(p, st);
+  } else if (bn == 64) {
+    if (big) launch<128, 64>(p, st); else launch<64, 64>(p, st);
+  } else {
+    if (big) launch<128, 32>(p, st); else launch<64, 32>(p, st);
+  }
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

@@ -8,8 +8,9 @@ namespace sd {
 // ---------------------------------------------------------------- conv_gemm
 struct ConvGemmArgs {
   // Input activation, channel-last: element (b, h, w, c) at
-  // A[((b*H + h)*W + w)*lda + a_coff + c].
-  const float* A = nullptr;
+  // A[((b*H + h)*W + w)*lda + a_coff + c]; fp32, or bf16 when a_bf16.
+  const void* A = nullptr;
+  bool a_bf16 = false;
   int B = 1, H = 1, W = 1, Cin = 0, lda = 0, a_coff = 0;
   int Ho = 1, Wo = 1;
   int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
@@ -20,37 +21,43 @@ struct ConvGemmArgs {
   const float* pre_shift = nullptr;
   const float* alpha = nullptr;      // per output channel scale
   const float* beta = nullptr;       // per output channel shift
-  const float* res = nullptr;        // residual, res[m*res_ld + n]
+  const void* res = nullptr;         // residual at the output's (m, n) address map, stride res_ld
+  bool res_bf16 = false;
   int res_ld = 0;
   int act = kActNone;
   const float* gate = nullptr;       // gate[(b*gate_nseg + wo/gate_seg)*N + n]
   int gate_seg = 1, gate_nseg = 1;
-  float* out = nullptr;              // out[b*o_sb + ho*o_sh + wo*o_sw + n*o_sn]
+  void* out = nullptr;               // out[b*o_sb + ho*o_sh + wo*o_sw + n*o_sn]
+  bool out_bf16 = false;
   int64_t o_sb = 0, o_sh = 0, o_sw = 0, o_sn = 1;
 };
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
+void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
+bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
+void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
 
 // Plain row-major linear layer helper: out[m*ldo + o_coff + n] = act(A[m*lda+k]·W[n][k] * alpha + beta (+res)).
-ConvGemmArgs linear_args(const float* A, int M, int K, int lda, const void* Wt, int N,
-                         float* out, int ldo);
+ConvGemmArgs linear_args(const void* A, int M, int K, int lda, const void* Wt, int N,
+                         void* out, int ldo);
 
 // ---------------------------------------------------------------- fcm / cam++
 // First FCM conv (Cin = 1, 3x3, pad 1) + folded BN + ReLU.  fbank (B, T, F) ->
 // NHWC (B, F, T, 32).  cam_pplus_wespeaker.py:277-301.
 void fcm_conv1(const float* fbank, int B, int T, int F, const float* w /*32x9*/,
-               const float* alpha, const float* beta, float* out, hipStream_t st);
+               const float* alpha, const float* beta, void* out, bool out_bf16, hipStream_t st);
 
 // CAMLayer context gate (cam_pplus_wespeaker.py:106-123):
 // ctx[b,s,c] = mean_t x[b,t,c] + mean_{t in seg s} x[b,t,c];
 // gate[b,s,:] = sigmoid(W2·relu(W1·ctx + b1) + b2).
-void cam_context(const float* x, int B, int T, int C, int ldx, int seg_len,
+void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int seg_len,
                  const float* w1, const float* b1, int C1, const float* w2, const float* b2,
                  int C2, float* gate, hipStream_t st);
 
 // ---------------------------------------------------------------- norms
 // y = LN(x) * g + b over the last dim D; rows of x at stride ldx, y at ldy.
+// y may be bf16 (y_bf16); x is fp32 (the residual stream).
 void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
-               float eps, float* y, int ldy, hipStream_t st);
+               float eps, void* y, int ldy, bool y_bf16, hipStream_t st);
 
 // ---------------------------------------------------------------- attention
 // Multi-head self-attention core on a packed in-projection output.
@@ -58,10 +65,11 @@ void layernorm(const float* x, int rows, int D, int ldx, const float* g, const f
 // out: (S*T, ldo) at column h*hd.  Optional causal mask (key > query + delay is
 // masked) and per-sequence key lengths (keys >= len[s] masked).
 struct AttnArgs {
-  const float* qkv = nullptr;
+  const void* qkv = nullptr;       // fp32, or bf16 when io_bf16 (also the output dtype)
+  bool io_bf16 = false;
   int S = 0, T = 0, D = 0, nh = 0;
   int ld_qkv = 0;
-  float* out = nullptr;
+  void* out = nullptr;
   int ldo = 0;
   float scale = 1.f;
   int causal = 0, causal_delay = 0;
@@ -84,19 +92,19 @@ void gsp_fc(const float* x, int rows, int C, int ldx, const float* w /*E x 2*/,
             const float* bias, int E, float* out, int ldo, hipStream_t st);
 
 // (B*NS, T, E) speaker-major rows -> (B, T, NS*E) channel-concatenated rows.
-void speakers_to_channels(const float* x, int B, int NS, int T, int E, float* out,
+void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out, bool out_bf16,
                           hipStream_t st);
 
 // ---------------------------------------------------------------- conformer conv module
 // GLU over channel pairs (a = x[:, c], g = x[:, C + c]) followed by a depthwise
 // conv over time (kernel k, pad (k-1)/2, with bias).  x: (S, T, 2C); y: (S, T, C).
 // Also writes per (sequence, channel-block) partial sums for GroupNorm(1, C).
-void glu_dwconv(const float* x, int S, int T, int C, const float* w /*C x k*/,
-                const float* bias, int k, float* y, float* partial /*S x nblk x 2*/,
+void glu_dwconv(const void* x, int S, int T, int C, const float* w /*C x k*/,
+                const float* bias, int k, void* y, float* partial /*S x nblk x 2*/, bool io_bf16,
                 hipStream_t st);
 // GroupNorm(num_groups=1) over (T, C) of each sequence, affine, then SiLU (in place).
-void groupnorm_silu(float* y, int S, int T, int C, const float* partial, const float* g,
-                    const float* b, float eps, hipStream_t st);
+void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
+                    const float* b, float eps, bool io_bf16, hipStream_t st);
 
 // ---------------------------------------------------------------- lstm
 // One bidirectional (or unidirectional) LSTM layer recurrence given the
@@ -130,4 +138,8 @@ void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16,
 namespace sd {
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
                      int dis, int chunk, int n_frames, float* out, hipStream_t st);
+}  // namespace sd
+
+namespace sd {
+void f32_to_bf16(const float* x, int64_t n, void* y, hipStream_t st);
 }  // namespace sd

@@ -7,8 +7,8 @@
 
 namespace sd {
 
-ConvGemmArgs linear_args(const float* A, int M, int K, int lda, const void* Wt, int N,
-                         float* out, int ldo) {
+ConvGemmArgs linear_args(const void* A, int M, int K, int lda, const void* Wt, int N,
+                         void* out, int ldo) {
   ConvGemmArgs p;
   p.A = A; p.B = 1; p.H = 1; p.W = M; p.Cin = K; p.lda = lda; p.a_coff = 0;
   p.Ho = 1; p.Wo = M;
@@ -18,11 +18,12 @@ ConvGemmArgs linear_args(const float* A, int M, int K, int lda, const void* Wt, 
 }
 
 // ------------------------------------------------------------------ FCM stem
+template <bool OBF>
 __global__ __launch_bounds__(256) void fcm_conv1_kernel(const float* __restrict__ fb, int B, int T,
                                                         int F, const float* __restrict__ w,
                                                         const float* __restrict__ alpha,
                                                         const float* __restrict__ beta,
-                                                        float* __restrict__ out) {
+                                                        void* __restrict__ out) {
   __shared__ float ws[32 * 9];
   __shared__ float al[32], be[32];
   for (int i = threadIdx.x; i < 32 * 9; i += blockDim.x) ws[i] = w[i];
@@ -43,108 +44,153 @@ __global__ __launch_bounds__(256) void fcm_conv1_kernel(const float* __restrict_
       int ff = f + i - 1, tt = t + j - 1;
       x[i * 3 + j] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? fb[((int64_t)b * T + tt) * F + ff] : 0.f;
     }
-  float4* o = reinterpret_cast<float4*>(out + idx * 32);
 #pragma unroll
-  for (int c4 = 0; c4 < 8; ++c4) {
-    float v[4];
+  for (int c8 = 0; c8 < 4; ++c8) {
+    float v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int c = c4 * 4 + u;
+    for (int u = 0; u < 8; ++u) {
+      int c = c8 * 8 + u;
       float acc = 0.f;
 #pragma unroll
       for (int k = 0; k < 9; ++k) acc = fmaf(ws[c * 9 + k], x[k], acc);
       v[u] = fmaxf(acc * al[c] + be[c], 0.f);
     }
-    o[c4] = make_float4(v[0], v[1], v[2], v[3]);
+    if constexpr (OBF) {
+      uint4 pk;
+      pk.x = (uint32_t)f2bf_bits(v[0]) | ((uint32_t)f2bf_bits(v[1]) << 16);
+      pk.y = (uint32_t)f2bf_bits(v[2]) | ((uint32_t)f2bf_bits(v[3]) << 16);
+      pk.z = (uint32_t)f2bf_bits(v[4]) | ((uint32_t)f2bf_bits(v[5]) << 16);
+      pk.w = (uint32_t)f2bf_bits(v[6]) | ((uint32_t)f2bf_bits(v[7]) << 16);
+      reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + idx * 32)[c8] = pk;
+    } else {
+      float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + idx * 32);
+      o[2 * c8] = make_float4(v[0], v[1], v[2], v[3]);
+      o[2 * c8 + 1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
   }
 }
 
 void fcm_conv1(const float* fbank, int B, int T, int F, const float* w, const float* alpha,
-               const float* beta, float* out, hipStream_t st) {
+               const float* beta, void* out, bool out_bf16, hipStream_t st) {
   int64_t total = (int64_t)B * F * T;
   ProfScope prof("fcm_conv1", 2.0 * total * 32 * 9, 4.0 * total * 33, st);
-  hipLaunchKernelGGL(fcm_conv1_kernel, dim3((unsigned)cdiv((int)total, 256)), dim3(256), 0, st,
-                     fbank, B, T, F, w, alpha, beta, out);
+  if (out_bf16)
+    hipLaunchKernelGGL(fcm_conv1_kernel<true>, dim3((unsigned)cdiv((int)total, 256)), dim3(256), 0, st,
+                       fbank, B, T, F, w, alpha, beta, out);
+  else
+    hipLaunchKernelGGL(fcm_conv1_kernel<false>, dim3((unsigned)cdiv((int)total, 256)), dim3(256), 0, st,
+                       fbank, B, T, F, w, alpha, beta, out);
   SD_LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------------------ CAM context
 constexpr int kMaxSeg = 32;
 
+// One workgroup per batch item: segment sums over time (4 independent
+// accumulators per thread for load ILP), then the 2-layer context MLP with both
+// weight matrices staged in LDS at a padded (+1) row stride.
+template <bool XBF>
 __global__ __launch_bounds__(256) void cam_context_kernel(
-    const float* __restrict__ x, int T, int C, int ldx, int seg_len,
+    const void* __restrict__ xv, int T, int C, int ldx, int seg_len,
     const float* __restrict__ w1, const float* __restrict__ b1, int C1,
     const float* __restrict__ w2, const float* __restrict__ b2, int C2, float* __restrict__ gate) {
   extern __shared__ float sm[];
   const int b = blockIdx.x;
   const int nseg = (T + seg_len - 1) / seg_len;
   const int parts = blockDim.x / C;
-  float* psum = sm;                       // [parts][nseg][C]
-  float* ctx = psum + parts * nseg * C;   // [nseg][C]
-  float* h1 = ctx + nseg * C;             // [nseg][C1]
-  const int c = threadIdx.x % C;
-  const int part = threadIdx.x / C;
-  const float* xb = x + (int64_t)b * T * ldx;
+  float* psum = sm;                         // [parts][nseg][C]
+  float* ctx = psum + parts * nseg * C;     // [nseg][C]
+  float* h1 = ctx + nseg * C;               // [nseg][C1]
+  float* W1 = h1 + nseg * C1;               // [C1][C+1]
+  float* W2 = W1 + C1 * (C + 1);            // [C2][C1+1]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C1 * C; i += blockDim.x) W1[(i / C) * (C + 1) + i % C] = w1[i];
+  for (int i = tid; i < C2 * C1; i += blockDim.x) W2[(i / C1) * (C1 + 1) + i % C1] = w2[i];
+  const int c = tid % C;
+  const int part = tid / C;
   if (part < parts) {
     for (int s = 0; s < nseg; ++s) {
-      float acc = 0.f;
-      int t1 = min(T, (s + 1) * seg_len);
-      for (int t = s * seg_len + part; t < t1; t += parts) acc += xb[(int64_t)t * ldx + c];
-      psum[(part * nseg + s) * C + c] = acc;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      const int t1 = min(T, (s + 1) * seg_len);
+      int t = s * seg_len + part;
+      auto ld = [&](int tt) -> float {
+        const int64_t o = ((int64_t)b * T + tt) * ldx + c;
+        if constexpr (XBF) return bf_bits2f(reinterpret_cast<const uint16_t*>(xv)[o]);
+        else return reinterpret_cast<const float*>(xv)[o];
+      };
+      for (; t + 3 * parts < t1; t += 4 * parts) {
+        a0 += ld(t); a1 += ld(t + parts); a2 += ld(t + 2 * parts); a3 += ld(t + 3 * parts);
+      }
+      for (; t < t1; t += parts) a0 += ld(t);
+      psum[(part * nseg + s) * C + c] = (a0 + a1) + (a2 + a3);
     }
   }
   __syncthreads();
-  if (threadIdx.x < C) {
+  if (tid < C) {
     float tot = 0.f;
     for (int s = 0; s < nseg; ++s) {
       float ss = 0.f;
-      for (int q = 0; q < parts; ++q) ss += psum[(q * nseg + s) * C + threadIdx.x];
-      ctx[s * C + threadIdx.x] = ss;
+      for (int q = 0; q < parts; ++q) ss += psum[(q * nseg + s) * C + tid];
+      ctx[s * C + tid] = ss;
       tot += ss;
     }
-    float mean = tot / (float)T;
+    const float mean = tot / (float)T;
     for (int s = 0; s < nseg; ++s) {
-      int cnt = min(T, (s + 1) * seg_len) - s * seg_len;
-      ctx[s * C + threadIdx.x] = mean + ctx[s * C + threadIdx.x] / (float)cnt;
+      const int cnt = min(T, (s + 1) * seg_len) - s * seg_len;
+      ctx[s * C + tid] = mean + ctx[s * C + tid] / (float)cnt;
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nseg * C1; i += blockDim.x) {
-    int s = i / C1, j = i % C1;
-    float acc = b1[j];
-    const float* wr = w1 + (int64_t)j * C;
-    for (int k = 0; k < C; ++k) acc = fmaf(wr[k], ctx[s * C + k], acc);
-    h1[i] = fmaxf(acc, 0.f);
+  for (int i = tid; i < nseg * C1; i += blockDim.x) {
+    const int s = i / C1, j = i % C1;
+    const float* wr = W1 + j * (C + 1);
+    const float* cr = ctx + s * C;
+    float a0 = b1[j], a1 = 0.f;
+    for (int k = 0; k < C; k += 2) {
+      a0 = fmaf(wr[k], cr[k], a0);
+      a1 = fmaf(wr[k + 1], cr[k + 1], a1);
+    }
+    h1[i] = fmaxf(a0 + a1, 0.f);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nseg * C2; i += blockDim.x) {
-    int s = i / C2, o = i % C2;
-    float acc = b2[o];
-    const float* wr = w2 + (int64_t)o * C1;
-    for (int k = 0; k < C1; ++k) acc = fmaf(wr[k], h1[s * C1 + k], acc);
-    gate[((int64_t)b * nseg + s) * C2 + o] = 1.f / (1.f + expf(-acc));
+  for (int i = tid; i < nseg * C2; i += blockDim.x) {
+    const int s = i / C2, o = i % C2;
+    const float* wr = W2 + o * (C1 + 1);
+    const float* hr = h1 + s * C1;
+    float a0 = b2[o], a1 = 0.f;
+    for (int k = 0; k < C1; k += 2) {
+      a0 = fmaf(wr[k], hr[k], a0);
+      a1 = fmaf(wr[k + 1], hr[k + 1], a1);
+    }
+    gate[((int64_t)b * nseg + s) * C2 + o] = 1.f / (1.f + expf(-(a0 + a1)));
   }
 }
 
-void cam_context(const float* x, int B, int T, int C, int ldx, int seg_len, const float* w1,
+void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int seg_len, const float* w1,
                  const float* b1, int C1, const float* w2, const float* b2, int C2, float* gate,
                  hipStream_t st) {
-  SD_CHECK(C <= 256 && 256 % C == 0, kErrInvalid, "cam_context: C must divide 256");
-  int nseg = cdiv(T, seg_len);
+  SD_CHECK(C <= 256 && 256 % C == 0 && C % 2 == 0 && C1 % 2 == 0, kErrInvalid,
+           "cam_context: C must divide 256");
+  const int nseg = cdiv(T, seg_len);
   SD_CHECK(nseg <= kMaxSeg, kErrInvalid, "cam_context: too many segments");
-  size_t smem = sizeof(float) * ((256 / C) * nseg * C + nseg * C + nseg * C1);
-  ProfScope prof("cam_context", 2.0 * B * nseg * (C * C1 + C1 * C2), 4.0 * B * T * C, st);
-  hipLaunchKernelGGL(cam_context_kernel, dim3(B), dim3(256), smem, st, x, T, C, ldx, seg_len, w1,
-                     b1, C1, w2, b2, C2, gate);
+  const size_t smem = sizeof(float) * ((256 / C) * nseg * C + nseg * C + nseg * C1 + C1 * (C + 1) +
+                                       C2 * (C1 + 1));
+  ProfScope prof("cam_context", 2.0 * B * nseg * (C * C1 + C1 * C2), (x_bf16 ? 2.0 : 4.0) * B * T * C, st);
+  if (x_bf16)
+    hipLaunchKernelGGL(cam_context_kernel<true>, dim3(B), dim3(256), smem, st, x, T, C, ldx, seg_len, w1,
+                       b1, C1, w2, b2, C2, gate);
+  else
+    hipLaunchKernelGGL(cam_context_kernel<false>, dim3(B), dim3(256), smem, st, x, T, C, ldx, seg_len, w1,
+                       b1, C1, w2, b2, C2, gate);
   SD_LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------------------ LayerNorm
-template <int PER>
+template <int PER, bool YBF>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows, int D,
                                                         int ldx, const float* __restrict__ g,
                                                         const float* __restrict__ bb, float eps,
-                                                        float* __restrict__ y, int ldy) {
+                                                        act_t<YBF>* __restrict__ y, int ldy) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -168,26 +214,33 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
   q = warp_sum(q);
   const float rstd = rsqrtf(q / (float)D + eps);
-  float* yr = y + (int64_t)row * ldy;
+  act_t<YBF>* yr = y + (int64_t)row * ldy;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     int c = lane + i * 64;
-    if (c < D) yr[c] = (v[i] - mean) * rstd * g[c] + bb[c];
+    if (c < D) st_act(yr, c, (v[i] - mean) * rstd * g[c] + bb[c]);
   }
 }
 
-void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
-               float eps, float* y, int ldy, hipStream_t st) {
+template <int PER>
+static void ln_launch(const float* x, int rows, int D, int ldx, const float* g, const float* b, float eps,
+                      void* y, int ldy, bool ybf, hipStream_t st) {
   dim3 grid(cdiv(rows, 4));
-  ProfScope prof("layernorm", 0.0, 8.0 * rows * D, st);
-  if (D <= 256)
-    hipLaunchKernelGGL((layernorm_kernel<4>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
-  else if (D <= 512)
-    hipLaunchKernelGGL((layernorm_kernel<8>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
-  else if (D <= 1024)
-    hipLaunchKernelGGL((layernorm_kernel<16>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps, y, ldy);
+  if (ybf)
+    hipLaunchKernelGGL((layernorm_kernel<PER, true>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps,
+                       reinterpret_cast<uint16_t*>(y), ldy);
   else
-    SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");
+    hipLaunchKernelGGL((layernorm_kernel<PER, false>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps,
+                       reinterpret_cast<float*>(y), ldy);
+}
+
+void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
+               float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
+  ProfScope prof("layernorm", 0.0, (4.0 + (y_bf16 ? 2.0 : 4.0)) * rows * D, st);
+  if (D <= 256) ln_launch<4>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
+  else if (D <= 512) ln_launch<8>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
+  else if (D <= 1024) ln_launch<16>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
+  else SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");
   SD_LAUNCH_CHECK();
 }
 
@@ -257,20 +310,27 @@ void gsp_fc(const float* x, int rows, int C, int ldx, const float* w, const floa
   SD_LAUNCH_CHECK();
 }
 
+template <bool OBF>
 __global__ void speakers_to_channels_kernel(const float* __restrict__ x, int B, int NS, int T, int E,
-                                            float* __restrict__ out) {
+                                            act_t<OBF>* __restrict__ out) {
   const int row = blockIdx.x;  // (b, t)
   const int t = row % T;
   const int b = row / T;
-  float* o = out + (int64_t)row * NS * E;
+  act_t<OBF>* o = out + (int64_t)row * NS * E;
   for (int c = threadIdx.x; c < NS * E; c += blockDim.x) {
     int spk = c / E, e = c % E;
-    o[c] = x[(((int64_t)b * NS + spk) * T + t) * E + e];
+    st_act(o, c, x[(((int64_t)b * NS + spk) * T + t) * E + e]);
   }
 }
 
-void speakers_to_channels(const float* x, int B, int NS, int T, int E, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(speakers_to_channels_kernel, dim3(B * T), dim3(256), 0, st, x, B, NS, T, E, out);
+void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out, bool out_bf16,
+                          hipStream_t st) {
+  if (out_bf16)
+    hipLaunchKernelGGL(speakers_to_channels_kernel<true>, dim3(B * T), dim3(256), 0, st, x, B, NS, T, E,
+                       reinterpret_cast<uint16_t*>(out));
+  else
+    hipLaunchKernelGGL(speakers_to_channels_kernel<false>, dim3(B * T), dim3(256), 0, st, x, B, NS, T, E,
+                       reinterpret_cast<float*>(out));
   SD_LAUNCH_CHECK();
 }
 
@@ -278,10 +338,11 @@ void speakers_to_channels(const float* x, int B, int NS, int T, int E, float* ou
 constexpr int kDwCB = 64;    // channels per block
 constexpr int kDwTT = 64;    // time tile
 
-__global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict__ x, int T, int C,
+template <bool BF>
+__global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __restrict__ x, int T, int C,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias, int k,
-                                                         float* __restrict__ y,
+                                                         act_t<BF>* __restrict__ y,
                                                          float* __restrict__ partial) {
   extern __shared__ float sm[];
   const int pad = (k - 1) / 2;
@@ -295,8 +356,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict
     int cc = i / k, j = i % k;
     wsm[i] = (c0 + cc < C) ? w[(int64_t)(c0 + cc) * k + j] : 0.f;
   }
-  const float* xs = x + (int64_t)s * T * 2 * C;
-  float* ys = y + (int64_t)s * T * C;
+  const act_t<BF>* xs = x + (int64_t)s * T * 2 * C;
+  act_t<BF>* ys = y + (int64_t)s * T * C;
   float lsum = 0.f, lsq = 0.f;
   const int cc = threadIdx.x % kDwCB;
   const int tq = threadIdx.x / kDwCB;   // 0..3
@@ -308,8 +369,8 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict
       int t = t0 - pad + tt;
       float v = 0.f;
       if (t >= 0 && t < T && c0 + c < C) {
-        float a = xs[(int64_t)t * 2 * C + c0 + c];
-        float gg = xs[(int64_t)t * 2 * C + C + c0 + c];
+        float a = ld_act(xs, (int64_t)t * 2 * C + c0 + c);
+        float gg = ld_act(xs, (int64_t)t * 2 * C + C + c0 + c);
         v = a / (1.f + expf(-gg));
       }
       g[i] = v;
@@ -320,7 +381,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict
       for (int tt = tq; tt < kDwTT && t0 + tt < T; tt += 4) {
         float acc = bv;
         for (int j = 0; j < k; ++j) acc = fmaf(wsm[cc * k + j], g[(tt + j) * kDwCB + cc], acc);
-        ys[(int64_t)(t0 + tt) * C + c0 + cc] = acc;
+        st_act(ys, (int64_t)(t0 + tt) * C + c0 + cc, acc);
         lsum += acc;
         lsq += acc * acc;
       }
@@ -342,16 +403,23 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const float* __restrict
   }
 }
 
-void glu_dwconv(const float* x, int S, int T, int C, const float* w, const float* bias, int k,
-                float* y, float* partial, hipStream_t st) {
+void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
+                void* y, float* partial, bool io_bf16, hipStream_t st) {
   dim3 grid(cdiv(C, kDwCB), S);
   size_t smem = sizeof(float) * ((kDwTT + k - 1) * kDwCB + kDwCB * k);
   ProfScope prof("glu_dwconv", 2.0 * S * T * C * k, 4.0 * S * T * 3.0 * C, st);
-  hipLaunchKernelGGL(glu_dwconv_kernel, grid, dim3(256), smem, st, x, T, C, w, bias, k, y, partial);
+  if (io_bf16)
+    hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), smem, st,
+                       reinterpret_cast<const uint16_t*>(x), T, C, w, bias, k, reinterpret_cast<uint16_t*>(y),
+                       partial);
+  else
+    hipLaunchKernelGGL(glu_dwconv_kernel<false>, grid, dim3(256), smem, st, reinterpret_cast<const float*>(x),
+                       T, C, w, bias, k, reinterpret_cast<float*>(y), partial);
   SD_LAUNCH_CHECK();
 }
 
-__global__ __launch_bounds__(256) void groupnorm_silu_kernel(float* __restrict__ y, int T, int C,
+template <bool BF>
+__global__ __launch_bounds__(256) void groupnorm_silu_kernel(act_t<BF>* __restrict__ y, int T, int C,
                                                              const float* __restrict__ partial, int nblk,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float eps) {
@@ -367,23 +435,28 @@ __global__ __launch_bounds__(256) void groupnorm_silu_kernel(float* __restrict__
   if (var < 0) var = 0;
   const float fm = (float)mean;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  float* ys = y + (int64_t)s * T * C;
+  act_t<BF>* ys = y + (int64_t)s * T * C;
   const int64_t total = (int64_t)T * C;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     int c = i % C;
-    float v = (ys[i] - fm) * rstd * g[c] + b[c];
-    ys[i] = v / (1.f + expf(-v));
+    float v = (ld_act(ys, i) - fm) * rstd * g[c] + b[c];
+    st_act(ys, i, v / (1.f + expf(-v)));
   }
 }
 
-void groupnorm_silu(float* y, int S, int T, int C, const float* partial, const float* g,
-                    const float* b, float eps, hipStream_t st) {
+void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
+                    const float* b, float eps, bool io_bf16, hipStream_t st) {
   int nblk = cdiv(C, kDwCB);
   int per = cdiv(T * C, 256);
   dim3 grid(min(per, 16), S);
   ProfScope prof("groupnorm_silu", 0.0, 8.0 * S * T * C, st);
-  hipLaunchKernelGGL(groupnorm_silu_kernel, grid, dim3(256), 0, st, y, T, C, partial, nblk, g, b, eps);
+  if (io_bf16)
+    hipLaunchKernelGGL(groupnorm_silu_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<uint16_t*>(y), T,
+                       C, partial, nblk, g, b, eps);
+  else
+    hipLaunchKernelGGL(groupnorm_silu_kernel<false>, grid, dim3(256), 0, st, reinterpret_cast<float*>(y), T,
+                       C, partial, nblk, g, b, eps);
   SD_LAUNCH_CHECK();
 }
 
@@ -485,6 +558,22 @@ void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* 
   if (total == 0) return;
   hipLaunchKernelGGL(overlap_average_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd
+
+namespace sd {
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, int64_t n, uint16_t* __restrict__ y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = f2bf_bits(x[i]);
+}
+
+void f32_to_bf16(const float* x, int64_t n, void* y, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n,
+                     reinterpret_cast<uint16_t*>(y));
   SD_LAUNCH_CHECK();
 }
 

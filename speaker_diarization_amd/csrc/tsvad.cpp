@@ -20,38 +20,48 @@ namespace sd {
 
 namespace {
 
-ConvGemmArgs conv1d(const float* in, int B, int T, int lda, int a_coff, const ConvL& L, int stride,
-                    int pad, int dil, float* out, int ldo) {
+// Activation tensors: fp32, or bf16 bits when the flag is set.
+struct Tens {
+  void* p;
+  bool bf;
+};
+inline Tens act_at(const Tens& a, int64_t elems) {
+  return Tens{static_cast<char*>(a.p) + elems * (a.bf ? 2 : 4), a.bf};
+}
+
+ConvGemmArgs conv1d(Tens in, int B, int T, int lda, const ConvL& L, int stride, int pad, int dil, Tens out,
+                    int ldo) {
   ConvGemmArgs p;
-  p.A = in; p.B = B; p.H = 1; p.W = T; p.Cin = L.w.Cin; p.lda = lda; p.a_coff = a_coff;
+  p.A = in.p; p.a_bf16 = in.bf; p.B = B; p.H = 1; p.W = T; p.Cin = L.w.Cin; p.lda = lda; p.a_coff = 0;
   p.kh = 1; p.kw = L.w.kw; p.sh = 1; p.sw = stride; p.ph = 0; p.pw = pad; p.dh = 1; p.dw = dil;
   p.Ho = 1;
   p.Wo = (T + 2 * pad - dil * (L.w.kw - 1) - 1) / stride + 1;
   p.Wt = L.w.w; p.N = L.w.N; p.K = L.w.K;
   p.pre_scale = L.pre_s; p.pre_shift = L.pre_h;
   p.alpha = L.alpha; p.beta = L.beta;
-  p.out = out; p.o_sb = (int64_t)p.Wo * ldo; p.o_sh = 0; p.o_sw = ldo; p.o_sn = 1;
+  p.out = out.p; p.out_bf16 = out.bf;
+  p.o_sb = (int64_t)p.Wo * ldo; p.o_sh = 0; p.o_sw = ldo; p.o_sn = 1;
   return p;
 }
 
-ConvGemmArgs conv2d(const float* in, int B, int H, int W, const ConvL& L, int sh, int sw, int ph,
-                    int pw, float* out) {
+ConvGemmArgs conv2d(Tens in, int B, int H, int W, const ConvL& L, int sh, int sw, int ph, int pw, Tens out) {
   ConvGemmArgs p;
-  p.A = in; p.B = B; p.H = H; p.W = W; p.Cin = L.w.Cin; p.lda = L.w.Cin; p.a_coff = 0;
+  p.A = in.p; p.a_bf16 = in.bf; p.B = B; p.H = H; p.W = W; p.Cin = L.w.Cin; p.lda = L.w.Cin; p.a_coff = 0;
   p.kh = L.w.kh; p.kw = L.w.kw; p.sh = sh; p.sw = sw; p.ph = ph; p.pw = pw; p.dh = 1; p.dw = 1;
   p.Ho = (H + 2 * ph - L.w.kh) / sh + 1;
   p.Wo = (W + 2 * pw - L.w.kw) / sw + 1;
   p.Wt = L.w.w; p.N = L.w.N; p.K = L.w.K;
   p.pre_scale = L.pre_s; p.pre_shift = L.pre_h;
   p.alpha = L.alpha; p.beta = L.beta;
-  p.out = out;
+  p.out = out.p; p.out_bf16 = out.bf;
   p.o_sb = (int64_t)p.Ho * p.Wo * p.N; p.o_sh = (int64_t)p.Wo * p.N; p.o_sw = p.N; p.o_sn = 1;
   return p;
 }
 
-ConvGemmArgs lin(const float* A, int M, int lda, const PackedW& w, const float* bias, float* out,
-                 int ldo) {
-  ConvGemmArgs p = linear_args(A, M, w.K, lda, w.w, w.N, out, ldo);
+ConvGemmArgs lin(Tens A, int M, int lda, const PackedW& w, const float* bias, Tens out, int ldo) {
+  ConvGemmArgs p = linear_args(A.p, M, w.K, lda, w.w, w.N, out.p, ldo);
+  p.a_bf16 = A.bf;
+  p.out_bf16 = out.bf;
   p.beta = bias;
   return p;
 }
@@ -290,65 +300,70 @@ void TsvadModel::alloc_workspace() {
 }
 
 void TsvadModel::run_transformer(const TransformerL& L, float* X, int S, int T, int nh, hipStream_t st) {
-  const int E = cfg_.embed_dim;
-  const int rows = S * T;
-  conv_gemm(lin(X, rows, E, L.in_proj, L.in_b, QKV_, 3 * E), cfg_.bf16, st);
-  AttnArgs a;
-  a.qkv = QKV_; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
-  a.out = AO_; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
-  attention(a, cfg_.bf16, st);
-  ConvGemmArgs p = lin(AO_, rows, E, L.out_proj, L.out_b, Y_, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, cfg_.bf16, st);
-  layernorm(Y_, rows, E, E, L.n1g, L.n1b, 1e-5f, X, E, st);
-  p = lin(X, rows, E, L.l1, L.b1, H_, L.l1.N);
-  p.act = kActRelu;
-  conv_gemm(p, cfg_.bf16, st);
-  p = lin(H_, rows, L.l1.N, L.l2, L.b2, Y_, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, cfg_.bf16, st);
-  layernorm(Y_, rows, E, E, L.n2g, L.n2b, 1e-5f, X, E, st);
-}
-
-void TsvadModel::run_conformer(const ConformerL& L, float* X, int S, int T, hipStream_t st) {
+  // nn.TransformerEncoderLayer (post-LN): X fp32 residual stream; QKV/AO/H bf16 in bf16 mode.
   const int E = cfg_.embed_dim;
   const int rows = S * T;
   const bool bf = cfg_.bf16;
+  const Tens x{X, false}, y{Y_, false}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
+  conv_gemm(lin(x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
+  AttnArgs a;
+  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
+  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
+  attention(a, bf, st);
+  ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, y, E);
+  p.res = X; p.res_ld = E;
+  conv_gemm(p, bf, st);
+  layernorm(Y_, rows, E, E, L.n1g, L.n1b, 1e-5f, X, E, false, st);
+  p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
+  p.act = kActRelu;
+  conv_gemm(p, bf, st);
+  p = lin(h, rows, L.l1.N, L.l2, L.b2, y, E);
+  p.res = X; p.res_ld = E;
+  conv_gemm(p, bf, st);
+  layernorm(Y_, rows, E, E, L.n2g, L.n2b, 1e-5f, X, E, false, st);
+}
+
+void TsvadModel::run_conformer(const ConformerL& L, float* X, int S, int T, hipStream_t st) {
+  // torchaudio ConformerLayer: X fp32 residual stream; LN outputs / GEMM-only intermediates bf16.
+  const int E = cfg_.embed_dim;
+  const int rows = S * T;
+  const bool bf = cfg_.bf16;
+  const Tens x{X, false}, y{Y_, bf}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
   auto ffn = [&](const float* lng, const float* lnb, const PackedW& w1, const float* b1,
                  const PackedW& w2, const float* b2) {
-    layernorm(X, rows, E, E, lng, lnb, 1e-5f, Y_, E, st);
-    ConvGemmArgs p = lin(Y_, rows, E, w1, b1, H_, w1.N);
+    layernorm(X, rows, E, E, lng, lnb, 1e-5f, y.p, E, bf, st);
+    ConvGemmArgs p = lin(y, rows, E, w1, b1, h, w1.N);
     p.act = kActSilu;
     conv_gemm(p, bf, st);
-    p = lin(H_, rows, w1.N, w2, b2, X, E);   // weights pre-scaled by 0.5
+    p = lin(h, rows, w1.N, w2, b2, x, E);   // weights pre-scaled by 0.5
     p.res = X; p.res_ld = E;
     conv_gemm(p, bf, st);
   };
   ffn(L.f1_lng, L.f1_lnb, L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
   // self attention block
-  layernorm(X, rows, E, E, L.at_lng, L.at_lnb, 1e-5f, Y_, E, st);
-  conv_gemm(lin(Y_, rows, E, L.in_proj, L.in_b, QKV_, 3 * E), bf, st);
+  layernorm(X, rows, E, E, L.at_lng, L.at_lnb, 1e-5f, y.p, E, bf, st);
+  conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
   AttnArgs a;
-  a.qkv = QKV_; a.S = S; a.T = T; a.D = E; a.nh = cfg_.conformer_heads; a.ld_qkv = 3 * E;
-  a.out = AO_; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / cfg_.conformer_heads));
+  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = cfg_.conformer_heads; a.ld_qkv = 3 * E;
+  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / cfg_.conformer_heads));
   attention(a, bf, st);
   {
-    ConvGemmArgs p = lin(AO_, rows, E, L.out_proj, L.out_b, X, E);
+    ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, x, E);
     p.res = X; p.res_ld = E;
     conv_gemm(p, bf, st);
   }
   // convolution module
-  layernorm(X, rows, E, E, L.cv_lng, L.cv_lnb, 1e-5f, Y_, E, st);
-  conv_gemm(lin(Y_, rows, E, L.pw1, L.pw1_b, H_, 2 * E), bf, st);
-  glu_dwconv(H_, S, T, E, L.dw_w, L.dw_b, cfg_.conformer_kernel, AO_, partial_, st);
-  groupnorm_silu(AO_, S, T, E, partial_, L.gn_g, L.gn_b, 1e-5f, st);
+  layernorm(X, rows, E, E, L.cv_lng, L.cv_lnb, 1e-5f, y.p, E, bf, st);
+  conv_gemm(lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E), bf, st);
+  glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, cfg_.conformer_kernel, ao.p, partial_, bf, st);
+  groupnorm_silu(ao.p, S, T, E, partial_, L.gn_g, L.gn_b, 1e-5f, bf, st);
   {
-    ConvGemmArgs p = lin(AO_, rows, E, L.pw2, L.pw2_b, X, E);
+    ConvGemmArgs p = lin(ao, rows, E, L.pw2, L.pw2_b, x, E);
     p.res = X; p.res_ld = E;
     conv_gemm(p, bf, st);
   }
   ffn(L.f2_lng, L.f2_lnb, L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
-  layernorm(X, rows, E, E, L.fin_g, L.fin_b, 1e-5f, X, E, st);
+  layernorm(X, rows, E, E, L.fin_g, L.fin_b, 1e-5f, X, E, false, st);
 }
 
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
@@ -356,10 +371,10 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
-  const bool bf = cfg_.bf16;
+  const bool bf = cfg_.bf16;   // bf16 mode: CAM++ activations stored as bf16
   const int F = 80;
-  // ---------------- FCM head
-  fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA_, st);
+  // ---------------- FCM head (cam_pplus_wespeaker.py:271-308), NHWC (B, F, T, 32)
+  fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA_, bf, st);
   // layer1.0: A(80) -> B(40); shortcut A -> C(40); conv2 B -> A(40) + C
   // layer1.1: A -> B; conv2 B -> C + A
   // layer2.0: C(40) -> A(20); shortcut C -> B(20); conv2 A -> C(20) + B
@@ -374,22 +389,21 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     for (float* b : bufs) if (b != cur) others[k++] = b;
     float* t1 = others[0];
     float* t2 = others[1];
-    ConvGemmArgs p = conv2d(cur, B, H, Tf, rb.c1, rb.stride, 1, 1, 1, t1);
+    ConvGemmArgs p = conv2d(Tens{cur, bf}, B, H, Tf, rb.c1, rb.stride, 1, 1, 1, Tens{t1, bf});
     p.act = kActRelu;
     conv_gemm(p, bf, st);
     const int Ho = p.Ho;
     const float* res = cur;
     float* outb;
     if (rb.has_sc) {
-      ConvGemmArgs q = conv2d(cur, B, H, Tf, rb.sc, rb.stride, 1, 0, 0, t2);
-      conv_gemm(q, bf, st);
+      conv_gemm(conv2d(Tens{cur, bf}, B, H, Tf, rb.sc, rb.stride, 1, 0, 0, Tens{t2, bf}), bf, st);
       res = t2;
       outb = cur;   // input no longer needed
     } else {
       outb = t2;
     }
-    ConvGemmArgs r = conv2d(t1, B, Ho, Tf, rb.c2, 1, 1, 1, 1, outb);
-    r.res = res; r.res_ld = 32;
+    ConvGemmArgs r = conv2d(Tens{t1, bf}, B, Ho, Tf, rb.c2, 1, 1, 1, 1, Tens{outb, bf});
+    r.res = res; r.res_bf16 = bf; r.res_ld = 32;
     r.act = kActRelu;
     conv_gemm(r, bf, st);
     cur = outb;
@@ -397,48 +411,46 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   }
   {
     // head.conv2 (stride (2,1)) + bn2 + relu, stored as (B, T, C*F') with channel c*F'+f.
-    ConvGemmArgs p = conv2d(cur, B, H, Tf, fcm_conv2_, 2, 1, 1, 1, x0_);
+    ConvGemmArgs p = conv2d(Tens{cur, bf}, B, H, Tf, fcm_conv2_, 2, 1, 1, 1, Tens{x0_, bf});
     p.act = kActRelu;
     const int Fo = p.Ho;
     SD_CHECK(Fo * 32 == 320, kErrShape, "FCM output width mismatch");
     p.o_sb = (int64_t)Tf * 320; p.o_sh = 1; p.o_sw = 320; p.o_sn = Fo;
     conv_gemm(p, bf, st);
   }
-  // ---------------- xvector: TDNN + dense blocks + transits
+  // ---------------- xvector: TDNN + dense blocks + transits (channel-last (B, T, C))
   const int T2 = (Tf - 1) / 2 + 1;
   const int ctot[3] = {512, 1024, 1024};
   {
-    ConvGemmArgs p = conv1d(x0_, B, Tf, 320, 0, tdnn_, 2, 2, 1, d_[0], ctot[0]);
+    ConvGemmArgs p = conv1d(Tens{x0_, bf}, B, Tf, 320, tdnn_, 2, 2, 1, Tens{d_[0], bf}, ctot[0]);
     p.act = kActRelu;
     SD_CHECK(p.Wo == T2, kErrShape, "tdnn output length");
     conv_gemm(p, bf, st);
   }
   int cin = 128;
   for (int b = 0; b < 3; ++b) {
-    float* D = d_[b];
+    const Tens D{d_[b], bf};
     const int ld = ctot[b];
     for (const DenseL& L : dense_[b]) {
-      ConvGemmArgs p = conv1d(D, B, T2, ld, 0, L.bottleneck, 1, 0, 1, tmp_, 128);
-      p.Cin = cin; p.K = cin;
       SD_CHECK(L.bottleneck.w.Cin == cin, kErrParam, "dense layer input width");
+      ConvGemmArgs p = conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp_, bf}, 128);
       p.act = kActRelu;
       conv_gemm(p, bf, st);
-      cam_context(tmp_, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
-      ConvGemmArgs q = conv1d(tmp_, B, T2, 128, 0, L.local, 1, L.dil, L.dil, D + cin, ld);
+      cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
+      ConvGemmArgs q = conv1d(Tens{tmp_, bf}, B, T2, 128, L.local, 1, L.dil, L.dil, act_at(D, cin), ld);
       q.gate = gate_; q.gate_seg = 100; q.gate_nseg = (T2 + 99) / 100;
       conv_gemm(q, bf, st);
       cin += L.local.w.N;
     }
     SD_CHECK(cin == ld, kErrShape, "dense block width");
-    float* dst = b < 2 ? d_[b + 1] : x4_;
+    const Tens dst{b < 2 ? d_[b + 1] : x4_, bf};
     const int ldo = b < 2 ? ctot[b + 1] : 512;
-    ConvGemmArgs p = conv1d(D, B, T2, ld, 0, transit_[b], 1, 0, 1, dst, ldo);
-    conv_gemm(p, bf, st);
+    conv_gemm(conv1d(D, B, T2, ld, transit_[b], 1, 0, 1, dst, ldo), bf, st);
     cin = transit_[b].w.N;
   }
-  // ---------------- speech_down_or_up (out_nonlinear BN-ReLU fused as prologue)
+  // ---------------- speech_down_or_up (out_nonlinear BN-ReLU fused as prologue), fp32 out
   const int E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim, NS = cfg_.max_num_speaker;
-  ConvGemmArgs pd = conv1d(x4_, B, T2, 512, 0, down_, 2, 2, 1, mix_, SE);
+  ConvGemmArgs pd = conv1d(Tens{x4_, bf}, B, T2, 512, down_, 2, 2, 1, Tens{mix_, false}, SE);
   pd.act = kActRelu;
   const int T3 = pd.Wo;
   conv_gemm(pd, bf, st);
@@ -450,13 +462,13 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     // Per-speaker encoder over S = B*NS sequences (model.py:869-879).
     build_speaker_input(ts, mix_, SE, T3, B, NS, Tl, SE, pe_, X_, st);
     for (const auto& L : single_) run_transformer(L, X_, S, Tl, cfg_.num_attention_head, st);
-    speakers_to_channels(X_, B, NS, Tl, E, X2_, st);
-    ConvGemmArgs p = conv1d(X2_, B, Tl, NS * E, 0, backend_down_, 1, 2, 1, X_, E);
+    speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
+    ConvGemmArgs p = conv1d(Tens{X2_, bf}, B, Tl, NS * E, backend_down_, 1, 2, 1, Tens{X_, false}, E);
     p.act = kActRelu;
     conv_gemm(p, bf, st);
     add_pe(X_, B * Tl, Tl, E, E, pe_, st);
     for (const auto& L : multi_) run_transformer(L, X_, B, Tl, cfg_.num_attention_head, st);
-    ConvGemmArgs f = conv1d(X_, B, Tl, E, 0, fc_, 1, 0, 1, logits, 1);
+    ConvGemmArgs f = conv1d(Tens{X_, false}, B, Tl, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
   } else {
@@ -465,13 +477,12 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
     build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
     for (const auto& L : conf_) run_conformer(L, X_, S, Tl, st);
-    speakers_to_channels(X_, B, NS, Tl, E, X2_, st);
+    speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     const int Hh = cfg_.lstm_hidden;
-    ConvGemmArgs p = lin(X2_, B * Tl, NS * E, lstm_ih_, lstm_b_, H_, 8 * Hh);
-    conv_gemm(p, bf, st);
+    conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
                     nullptr, lstm_work_, st);
-    ConvGemmArgs f = conv1d(Y_, B, Tl, 2 * Hh, 0, fc_, 1, 0, 1, logits, 1);
+    ConvGemmArgs f = conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
   }

@@ -47,14 +47,26 @@ class TSVADPipeline:
         fstart = torch.from_numpy((plan.fbank_start[w0:w1] - f0).astype(np.int32)).to(dev)
         fn = torch.from_numpy(plan.fbank_n[w0:w1].astype(np.int32)).to(dev)
         ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
-        for b0 in range(w0, w1, self.batch_size):
-            b1 = min(w1, b0 + self.batch_size)
-            T_out = int(plan.fbank_n[b0:b1].max())
-            T_lab = int(plan.lens[b0:b1].max())
+        for b0, b1, T_out, T_lab in self.device_batches(plan, w0, w1):
             ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
             lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab)
             out[b0 - w0:b1 - w0, :, :T_lab] = lg
         return out
+
+    def device_batches(self, plan: WindowPlan, w0: int, w1: int):
+        """Reference batches (batch_size windows, zero-padded to their own max length,
+        ts_vad_dataset.py:664-701) of [w0, w1); consecutive batches with the same
+        padded shape are fused into one device launch of up to model.max_batch
+        windows — identical inputs per window, fewer and larger kernels."""
+        groups = []
+        for b0 in range(w0, w1, self.batch_size):
+            b1 = min(w1, b0 + self.batch_size)
+            key = (int(plan.fbank_n[b0:b1].max()), int(plan.lens[b0:b1].max()))
+            if groups and groups[-1][2:] == key and b1 - groups[-1][0] <= self.model.max_batch:
+                groups[-1] = (groups[-1][0], b1) + key
+            else:
+                groups.append((b0, b1) + key)
+        return groups
 
     @staticmethod
     def average(logits, plan: WindowPlan):

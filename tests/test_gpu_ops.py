@@ -40,7 +40,7 @@ def _rel_err(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("M,K,N,act", [(1, 32, 4, 0), (257, 384, 1152, 0), (1000, 1536, 384, 1),
                                        (64, 512, 4, 0), (333, 96, 130, 3), (4096, 256, 2048, 2)])
 def test_linear(gpu, precision, M, K, N, act):
@@ -61,13 +61,16 @@ def test_linear(gpu, precision, M, K, N, act):
         assert _rel_err(out.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("B,T,Cin,Cout,k,stride,pad,dil", [
     (2, 299, 128, 32, 3, 1, 2, 2),     # CAM dense k3 dilation 2
     (3, 598, 320, 128, 5, 2, 2, 1),    # TDNN
     (2, 299, 512, 192, 5, 2, 2, 1),    # speech_down_or_up
     (2, 100, 1536, 384, 5, 1, 2, 1),   # backend_down
     (1, 7, 64, 40, 1, 1, 0, 1),
+    (3, 150, 384, 768, 1, 1, 0, 1),    # conformer pointwise
+    (2, 50, 64, 130, 3, 1, 1, 1),      # Cin % 64 == 0 multi-tap, N tail
+    (2, 299, 136, 32, 1, 1, 0, 1),     # K tail (136 = 2*64 + 8)
 ])
 def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
     g = torch.Generator().manual_seed(B * T + Cout)
@@ -86,7 +89,7 @@ def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
         assert _rel_err(out.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("B,H,W,sh,kh,pad", [(2, 80, 50, 2, 3, 1), (1, 40, 37, 1, 3, 1), (2, 40, 21, 2, 1, 0),
                                              (2, 20, 33, 2, 3, 1)])
 def test_conv2d(gpu, precision, B, H, W, sh, kh, pad):
