@@ -65,3 +65,20 @@ def meeting_posteriors(sd, cfg, wav, ts, n_labels, shift=1, batch_size=64, n_rea
         for t, v in res[i].items():
             out[i, t] = np.mean(v)
     return out
+
+
+def overlap_average(logits, starts, lens, n_labels):
+    """(n_win, NS, chunk) logits -> (NS, n_labels): sigmoid (model.py:945-946), then
+    the per-frame np.mean over covering windows in window order (infer.py:90-94)."""
+    prob = torch.sigmoid(torch.from_numpy(np.ascontiguousarray(logits, np.float32))).numpy()
+    ns = prob.shape[1]
+    res = [defaultdict(list) for _ in range(ns)]
+    for w, (s, l) in enumerate(zip(starts, lens)):
+        for t in range(int(l)):
+            for i in range(ns):
+                res[i][int(s) + t].append(prob[w, i, t])
+    out = np.full((ns, n_labels), np.nan, np.float32)
+    for i in range(ns):
+        for t, v in res[i].items():
+            out[i, t] = np.mean(v)
+    return out
