@@ -77,6 +77,59 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_s
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 int sd_tsvad_destroy(sd_tsvad* h);
 
+/* ------------------------------------------------------------------ EEND-EDA
+ * Replaces TransformerEdaModel (speaker_diarization/eend_eda/models.py:161-347) and
+ * EendEdaModel (models.py:466-652) with LstmEncoderDedecoderAttractor
+ * (eend_eda/encoder_decoder_attractor.py:8-59):
+ *   construction  infer_eda.py:50-71;  load_state_dict  infer_eda.py:88
+ *   infer(src, infer_num_speakers, max_n_speakers, attractor_threshold)  models.py:297 / 601
+ * The forward computes everything before speaker selection; the selection
+ * (sort / first-n / threshold on the max_n_speakers probs) stays on the host.
+ */
+typedef struct sd_eda sd_eda;
+
+typedef struct {
+  int variant;          /* 0: TransformerEdaModel; 1: EendEdaModel(encoder_type "transformer");
+                           2: EendEdaModel(encoder_type "conformer") (infer_eda.py model_type ConformerEda) */
+  int in_size;          /* 345 = (2*context_size+1) * 23                                     */
+  int n_units;          /* hidden_size (256)                                                  */
+  int n_heads;          /* transformer_encoder_n_heads (4)                                    */
+  int n_layers;         /* transformer_encoder_n_layers (2 / 4)                               */
+  int dim_feedforward;  /* 2048 (never passed by infer_eda.py)                                */
+  int max_seqs;         /* workspace: sequences (chunks) per forward                          */
+  int max_frames;       /* workspace: frames per sequence (chunk_size, 2000)                  */
+  int max_n_speakers;   /* attractors decoded (15)                                            */
+  int precision;        /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate            */
+} sd_eda_config;
+
+int sd_eda_create(const sd_eda_config* cfg, sd_eda** out);
+int sd_eda_set_param(sd_eda* h, const char* name, const float* host_data, const int64_t* shape, int ndim);
+int sd_eda_finalize(sd_eda* h);
+/* Row stride (floats) the input features must have: in_size rounded up to 8 (352). */
+int sd_eda_input_stride(const sd_eda* h);
+/* feats: device (S, T, ld_feats) f32 (pad columns finite, e.g. zero or pad_sequence's -1);
+ * lengths: device int32 (S) frames per sequence (ilens); key_len: device int32 (S) attention
+ * key mask or NULL (the transformer variants attend to padded frames, models.py:216-226;
+ * the conformer variant masks by ilens, :527-528); perm: device int32 (S, T), row s holds
+ * torch.randperm(lengths[s]) drawn by the caller on the host CPU generator (models.py:229-233).
+ * probs: device (S, max_n_speakers) attractor existence probabilities;
+ * act: device (S, T, max_n_speakers - 1) = sigmoid(emb · attractors[:-1]ᵀ). */
+int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S, int T, const int* lengths,
+                   const int* key_len, const int* perm, float* probs, float* act, void* stream);
+int64_t sd_eda_device_bytes(const sd_eda* h);
+int sd_eda_destroy(sd_eda* h);
+
+/* feature.stft + feature.transform('logmel23_mn' | 'logmel23') + feature.splice + [::subsampling]
+ * (speaker_diarization/feature.py:155-184, 56-73, 130-152; eend_eda/infer_eda.py:94-98).
+ * wav: device f32 (n_samples) (soundfile values, computed in float64 like the reference);
+ * n_frames: STFT frames = 1 + n_samples/frame_shift, minus one when divisible (feature.py:176-184);
+ * mel_fb: device (n_mels, n_fft/2+1) Slaney mel (librosa.filters.mel, host-built);
+ * mean_norm: 1 for logmel23_mn; work: device float64 (n_frames*n_mels + n_mels);
+ * out: device (ceil(n_frames/subsampling), ld_out) f32, columns >= (2c+1)*n_mels zeroed. */
+int sd_eend_features(const float* wav, int64_t n_samples, int frame_size, int frame_shift, int n_frames,
+                     const float* mel_fb, int n_mels, int mean_norm, int context_size, int subsampling,
+                     double* work, float* out, int ld_out, void* stream);
+
 /* ------------------------------------------------------------------ frontend
  * FBank.__call__ (ts_vad2/ts_vad_dataset.py:29-56) over a whole recording at
  * dither 0: wav (n_samples) device fp32 in [-1,1), in_scale = 32768.

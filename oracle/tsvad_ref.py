@@ -106,9 +106,10 @@ def transformer_layer(x, sd, p, nh, eps=1e-5, causal_mask=None):
     return F.layer_norm(x + h, (e,), sd[p + "norm2.weight"], sd[p + "norm2.bias"], eps)
 
 
-def conformer(x, lengths, sd, p, num_layers=6, nh=8, eps=1e-5):
+def conformer(x, lengths, sd, p, num_layers=6, nh=8, eps=1e-5, group_norm=True):
     """torchaudio.models.Conformer(input_dim, num_heads, ffn_dim, num_layers,
-    depthwise_conv_kernel_size=31, use_group_norm=True).forward in eval —
+    depthwise_conv_kernel_size=31, use_group_norm).forward in eval (GroupNorm(1, D)
+    for TS-VAD ots_vad, model.py:259-267; BatchNorm1d for EendEdaModel, models.py:502) —
     restated from the published torchaudio 2.5.1 algorithm (parity unpinned:
     torchaudio is not installed here).  x: (B, T, D) -> (B, T, D)."""
     B, T, E = x.shape
@@ -135,7 +136,12 @@ def conformer(x, lengths, sd, p, num_layers=6, nh=8, eps=1e-5):
         k = sd[q + "conv_module.sequential.2.weight"].shape[-1]
         c = F.conv1d(c, sd[q + "conv_module.sequential.2.weight"], sd[q + "conv_module.sequential.2.bias"],
                      padding=(k - 1) // 2, groups=E)
-        c = F.group_norm(c, 1, sd[q + "conv_module.sequential.3.weight"], sd[q + "conv_module.sequential.3.bias"], eps)
+        n = q + "conv_module.sequential.3."
+        if group_norm:
+            c = F.group_norm(c, 1, sd[n + "weight"], sd[n + "bias"], eps)
+        else:
+            c = F.batch_norm(c, sd[n + "running_mean"], sd[n + "running_var"], sd[n + "weight"], sd[n + "bias"],
+                             False, 0.0, eps)
         c = F.silu(c)
         c = F.conv1d(c, sd[q + "conv_module.sequential.5.weight"], sd[q + "conv_module.sequential.5.bias"])
         x = c.permute(2, 0, 1) + r

@@ -40,6 +40,21 @@ class TsvadConfig(ctypes.Structure):
     ]
 
 
+class EdaConfig(ctypes.Structure):
+    _fields_ = [
+        ("variant", c_int),
+        ("in_size", c_int),
+        ("n_units", c_int),
+        ("n_heads", c_int),
+        ("n_layers", c_int),
+        ("dim_feedforward", c_int),
+        ("max_seqs", c_int),
+        ("max_frames", c_int),
+        ("max_n_speakers", c_int),
+        ("precision", c_int),
+    ]
+
+
 _SIGS = {
     "sd_last_error": (c_char_p, []),
     "sd_version": (c_int, []),
@@ -53,6 +68,16 @@ _SIGS = {
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
+    "sd_eda_create": (c_int, [POINTER(EdaConfig), POINTER(c_void_p)]),
+    "sd_eda_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_eda_finalize": (c_int, [c_void_p]),
+    "sd_eda_input_stride": (c_int, [c_void_p]),
+    "sd_eda_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "sd_eda_device_bytes": (c_int64, [c_void_p]),
+    "sd_eda_destroy": (c_int, [c_void_p]),
+    "sd_eend_features": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                 c_void_p, c_void_p, c_int, c_void_p]),
     "sd_fbank_kaldi": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "sd_window_cmn": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sd_overlap_average": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,

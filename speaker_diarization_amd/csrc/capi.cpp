@@ -10,6 +10,7 @@
 
 #include "kernels.h"
 #include "prof.h"
+#include "eda.h"
 #include "tsvad.h"
 
 namespace sd {
@@ -20,6 +21,10 @@ const char* last_error() { return g_err.c_str(); }
 
 struct sd_tsvad {
   std::unique_ptr<sd::TsvadModel> model;
+};
+
+struct sd_eda {
+  std::unique_ptr<sd::EdaModel> model;
 };
 
 namespace {
@@ -129,6 +134,84 @@ int64_t sd_tsvad_device_bytes(const sd_tsvad* h) { return h ? (int64_t)h->model-
 
 int sd_tsvad_destroy(sd_tsvad* h) {
   return guard([&] { delete h; });
+}
+
+int sd_eda_create(const sd_eda_config* c, sd_eda** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->variant >= 0 && c->variant <= 2, sd::kErrInvalid, "Unknown model type.");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->max_seqs > 0 && c->max_frames > 0 && c->max_n_speakers >= 2, sd::kErrInvalid,
+             "bad workspace sizes");
+    SD_CHECK(c->n_units > 0 && c->n_heads > 0 && c->n_units % c->n_heads == 0, sd::kErrInvalid,
+             "n_units must be divisible by n_heads");
+    sd::EdaConfig t;
+    t.variant = c->variant;
+    t.in_size = c->in_size;
+    t.n_units = c->n_units;
+    t.n_heads = c->n_heads;
+    t.n_layers = c->n_layers;
+    t.dim_feedforward = c->dim_feedforward;
+    t.max_seqs = c->max_seqs;
+    t.max_frames = c->max_frames;
+    t.max_n_speakers = c->max_n_speakers;
+    t.bf16 = c->precision == 1;
+    auto* h = new sd_eda;
+    h->model.reset(new sd::EdaModel(t));
+    *out = h;
+  });
+}
+
+int sd_eda_set_param(sd_eda* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_eda_finalize(sd_eda* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_eda_input_stride(const sd_eda* h) { return h && h->model->finalized() ? h->model->in_ld() : 0; }
+
+int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S_, int T, const int* lengths,
+                   const int* key_len, const int* perm, float* probs, float* act, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && feats && lengths && perm && probs && act, sd::kErrInvalid, "null argument");
+    h->model->forward(feats, ld_feats, S_, T, lengths, key_len, perm, probs, act, S(stream));
+  });
+}
+
+int64_t sd_eda_device_bytes(const sd_eda* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
+
+int sd_eda_destroy(sd_eda* h) {
+  return guard([&] { delete h; });
+}
+
+int sd_eend_features(const float* wav, int64_t n_samples, int frame_size, int frame_shift, int n_frames,
+                     const float* mel_fb, int n_mels, int mean_norm, int context_size, int subsampling,
+                     double* work, float* out, int ld_out, void* stream) {
+  return guard([&] {
+    SD_CHECK(wav && mel_fb && work && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(frame_size > 0 && frame_shift > 0 && subsampling > 0 && context_size >= 0, sd::kErrInvalid,
+             "bad frame geometry");
+    const int n_fft = 1 << (32 - __builtin_clz((unsigned)(frame_size - 1)));
+    const int64_t nf_max = 1 + n_samples / frame_shift;
+    SD_CHECK(n_frames >= 1 && n_frames <= nf_max, sd::kErrInvalid, "n_frames exceeds the STFT frames");
+    hipStream_t st = S(stream);
+    double* lm = work;
+    double* mean = work + (int64_t)n_frames * n_mels;
+    sd::stft_logmel(wav, n_samples, n_frames, n_fft, frame_shift, frame_size, mel_fb, n_mels, lm, st);
+    if (mean_norm) sd::col_mean(lm, n_frames, n_mels, mean, st);
+    const int n_out = (n_frames + subsampling - 1) / subsampling;
+    sd::splice_subsample(lm, n_frames, n_mels, mean_norm ? mean : nullptr, context_size, subsampling, n_out,
+                         out, ld_out, st);
+  });
 }
 
 int sd_fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,

@@ -1,0 +1,252 @@
+// EEND frontend + EDA glue kernels for gfx950.
+//
+// Frontend (speaker_diarization/feature.py, called from eend_eda/infer_eda.py:94-98
+// and fs_eend/dataset.py):
+//   stft_logmel  librosa.stft(n_fft, win_length, hop, 'hann', center=True,
+//                pad_mode='constant') of the float64 wav (soundfile reads f64,
+//                kaldi_data.py:82) -> |Y|^2 · mel^T (float64) -> log10(max(·, 1e-10)).
+//                One wavefront per frame; the n_fft-point complex FFT runs in
+//                float64 in LDS (the reference computes this stage in float64).
+//   col_mean     per-recording mean of each mel channel ('logmel23_mn', feature.py:72).
+//   splice       (x - mean) cast to f32, ±context zero-padded splice (feature.py:130-152)
+//                and [::subsampling], written as 352-wide rows (in_size 345 + zero pad)
+//                so the first Linear's K is a multiple of the MFMA k-step.
+// EDA (eend_eda/models.py, encoder_decoder_attractor.py):
+//   gather_rows       the frame shuffle emb[randperm(T)] (models.py:229-233)
+//   fill_rows         decoder LSTM gates for the zero inputs = b_ih + b_hh (:50)
+//   attractor_scores  sigmoid(linear(att)) (:53-58) and sigmoid(emb · att[:-1]ᵀ)
+//                     (models.py:324-331)
+#include <cmath>
+
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kMaxMels = 64;
+
+template <int LOG2N>
+__global__ __launch_bounds__(256) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
+                                                          int n_frames, int hop, int win_len,
+                                                          const float* __restrict__ mel_fb, int n_mels,
+                                                          double* __restrict__ out) {
+  constexpr int N = 1 << LOG2N;
+  constexpr int BINS = N / 2 + 1;
+  constexpr int FPB = 4;
+  __shared__ double2 buf[FPB][N];
+  __shared__ double2 tw[N / 2];
+  __shared__ double pw[FPB][BINS + 1];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int f = blockIdx.x * FPB + w;
+  const bool active = f < n_frames;
+  for (int k = threadIdx.x; k < N / 2; k += blockDim.x) {
+    double s, c;
+    sincospi(-2.0 * (double)k / (double)N, &s, &c);
+    tw[k] = make_double2(c, s);
+  }
+  // Frame f covers padded samples [f*hop, f*hop + N) of the wav zero-padded by N/2;
+  // the periodic Hann window of win_len sits at offset (N - win_len)/2.
+  const int lpad = (N - win_len) / 2;
+  const int64_t base = (int64_t)f * hop - N / 2 + lpad;
+  for (int n = lane; n < N; n += 64) {
+    double v = 0.0;
+    const int j = n - lpad;
+    if (active && j >= 0 && j < win_len) {
+      const int64_t gi = base + j;
+      if (gi >= 0 && gi < n_samples) {
+        double s, c;
+        sincospi(2.0 * (double)j / (double)win_len, &s, &c);
+        v = (double)wav[gi] * (0.5 - 0.5 * c);
+      }
+    }
+    const int r = (int)(__brev((unsigned)n) >> (32 - LOG2N));
+    buf[w][r] = make_double2(v, 0.0);
+  }
+  __syncthreads();
+  for (int half = 1; half < N; half <<= 1) {
+    const int tstride = N / (2 * half);
+    for (int bfly = lane; bfly < N / 2; bfly += 64) {
+      const int grp = bfly / half, pos = bfly % half;
+      const int i0 = grp * 2 * half + pos, i1 = i0 + half;
+      const double2 t0 = tw[pos * tstride];
+      const double2 a = buf[w][i0], b = buf[w][i1];
+      const double2 t = make_double2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
+      buf[w][i0] = make_double2(a.x + t.x, a.y + t.y);
+      buf[w][i1] = make_double2(a.x - t.x, a.y - t.y);
+    }
+    __syncthreads();
+  }
+  for (int k = lane; k < BINS; k += 64) {
+    const double2 c = buf[w][k];
+    pw[w][k] = c.x * c.x + c.y * c.y;
+  }
+  __syncthreads();
+  if (!active) return;
+  for (int m = lane; m < n_mels; m += 64) {
+    const float* fr = mel_fb + (int64_t)m * BINS;
+    double acc = 0.0;
+    for (int k = 0; k < BINS; ++k) acc = fma((double)fr[k], pw[w][k], acc);
+    out[(int64_t)f * n_mels + m] = log10(fmax(acc, 1e-10));
+  }
+}
+
+// One block per mel channel: fixed-order strided partial sums + tree -> deterministic.
+__global__ __launch_bounds__(256) void col_mean_kernel(const double* __restrict__ x, int rows, int cols,
+                                                       double* __restrict__ mean) {
+  __shared__ double red[256];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < rows; r += 256) s += x[(int64_t)r * cols + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mean[c] = red[0] / (double)rows;
+}
+
+__global__ __launch_bounds__(256) void splice_kernel(const double* __restrict__ lm, int n_frames, int n_mels,
+                                                     const double* __restrict__ mean, int context, int sub,
+                                                     int n_out, float* __restrict__ out, int ld_out) {
+  const int r = blockIdx.x;
+  if (r >= n_out) return;
+  const int width = (2 * context + 1) * n_mels;
+  for (int i = threadIdx.x; i < ld_out; i += blockDim.x) {
+    float v = 0.f;
+    if (i < width) {
+      const int c = i / n_mels, m = i % n_mels;
+      const int f = r * sub + c - context;
+      if (f >= 0 && f < n_frames) {
+        const double y = lm[(int64_t)f * n_mels + m] - (mean ? mean[m] : 0.0);
+        v = (float)y;
+      }
+    }
+    out[(int64_t)r * ld_out + i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ x, int T, int D,
+                                                          const int* __restrict__ perm,
+                                                          const int* __restrict__ lengths,
+                                                          float* __restrict__ y) {
+  const int s = blockIdx.y, t = blockIdx.x;
+  const int len = lengths ? lengths[s] : T;
+  const int src = t < len ? perm[(int64_t)s * T + t] : t;
+  const float* xr = x + ((int64_t)s * T + src) * D;
+  float* yr = y + ((int64_t)s * T + t) * D;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) yr[i] = xr[i];
+}
+
+__global__ __launch_bounds__(256) void fill_rows_kernel(const float* __restrict__ row, int D, int rows,
+                                                        float* __restrict__ y) {
+  const int64_t n = (int64_t)rows * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = row[i % D];
+}
+
+constexpr int kScoreRows = 32;
+
+// One block per (sequence, 32 frames): attractors of the sequence in LDS.
+__global__ __launch_bounds__(256) void attractor_scores_kernel(
+    const float* __restrict__ emb, int T, int E, const float* __restrict__ att, int n_att,
+    const float* __restrict__ lw, const float* __restrict__ lb, float* __restrict__ probs,
+    float* __restrict__ act) {
+  extern __shared__ float sm[];
+  const int ES = E + 1;
+  float* as = sm;                       // [n_att][ES]
+  float* es = as + n_att * ES;          // [kScoreRows][ES]
+  const int s = blockIdx.y;
+  const int t0 = blockIdx.x * kScoreRows;
+  const float* a = att + (int64_t)s * n_att * E;
+  for (int i = threadIdx.x; i < n_att * E; i += blockDim.x) as[(i / E) * ES + i % E] = a[i];
+  const int nr = min(kScoreRows, T - t0);
+  for (int i = threadIdx.x; i < nr * E; i += blockDim.x)
+    es[(i / E) * ES + i % E] = emb[((int64_t)s * T + t0 + i / E) * E + i % E];
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < n_att) {
+    const int j = threadIdx.x;
+    float acc = 0.f;
+    for (int k = 0; k < E; ++k) acc = fmaf(as[j * ES + k], lw[k], acc);
+    acc += lb[0];
+    probs[(int64_t)s * n_att + j] = 1.f / (1.f + expf(-acc));
+  }
+  const int ns = n_att - 1;
+  for (int i = threadIdx.x; i < nr * ns; i += blockDim.x) {
+    const int r = i / ns, j = i % ns;
+    float acc = 0.f;
+    for (int k = 0; k < E; ++k) acc = fmaf(es[r * ES + k], as[j * ES + k], acc);
+    act[((int64_t)s * T + t0 + r) * ns + j] = 1.f / (1.f + expf(-acc));
+  }
+}
+
+}  // namespace
+
+void stft_logmel(const float* wav, int64_t n_samples, int n_frames, int n_fft, int hop, int win_len,
+                 const float* mel_fb, int n_mels, double* out, hipStream_t st) {
+  SD_CHECK(n_fft == 256 || n_fft == 512, kErrInvalid, "stft: n_fft must be 256 or 512");
+  SD_CHECK(win_len > 0 && win_len <= n_fft && hop > 0, kErrInvalid, "stft: bad frame_size/frame_shift");
+  SD_CHECK(n_mels > 0 && n_mels <= kMaxMels, kErrInvalid, "stft: n_mels out of range");
+  if (n_frames <= 0) return;
+  ProfScope prof("stft_logmel", 5.0 * n_fft * std::log2((double)n_fft) * n_frames,
+                 4.0 * (double)n_frames * hop + 8.0 * n_frames * n_mels, st);
+  const dim3 grid(cdiv(n_frames, 4));
+  if (n_fft == 512)
+    hipLaunchKernelGGL(stft_logmel_kernel<9>, grid, dim3(256), 0, st, wav, n_samples, n_frames, hop, win_len,
+                       mel_fb, n_mels, out);
+  else
+    hipLaunchKernelGGL(stft_logmel_kernel<8>, grid, dim3(256), 0, st, wav, n_samples, n_frames, hop, win_len,
+                       mel_fb, n_mels, out);
+  SD_LAUNCH_CHECK();
+}
+
+void col_mean(const double* x, int rows, int cols, double* mean, hipStream_t st) {
+  SD_CHECK(rows > 0, kErrInvalid, "col_mean: empty input");
+  hipLaunchKernelGGL(col_mean_kernel, dim3(cols), dim3(256), 0, st, x, rows, cols, mean);
+  SD_LAUNCH_CHECK();
+}
+
+void splice_subsample(const double* lm, int n_frames, int n_mels, const double* mean, int context,
+                      int sub, int n_out, float* out, int ld_out, hipStream_t st) {
+  SD_CHECK(ld_out >= (2 * context + 1) * n_mels, kErrInvalid, "splice: ld_out < spliced width");
+  if (n_out <= 0) return;
+  ProfScope prof("splice", 0.0, 4.0 * (double)n_out * ld_out + 8.0 * n_frames * n_mels, st);
+  hipLaunchKernelGGL(splice_kernel, dim3(n_out), dim3(128), 0, st, lm, n_frames, n_mels, mean, context, sub,
+                     n_out, out, ld_out);
+  SD_LAUNCH_CHECK();
+}
+
+void gather_rows(const float* x, int S, int T, int D, const int* perm, const int* lengths, float* y,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(T, S), dim3(64), 0, st, x, T, D, perm, lengths, y);
+  SD_LAUNCH_CHECK();
+}
+
+void fill_rows(const float* row, int D, int rows, float* y, hipStream_t st) {
+  const int64_t n = (int64_t)rows * D;
+  if (n <= 0) return;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(fill_rows_kernel, dim3(blocks), dim3(256), 0, st, row, D, rows, y);
+  SD_LAUNCH_CHECK();
+}
+
+void attractor_scores(const float* emb, int S, int T, int E, const float* att, int n_att, const float* lw,
+                      const float* lb, float* probs, float* act, hipStream_t st) {
+  const size_t smem = sizeof(float) * (size_t)(n_att + kScoreRows) * (E + 1);
+  SD_CHECK(smem <= 160 * 1024, kErrInvalid, "attractor_scores: too many attractors for LDS");
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attractor_scores_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  ProfScope prof("attractor_scores", 2.0 * S * T * E * (n_att - 1), 4.0 * S * T * (E + n_att), st);
+  hipLaunchKernelGGL(attractor_scores_kernel, dim3(cdiv(T, kScoreRows), S), dim3(256), smem, st, emb, T, E,
+                     att, n_att, lw, lb, probs, act);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

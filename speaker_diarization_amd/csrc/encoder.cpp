@@ -1,0 +1,170 @@
+// Shared encoder layers (see encoder.h).
+#include "encoder.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace sd {
+
+ConvGemmArgs lin(Tens A, int M, int lda, const PackedW& w, const float* bias, Tens out, int ldo) {
+  ConvGemmArgs p = linear_args(A.p, M, w.K, lda, w.w, w.N, out.p, ldo);
+  p.a_bf16 = A.bf;
+  p.out_bf16 = out.bf;
+  p.beta = bias;
+  return p;
+}
+
+const float* LayerLoader::up(const std::string& key) { return arena.upload(ps.get(key).data); }
+
+PackedW LayerLoader::packed(const std::string& key, float mult) {
+  int N, Cin, kh, kw;
+  auto w = ps.pack(key, N, Cin, kh, kw, mult);
+  return upload_packed(arena, w, N, Cin, kh, kw, bf16);
+}
+
+ConvL LayerLoader::linear(const std::string& prefix, float mult) {
+  ConvL L;
+  L.w = packed(prefix + ".weight", mult);
+  // nn.Linear / Conv1d(bias=True): the bias key is required (strict load).
+  std::vector<float> b = ps.get(prefix + ".bias").data;
+  for (auto& v : b) v *= mult;
+  L.beta = arena.upload(b);
+  return L;
+}
+
+TransformerL LayerLoader::transformer(const std::string& p) {
+  // torch/nn/modules/transformer.py TransformerEncoderLayer; nn.MultiheadAttention
+  // keeps its packed projection as in_proj_weight / in_proj_bias.
+  TransformerL L;
+  L.in_proj = packed(p + ".self_attn.in_proj_weight");
+  L.in_b = up(p + ".self_attn.in_proj_bias");
+  ConvL o = linear(p + ".self_attn.out_proj");
+  L.out_proj = o.w; L.out_b = o.beta;
+  ConvL l1 = linear(p + ".linear1");
+  L.l1 = l1.w; L.b1 = l1.beta;
+  ConvL l2 = linear(p + ".linear2");
+  L.l2 = l2.w; L.b2 = l2.beta;
+  L.n1g = up(p + ".norm1.weight");
+  L.n1b = up(p + ".norm1.bias");
+  L.n2g = up(p + ".norm2.weight");
+  L.n2b = up(p + ".norm2.bias");
+  return L;
+}
+
+ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
+  // torchaudio/models/conformer.py (2.5.1): ffn1 -> self-attn -> conv module -> ffn2 -> LN.
+  ConformerL L;
+  L.group_norm = group_norm;
+  // ffn: sequential.0 LayerNorm, .1 Linear, .2 SiLU, .4 Linear; residual x*0.5 folded into .4 (exact).
+  L.f1_lng = up(p + ".ffn1.sequential.0.weight"); L.f1_lnb = up(p + ".ffn1.sequential.0.bias");
+  { ConvL a = linear(p + ".ffn1.sequential.1"); L.f1_w1 = a.w; L.f1_b1 = a.beta; }
+  { ConvL a = linear(p + ".ffn1.sequential.4", 0.5f); L.f1_w2 = a.w; L.f1_b2 = a.beta; }
+  L.at_lng = up(p + ".self_attn_layer_norm.weight"); L.at_lnb = up(p + ".self_attn_layer_norm.bias");
+  L.in_proj = packed(p + ".self_attn.in_proj_weight");
+  L.in_b = up(p + ".self_attn.in_proj_bias");
+  { ConvL a = linear(p + ".self_attn.out_proj"); L.out_proj = a.w; L.out_b = a.beta; }
+  L.cv_lng = up(p + ".conv_module.layer_norm.weight"); L.cv_lnb = up(p + ".conv_module.layer_norm.bias");
+  { ConvL a = linear(p + ".conv_module.sequential.0"); L.pw1 = a.w; L.pw1_b = a.beta; }
+  {
+    const HostTensor& dw = ps.get(p + ".conv_module.sequential.2.weight");  // (C, 1, k)
+    SD_CHECK(dw.shape.size() == 3 && dw.shape[1] == 1, kErrParam, "depthwise conv weight shape");
+    std::vector<float> w = dw.data, b = ps.get(p + ".conv_module.sequential.2.bias").data;
+    if (group_norm) {
+      L.gn_g = up(p + ".conv_module.sequential.3.weight");
+      L.gn_b = up(p + ".conv_module.sequential.3.bias");
+    } else {
+      // eval BatchNorm1d after the depthwise conv: fold into its weight/bias.
+      std::vector<float> s, h;
+      ps.bn_fold(p + ".conv_module.sequential.3", s, h);
+      const int64_t C = dw.shape[0], k = dw.shape[2];
+      for (int64_t c = 0; c < C; ++c) {
+        for (int64_t j = 0; j < k; ++j) w[c * k + j] *= s[c];
+        b[c] = b[c] * s[c] + h[c];
+      }
+      L.gn_g = L.gn_b = nullptr;
+    }
+    L.dw_w = arena.upload(w);
+    L.dw_b = arena.upload(b);
+  }
+  { ConvL a = linear(p + ".conv_module.sequential.5"); L.pw2 = a.w; L.pw2_b = a.beta; }
+  L.f2_lng = up(p + ".ffn2.sequential.0.weight"); L.f2_lnb = up(p + ".ffn2.sequential.0.bias");
+  { ConvL a = linear(p + ".ffn2.sequential.1"); L.f2_w1 = a.w; L.f2_b1 = a.beta; }
+  { ConvL a = linear(p + ".ffn2.sequential.4", 0.5f); L.f2_w2 = a.w; L.f2_b2 = a.beta; }
+  L.fin_g = up(p + ".final_layer_norm.weight"); L.fin_b = up(p + ".final_layer_norm.bias");
+  return L;
+}
+
+void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
+                     const EncoderWork& w, hipStream_t st) {
+  // nn.TransformerEncoderLayer (post-LN): X fp32 residual stream; QKV/AO/H bf16 in bf16 mode.
+  const int rows = S * T;
+  const bool bf = w.bf16;
+  const Tens x{X, false}, y{w.Y, false}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
+  conv_gemm(lin(x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
+  AttnArgs a;
+  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
+  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
+  a.key_len = key_len;
+  attention(a, bf, st);
+  ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, y, E);
+  p.res = X; p.res_ld = E;
+  conv_gemm(p, bf, st);
+  layernorm(w.Y, rows, E, E, L.n1g, L.n1b, 1e-5f, X, E, false, st);
+  p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
+  p.act = kActRelu;
+  conv_gemm(p, bf, st);
+  p = lin(h, rows, L.l1.N, L.l2, L.b2, y, E);
+  p.res = X; p.res_ld = E;
+  conv_gemm(p, bf, st);
+  layernorm(w.Y, rows, E, E, L.n2g, L.n2b, 1e-5f, X, E, false, st);
+}
+
+void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
+                   const int* key_len, const EncoderWork& w, hipStream_t st) {
+  // torchaudio ConformerLayer: X fp32 residual stream; LN outputs / GEMM-only intermediates bf16.
+  const int rows = S * T;
+  const bool bf = w.bf16;
+  const Tens x{X, false}, y{w.Y, bf}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
+  auto ffn = [&](const float* lng, const float* lnb, const PackedW& w1, const float* b1,
+                 const PackedW& w2, const float* b2) {
+    layernorm(X, rows, E, E, lng, lnb, 1e-5f, y.p, E, bf, st);
+    ConvGemmArgs p = lin(y, rows, E, w1, b1, h, w1.N);
+    p.act = kActSilu;
+    conv_gemm(p, bf, st);
+    p = lin(h, rows, w1.N, w2, b2, x, E);   // weights pre-scaled by 0.5
+    p.res = X; p.res_ld = E;
+    conv_gemm(p, bf, st);
+  };
+  ffn(L.f1_lng, L.f1_lnb, L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
+  // self attention block (key_padding_mask from lengths)
+  layernorm(X, rows, E, E, L.at_lng, L.at_lnb, 1e-5f, y.p, E, bf, st);
+  conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
+  AttnArgs a;
+  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
+  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
+  a.key_len = key_len;
+  attention(a, bf, st);
+  {
+    ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, x, E);
+    p.res = X; p.res_ld = E;
+    conv_gemm(p, bf, st);
+  }
+  // convolution module (no padding mask in torchaudio's conv module)
+  layernorm(X, rows, E, E, L.cv_lng, L.cv_lnb, 1e-5f, y.p, E, bf, st);
+  conv_gemm(lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E), bf, st);
+  if (L.group_norm) {
+    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, w.partial, false, bf, st);
+    groupnorm_silu(ao.p, S, T, E, w.partial, L.gn_g, L.gn_b, 1e-5f, bf, st);
+  } else {
+    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, nullptr, true, bf, st);
+  }
+  {
+    ConvGemmArgs p = lin(ao, rows, E, L.pw2, L.pw2_b, x, E);
+    p.res = X; p.res_ld = E;
+    conv_gemm(p, bf, st);
+  }
+  ffn(L.f2_lng, L.f2_lnb, L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
+  layernorm(X, rows, E, E, L.fin_g, L.fin_b, 1e-5f, X, E, false, st);
+}
+
+}  // namespace sd

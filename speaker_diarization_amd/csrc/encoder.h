@@ -1,0 +1,79 @@
+// Encoder layers shared by the TS-VAD, EEND-EDA and EEND runners:
+// nn.TransformerEncoderLayer (post-LN, ReLU) and torchaudio's ConformerLayer,
+// with their state_dict loaders.  Activations are channel-last token streams
+// (S*T, E); the residual stream X stays fp32, GEMM-only intermediates are bf16
+// in bf16 mode.
+#pragma once
+#include <string>
+#include "kernels.h"
+#include "params.h"
+
+namespace sd {
+
+// Activation tensors: fp32, or bf16 bits when the flag is set.
+struct Tens {
+  void* p;
+  bool bf;
+};
+inline Tens act_at(const Tens& a, int64_t elems) {
+  return Tens{static_cast<char*>(a.p) + elems * (a.bf ? 2 : 4), a.bf};
+}
+
+// Linear on a row-major activation: out (M, w.N) with row stride ldo.
+ConvGemmArgs lin(Tens A, int M, int lda, const PackedW& w, const float* bias, Tens out, int ldo);
+
+struct ConvL {
+  PackedW w;
+  const float* alpha = nullptr;
+  const float* beta = nullptr;
+  const float* pre_s = nullptr;
+  const float* pre_h = nullptr;
+};
+
+struct TransformerL {     // nn.TransformerEncoderLayer, post-LN, ReLU FFN
+  PackedW in_proj, out_proj, l1, l2;
+  const float *in_b, *out_b, *b1, *b2, *n1g, *n1b, *n2g, *n2b;
+};
+
+struct ConformerL {       // torchaudio.models.conformer.ConformerLayer (conv after attention)
+  const float *f1_lng, *f1_lnb, *f1_b1, *f1_b2;
+  PackedW f1_w1, f1_w2;
+  const float *at_lng, *at_lnb, *in_b, *out_b;
+  PackedW in_proj, out_proj;
+  const float *cv_lng, *cv_lnb, *pw1_b, *dw_w, *dw_b, *gn_g, *gn_b, *pw2_b;
+  bool group_norm = true;  // false: BatchNorm1d folded into dw_w / dw_b, SiLU fused into the dwconv
+  PackedW pw1, pw2;
+  const float *f2_lng, *f2_lnb, *f2_b1, *f2_b2;
+  PackedW f2_w1, f2_w2;
+  const float *fin_g, *fin_b;
+};
+
+// Reads reference state_dict entries (strict: every key it touches is marked used).
+struct LayerLoader {
+  ParamStore& ps;
+  DeviceArena& arena;
+  bool bf16;
+  const float* up(const std::string& key);
+  PackedW packed(const std::string& key, float mult = 1.f);
+  ConvL linear(const std::string& prefix, float mult = 1.f);   // weight + required bias
+  TransformerL transformer(const std::string& prefix);
+  ConformerL conformer(const std::string& prefix, bool group_norm);
+};
+
+// Scratch for one encoder layer over up to `rows` tokens.
+struct EncoderWork {
+  float* Y;        // rows * E (fp32)
+  float* QKV;      // rows * 3E
+  float* AO;       // rows * E
+  float* H;        // rows * max(ffn, 2E)
+  float* partial;  // S * cdiv(E, 64) * 2
+  bool bf16;
+};
+
+// X: (S*T, E) fp32, updated in place.  key_len: device int32 (S) or nullptr.
+void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
+                     const EncoderWork& w, hipStream_t st);
+void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
+                   const int* key_len, const EncoderWork& w, hipStream_t st);
+
+}  // namespace sd

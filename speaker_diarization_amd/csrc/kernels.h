@@ -98,10 +98,11 @@ void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out
 // ---------------------------------------------------------------- conformer conv module
 // GLU over channel pairs (a = x[:, c], g = x[:, C + c]) followed by a depthwise
 // conv over time (kernel k, pad (k-1)/2, with bias).  x: (S, T, 2C); y: (S, T, C).
-// Also writes per (sequence, channel-block) partial sums for GroupNorm(1, C).
+// Writes per (sequence, channel-block) partial sums for GroupNorm(1, C), or with
+// fused_silu (BatchNorm already folded into w/bias) stores SiLU(y) and no partials.
 void glu_dwconv(const void* x, int S, int T, int C, const float* w /*C x k*/,
-                const float* bias, int k, void* y, float* partial /*S x nblk x 2*/, bool io_bf16,
-                hipStream_t st);
+                const float* bias, int k, void* y, float* partial /*S x nblk x 2*/, bool fused_silu,
+                bool io_bf16, hipStream_t st);
 // GroupNorm(num_groups=1) over (T, C) of each sequence, affine, then SiLU (in place).
 void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
                     const float* b, float eps, bool io_bf16, hipStream_t st);
@@ -142,4 +143,20 @@ void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* 
 
 namespace sd {
 void f32_to_bf16(const float* x, int64_t n, void* y, hipStream_t st);
+
+// ---------------------------------------------------------------- eend frontend + EDA glue (eend.hip)
+// librosa-style centred STFT (float64) -> log10 mel power: out (n_frames, n_mels) float64.
+void stft_logmel(const float* wav, int64_t n_samples, int n_frames, int n_fft, int hop, int win_len,
+                 const float* mel_fb /*(n_mels, n_fft/2+1)*/, int n_mels, double* out, hipStream_t st);
+void col_mean(const double* x, int rows, int cols, double* mean, hipStream_t st);
+// out (n_out, ld_out) f32: row r = splice of frame r*sub (±context, zero pad), minus mean (nullable).
+void splice_subsample(const double* lm, int n_frames, int n_mels, const double* mean, int context, int sub,
+                      int n_out, float* out, int ld_out, hipStream_t st);
+// y[s, t] = x[s, perm[s, t]] for t < lengths[s], else x[s, t].  Rows of D floats.
+void gather_rows(const float* x, int S, int T, int D, const int* perm, const int* lengths, float* y,
+                 hipStream_t st);
+void fill_rows(const float* row, int D, int rows, float* y, hipStream_t st);
+// probs (S, n_att) = sigmoid(att · lw + lb); act (S, T, n_att-1) = sigmoid(emb · att[:-1]ᵀ).
+void attractor_scores(const float* emb, int S, int T, int E, const float* att, int n_att, const float* lw,
+                      const float* lb, float* probs, float* act, hipStream_t st);
 }  // namespace sd

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias, int k,
                                                          act_t<BF>* __restrict__ y,
-                                                         float* __restrict__ partial) {
+                                                         float* __restrict__ partial, int fused_silu) {
   extern __shared__ float sm[];
   const int pad = (k - 1) / 2;
   const int s = blockIdx.y;
@@ -381,12 +381,14 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
       for (int tt = tq; tt < kDwTT && t0 + tt < T; tt += 4) {
         float acc = bv;
         for (int j = 0; j < k; ++j) acc = fmaf(wsm[cc * k + j], g[(tt + j) * kDwCB + cc], acc);
+        if (fused_silu) acc = acc / (1.f + expf(-acc));
         st_act(ys, (int64_t)(t0 + tt) * C + c0 + cc, acc);
         lsum += acc;
         lsq += acc * acc;
       }
     }
   }
+  if (fused_silu) return;   // uniform across the block
   red[0][threadIdx.x] = lsum;
   red[1][threadIdx.x] = lsq;
   __syncthreads();
@@ -404,17 +406,18 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
 }
 
 void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
-                void* y, float* partial, bool io_bf16, hipStream_t st) {
+                void* y, float* partial, bool fused_silu, bool io_bf16, hipStream_t st) {
+  SD_CHECK(fused_silu || partial, kErrInvalid, "glu_dwconv: GroupNorm partials buffer required");
   dim3 grid(cdiv(C, kDwCB), S);
   size_t smem = sizeof(float) * ((kDwTT + k - 1) * kDwCB + kDwCB * k);
   ProfScope prof("glu_dwconv", 2.0 * S * T * C * k, 4.0 * S * T * 3.0 * C, st);
   if (io_bf16)
     hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), smem, st,
                        reinterpret_cast<const uint16_t*>(x), T, C, w, bias, k, reinterpret_cast<uint16_t*>(y),
-                       partial);
+                       partial, (int)fused_silu);
   else
     hipLaunchKernelGGL(glu_dwconv_kernel<false>, grid, dim3(256), smem, st, reinterpret_cast<const float*>(x),
-                       T, C, w, bias, k, reinterpret_cast<float*>(y), partial);
+                       T, C, w, bias, k, reinterpret_cast<float*>(y), partial, (int)fused_silu);
   SD_LAUNCH_CHECK();
 }
 

@@ -20,15 +20,6 @@ namespace sd {
 
 namespace {
 
-// Activation tensors: fp32, or bf16 bits when the flag is set.
-struct Tens {
-  void* p;
-  bool bf;
-};
-inline Tens act_at(const Tens& a, int64_t elems) {
-  return Tens{static_cast<char*>(a.p) + elems * (a.bf ? 2 : 4), a.bf};
-}
-
 ConvGemmArgs conv1d(Tens in, int B, int T, int lda, const ConvL& L, int stride, int pad, int dil, Tens out,
                     int ldo) {
   ConvGemmArgs p;
@@ -58,14 +49,6 @@ ConvGemmArgs conv2d(Tens in, int B, int H, int W, const ConvL& L, int sh, int sw
   return p;
 }
 
-ConvGemmArgs lin(Tens A, int M, int lda, const PackedW& w, const float* bias, Tens out, int ldo) {
-  ConvGemmArgs p = linear_args(A.p, M, w.K, lda, w.w, w.N, out.p, ldo);
-  p.a_bf16 = A.bf;
-  p.out_bf16 = out.bf;
-  p.beta = bias;
-  return p;
-}
-
 }  // namespace
 
 ConvL TsvadModel::conv_bn(const std::string& wname, const std::string& bn, const std::string& bias) {
@@ -81,71 +64,6 @@ ConvL TsvadModel::conv_bn(const std::string& wname, const std::string& bn, const
   } else if (!bias.empty()) {
     L.beta = arena_.upload(ps_.get(bias).data);
   }
-  return L;
-}
-
-ConvL TsvadModel::linear(const std::string& prefix, float mult) {
-  ConvL L;
-  int N, Cin, kh, kw;
-  auto w = ps_.pack(prefix + ".weight", N, Cin, kh, kw, mult);
-  L.w = upload_packed(arena_, w, N, Cin, kh, kw, cfg_.bf16);
-  {  // nn.Linear / the conformer's Conv1d(bias=True): the bias key is required (strict load)
-    std::vector<float> b = ps_.get(prefix + ".bias").data;
-    for (auto& v : b) v *= mult;
-    L.beta = arena_.upload(b);
-  }
-  return L;
-}
-
-TransformerL TsvadModel::transformer(const std::string& p) {
-  TransformerL L;
-  // nn.MultiheadAttention names its packed projection in_proj_weight / in_proj_bias.
-  int N, Cin, kh, kw;
-  auto w = ps_.pack(p + ".self_attn.in_proj_weight", N, Cin, kh, kw);
-  L.in_proj = upload_packed(arena_, w, N, Cin, kh, kw, cfg_.bf16);
-  L.in_b = arena_.upload(ps_.get(p + ".self_attn.in_proj_bias").data);
-  ConvL o = linear(p + ".self_attn.out_proj");
-  L.out_proj = o.w; L.out_b = o.beta;
-  ConvL l1 = linear(p + ".linear1");
-  L.l1 = l1.w; L.b1 = l1.beta;
-  ConvL l2 = linear(p + ".linear2");
-  L.l2 = l2.w; L.b2 = l2.beta;
-  L.n1g = arena_.upload(ps_.get(p + ".norm1.weight").data);
-  L.n1b = arena_.upload(ps_.get(p + ".norm1.bias").data);
-  L.n2g = arena_.upload(ps_.get(p + ".norm2.weight").data);
-  L.n2b = arena_.upload(ps_.get(p + ".norm2.bias").data);
-  return L;
-}
-
-ConformerL TsvadModel::conformer(const std::string& p) {
-  ConformerL L;
-  auto up = [&](const std::string& k) { return arena_.upload(ps_.get(k).data); };
-  // ffn1: sequential.0 LayerNorm, .1 Linear, .2 SiLU, .4 Linear; residual x*0.5 (exact in bf16).
-  L.f1_lng = up(p + ".ffn1.sequential.0.weight"); L.f1_lnb = up(p + ".ffn1.sequential.0.bias");
-  { ConvL a = linear(p + ".ffn1.sequential.1"); L.f1_w1 = a.w; L.f1_b1 = a.beta; }
-  { ConvL a = linear(p + ".ffn1.sequential.4", 0.5f); L.f1_w2 = a.w; L.f1_b2 = a.beta; }
-  L.at_lng = up(p + ".self_attn_layer_norm.weight"); L.at_lnb = up(p + ".self_attn_layer_norm.bias");
-  {
-    int N, Cin, kh, kw;
-    auto w = ps_.pack(p + ".self_attn.in_proj_weight", N, Cin, kh, kw);
-    L.in_proj = upload_packed(arena_, w, N, Cin, kh, kw, cfg_.bf16);
-    L.in_b = up(p + ".self_attn.in_proj_bias");
-  }
-  { ConvL a = linear(p + ".self_attn.out_proj"); L.out_proj = a.w; L.out_b = a.beta; }
-  L.cv_lng = up(p + ".conv_module.layer_norm.weight"); L.cv_lnb = up(p + ".conv_module.layer_norm.bias");
-  { ConvL a = linear(p + ".conv_module.sequential.0"); L.pw1 = a.w; L.pw1_b = a.beta; }
-  {
-    const HostTensor& dw = ps_.get(p + ".conv_module.sequential.2.weight");  // (C, 1, k)
-    SD_CHECK(dw.shape.size() == 3 && dw.shape[1] == 1, kErrParam, "depthwise conv weight shape");
-    L.dw_w = arena_.upload(dw.data);
-    L.dw_b = up(p + ".conv_module.sequential.2.bias");
-  }
-  L.gn_g = up(p + ".conv_module.sequential.3.weight"); L.gn_b = up(p + ".conv_module.sequential.3.bias");
-  { ConvL a = linear(p + ".conv_module.sequential.5"); L.pw2 = a.w; L.pw2_b = a.beta; }
-  L.f2_lng = up(p + ".ffn2.sequential.0.weight"); L.f2_lnb = up(p + ".ffn2.sequential.0.bias");
-  { ConvL a = linear(p + ".ffn2.sequential.1"); L.f2_w1 = a.w; L.f2_b1 = a.beta; }
-  { ConvL a = linear(p + ".ffn2.sequential.4", 0.5f); L.f2_w2 = a.w; L.f2_b2 = a.beta; }
-  L.fin_g = up(p + ".final_layer_norm.weight"); L.fin_b = up(p + ".final_layer_norm.bias");
   return L;
 }
 
@@ -232,16 +150,16 @@ void TsvadModel::finalize() {
     pe_len_ = (int)pe.shape[0];
     pe_ = arena_.upload(pe.data);
     for (int i = 0; i < cfg_.num_transformer_layer; ++i) {
-      single_.push_back(transformer("single_backend.layers." + std::to_string(i)));
-      multi_.push_back(transformer("multi_backend.layers." + std::to_string(i)));
+      single_.push_back(loader().transformer("single_backend.layers." + std::to_string(i)));
+      multi_.push_back(loader().transformer("multi_backend.layers." + std::to_string(i)));
     }
     backend_down_ = conv_bn("backend_down.0.weight", "backend_down.1.bn", "backend_down.0.bias");
-    fc_ = linear("fc");
+    fc_ = loader().linear("fc");
   } else {
     gsp_w_ = arena_.upload(ps_.get("gsp_fc.weight").data);
     gsp_b_ = arena_.upload(ps_.get("gsp_fc.bias").data);
     for (int i = 0; i < cfg_.conformer_layers; ++i)
-      conf_.push_back(conformer("single_backend.conformer_layers." + std::to_string(i)));
+      conf_.push_back(loader().conformer("single_backend.conformer_layers." + std::to_string(i), true));
     // BiLSTM: stack both directions' W_ih, fold b_ih + b_hh.
     const int H = cfg_.lstm_hidden;
     std::vector<float> wih, bias, whh;
@@ -259,7 +177,7 @@ void TsvadModel::finalize() {
     lstm_ih_ = upload_packed(arena_, wih, 8 * H, (int)wi0.shape[1], 1, 1, cfg_.bf16);
     lstm_b_ = arena_.upload(bias);
     lstm_hh_ = arena_.upload(whh);
-    fc_ = linear("fc");
+    fc_ = loader().linear("fc");
   }
   auto extra = ps_.unused();
   if (!extra.empty()) {
@@ -297,73 +215,6 @@ void TsvadModel::alloc_workspace() {
   X2_ = ws(rows * E);
   partial_ = ws(Bm * NS * ((E + 63) / 64) * 2);
   lstm_work_ = ws(3 * 2 * Bm * cfg_.lstm_hidden);
-}
-
-void TsvadModel::run_transformer(const TransformerL& L, float* X, int S, int T, int nh, hipStream_t st) {
-  // nn.TransformerEncoderLayer (post-LN): X fp32 residual stream; QKV/AO/H bf16 in bf16 mode.
-  const int E = cfg_.embed_dim;
-  const int rows = S * T;
-  const bool bf = cfg_.bf16;
-  const Tens x{X, false}, y{Y_, false}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
-  conv_gemm(lin(x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
-  AttnArgs a;
-  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
-  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
-  attention(a, bf, st);
-  ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, y, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, bf, st);
-  layernorm(Y_, rows, E, E, L.n1g, L.n1b, 1e-5f, X, E, false, st);
-  p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
-  p.act = kActRelu;
-  conv_gemm(p, bf, st);
-  p = lin(h, rows, L.l1.N, L.l2, L.b2, y, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, bf, st);
-  layernorm(Y_, rows, E, E, L.n2g, L.n2b, 1e-5f, X, E, false, st);
-}
-
-void TsvadModel::run_conformer(const ConformerL& L, float* X, int S, int T, hipStream_t st) {
-  // torchaudio ConformerLayer: X fp32 residual stream; LN outputs / GEMM-only intermediates bf16.
-  const int E = cfg_.embed_dim;
-  const int rows = S * T;
-  const bool bf = cfg_.bf16;
-  const Tens x{X, false}, y{Y_, bf}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
-  auto ffn = [&](const float* lng, const float* lnb, const PackedW& w1, const float* b1,
-                 const PackedW& w2, const float* b2) {
-    layernorm(X, rows, E, E, lng, lnb, 1e-5f, y.p, E, bf, st);
-    ConvGemmArgs p = lin(y, rows, E, w1, b1, h, w1.N);
-    p.act = kActSilu;
-    conv_gemm(p, bf, st);
-    p = lin(h, rows, w1.N, w2, b2, x, E);   // weights pre-scaled by 0.5
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
-  };
-  ffn(L.f1_lng, L.f1_lnb, L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
-  // self attention block
-  layernorm(X, rows, E, E, L.at_lng, L.at_lnb, 1e-5f, y.p, E, bf, st);
-  conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
-  AttnArgs a;
-  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = cfg_.conformer_heads; a.ld_qkv = 3 * E;
-  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / cfg_.conformer_heads));
-  attention(a, bf, st);
-  {
-    ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, x, E);
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
-  }
-  // convolution module
-  layernorm(X, rows, E, E, L.cv_lng, L.cv_lnb, 1e-5f, y.p, E, bf, st);
-  conv_gemm(lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E), bf, st);
-  glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, cfg_.conformer_kernel, ao.p, partial_, bf, st);
-  groupnorm_silu(ao.p, S, T, E, partial_, L.gn_g, L.gn_b, 1e-5f, bf, st);
-  {
-    ConvGemmArgs p = lin(ao, rows, E, L.pw2, L.pw2_b, x, E);
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
-  }
-  ffn(L.f2_lng, L.f2_lnb, L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
-  layernorm(X, rows, E, E, L.fin_g, L.fin_b, 1e-5f, X, E, false, st);
 }
 
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
@@ -461,13 +312,13 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_CHECK(Tl <= pe_len_, kErrShape, "label length exceeds positional-encoding max_len");
     // Per-speaker encoder over S = B*NS sequences (model.py:869-879).
     build_speaker_input(ts, mix_, SE, T3, B, NS, Tl, SE, pe_, X_, st);
-    for (const auto& L : single_) run_transformer(L, X_, S, Tl, cfg_.num_attention_head, st);
+    for (const auto& L : single_) run_transformer(L, X_, S, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st);
     speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     ConvGemmArgs p = conv1d(Tens{X2_, bf}, B, Tl, NS * E, backend_down_, 1, 2, 1, Tens{X_, false}, E);
     p.act = kActRelu;
     conv_gemm(p, bf, st);
     add_pe(X_, B * Tl, Tl, E, E, pe_, st);
-    for (const auto& L : multi_) run_transformer(L, X_, B, Tl, cfg_.num_attention_head, st);
+    for (const auto& L : multi_) run_transformer(L, X_, B, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st);
     ConvGemmArgs f = conv1d(Tens{X_, false}, B, Tl, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
@@ -476,7 +327,8 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
              "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
     gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
     build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
-    for (const auto& L : conf_) run_conformer(L, X_, S, Tl, st);
+    for (const auto& L : conf_)
+      run_conformer(L, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
     speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);

@@ -1,8 +1,7 @@
 // Native TS-VAD inference runner (owns folded weights + workspace).
 #pragma once
 #include <vector>
-#include "kernels.h"
-#include "params.h"
+#include "encoder.h"
 
 namespace sd {
 
@@ -25,37 +24,12 @@ struct TsvadConfig {
   int lstm_hidden = 256;
 };
 
-struct ConvL {
-  PackedW w;
-  const float* alpha = nullptr;
-  const float* beta = nullptr;
-  const float* pre_s = nullptr;
-  const float* pre_h = nullptr;
-};
-
 struct DenseL {
   ConvL bottleneck;       // nonlinear1 (prologue) -> linear1 (1x1) -> nonlinear2 (epilogue, relu)
   ConvL local;            // cam_layer.linear_local (k3, dilation)
   int dil = 1;
   const float *c1w = nullptr, *c1b = nullptr, *c2w = nullptr, *c2b = nullptr;
   int c1 = 0, c2 = 0;
-};
-
-struct TransformerL {     // nn.TransformerEncoderLayer, post-LN, ReLU FFN
-  PackedW in_proj, out_proj, l1, l2;
-  const float *in_b, *out_b, *b1, *b2, *n1g, *n1b, *n2g, *n2b;
-};
-
-struct ConformerL {       // torchaudio.models.conformer.ConformerLayer (conv after attention)
-  const float *f1_lng, *f1_lnb, *f1_b1, *f1_b2;
-  PackedW f1_w1, f1_w2;
-  const float *at_lng, *at_lnb, *in_b, *out_b;
-  PackedW in_proj, out_proj;
-  const float *cv_lng, *cv_lnb, *pw1_b, *dw_w, *dw_b, *gn_g, *gn_b, *pw2_b;
-  PackedW pw1, pw2;
-  const float *f2_lng, *f2_lnb, *f2_b1, *f2_b2;
-  PackedW f2_w1, f2_w2;
-  const float *fin_g, *fin_b;
 };
 
 class TsvadModel {
@@ -71,11 +45,8 @@ class TsvadModel {
 
  private:
   ConvL conv_bn(const std::string& wname, const std::string& bn, const std::string& bias = "");
-  ConvL linear(const std::string& prefix, float mult = 1.f);
-  TransformerL transformer(const std::string& prefix);
-  ConformerL conformer(const std::string& prefix);
-  void run_transformer(const TransformerL& L, float* X, int S, int T, int nh, hipStream_t st);
-  void run_conformer(const ConformerL& L, float* X, int S, int T, hipStream_t st);
+  LayerLoader loader() { return LayerLoader{ps_, arena_, cfg_.bf16}; }
+  EncoderWork enc_work() const { return EncoderWork{Y_, QKV_, AO_, H_, partial_, cfg_.bf16}; }
   void alloc_workspace();
   float* ws(size_t n) { return static_cast<float*>(arena_.alloc(n * sizeof(float))); }
 

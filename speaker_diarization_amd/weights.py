@@ -276,3 +276,94 @@ def unwrap_checkpoint(obj, kind: str = "tsvad"):
         sd = obj["state_dict"]
         return OrderedDict((k[len("model."):] if k.startswith("model.") else k, v) for k, v in sd.items())
     return obj
+
+
+# ----------------------------------------------------------------------------- EEND-EDA
+@dataclass
+class EDAConfig:
+    """Constructor arguments of TransformerEdaModel (eend_eda/models.py:161) and
+    EendEdaModel (models.py:466-467) as eend_eda/infer_eda.py:50-71 passes them."""
+    model_type: str = "TransformerEda"     # "TransformerEda" | "EendEda" | "ConformerEda"
+    n_speakers: int = 2
+    in_size: int = 345                     # feature.get_input_dim(…, context 7, logmel23*) = 15 * 23
+    n_heads: int = 4
+    n_units: int = 256
+    n_layers: int = 2
+    dim_feedforward: int = 2048            # never passed by infer_eda.py (SURVEY §9.8)
+    encoder_type: str = "transformer"      # EendEda: "transformer" | "conformer"
+
+    @property
+    def variant(self) -> int:
+        """0: TransformerEdaModel, 1: EendEdaModel(transformer), 2: EendEdaModel(conformer)."""
+        if self.model_type == "TransformerEda":
+            return 0
+        if self.model_type == "ConformerEda":
+            return 2
+        if self.model_type == "EendEda":
+            if self.encoder_type == "transformer":
+                return 1
+            if self.encoder_type == "conformer":
+                return 2
+            raise NotImplementedError(f"encoder_type not support {self.encoder_type}!!!")
+        raise ValueError("Unknown model type.")
+
+
+def _lstm(k: list, p: str, i: int, h: int):
+    k.append((p + "weight_ih_l0", (4 * h, i), "lstm"))
+    k.append((p + "weight_hh_l0", (4 * h, h), "lstm"))
+    k.append((p + "bias_ih_l0", (4 * h,), "lstm"))
+    k.append((p + "bias_hh_l0", (4 * h,), "lstm"))
+
+
+def eda_layout(cfg: EDAConfig) -> list:
+    """Key layout of TransformerEdaModel / EendEdaModel (eend_eda/models.py:161-210,
+    466-512; encoder_decoder_attractor.py:8-16)."""
+    e, v = cfg.n_units, cfg.variant
+    k: list = []
+    inp, norm = ("encoder", "encoder_norm") if v == 0 else ("linear", "linear_norm")
+    k.append((inp + ".weight", (e, cfg.in_size), "linear"))
+    k.append((inp + ".bias", (e,), "small"))
+    _ln(k, norm, e)
+    if v in (0, 1):
+        root = "transformer_encoder" if v == 0 else "encoder"
+        for i in range(cfg.n_layers):
+            _tfm(k, f"{root}.layers.{i}.", e, cfg.dim_feedforward)
+    else:
+        for i in range(cfg.n_layers):
+            p = f"encoder.conformer_layers.{i}."
+            _conformer_layer(k, p, e, cfg.dim_feedforward, 31, group_norm=False)
+    _lstm(k, "eda.encoder.", e, e)
+    _lstm(k, "eda.decoder.", e, e)
+    k.append(("eda.linear.weight", (1, e), "linear"))
+    k.append(("eda.linear.bias", (1,), "small"))
+    return k
+
+
+def _conformer_layer(k: list, p: str, e: int, ffn: int, kernel: int, group_norm: bool):
+    """torchaudio.models.conformer.ConformerLayer parameter names (2.5.1)."""
+    for f in ("ffn1", "ffn2"):
+        _ln(k, p + f + ".sequential.0", e)
+        k.append((p + f + ".sequential.1.weight", (ffn, e), "linear"))
+        k.append((p + f + ".sequential.1.bias", (ffn,), "small"))
+        k.append((p + f + ".sequential.4.weight", (e, ffn), "linear"))
+        k.append((p + f + ".sequential.4.bias", (e,), "small"))
+        if f == "ffn1":
+            _ln(k, p + "self_attn_layer_norm", e)
+            _mha(k, p + "self_attn.", e)
+            _ln(k, p + "conv_module.layer_norm", e)
+            k.append((p + "conv_module.sequential.0.weight", (2 * e, e, 1), "conv1d"))
+            k.append((p + "conv_module.sequential.0.bias", (2 * e,), "small"))
+            k.append((p + "conv_module.sequential.2.weight", (e, 1, kernel), "conv1d"))
+            k.append((p + "conv_module.sequential.2.bias", (e,), "small"))
+            if group_norm:
+                k.append((p + "conv_module.sequential.3.weight", (e,), "ln_w"))
+                k.append((p + "conv_module.sequential.3.bias", (e,), "small"))
+            else:
+                _bn(k, p + "conv_module.sequential.3", e)
+            k.append((p + "conv_module.sequential.5.weight", (e, e, 1), "conv1d"))
+            k.append((p + "conv_module.sequential.5.bias", (e,), "small"))
+    _ln(k, p + "final_layer_norm", e)
+
+
+def eda_state_dict(cfg: EDAConfig, seed: int = 777):
+    return synthetic_state_dict(eda_layout(cfg), seed)

@@ -98,9 +98,162 @@ def make_tsvad(name):
         sys.modules.pop(mod, None)
 
 
+# ----------------------------------------------------------------------------- EEND-EDA
+EDA_CASES = {
+    # name: (model_type, n_layers, chunk lengths, infer_num_speakers, input seed, weight seed)
+    "eda_tfm_l2": ("TransformerEda", 2, [300, 300, 157], 2, 11, 781),
+    "eda_tfm_l2_thr": ("TransformerEda", 2, [256, 99], None, 14, 784),
+    "eda_eend_l4": ("EendEda", 4, [240, 240, 99], 3, 12, 782),
+    "eda_conformer_l2": ("ConformerEda", 2, [200, 77], None, 13, 783),
+}
+
+
+def eda_inputs(lens, in_size=345, seed=11):
+    rng = np.random.default_rng(seed)
+    return [rng.standard_normal((n, in_size)).astype(np.float32) for n in lens]
+
+
+def _import_eda():
+    from oracle.torchaudio_conformer import Conformer
+    install_stubs(Conformer)
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from speaker_diarization.eend_eda import models as eda_models
+    return eda_models
+
+
+def make_eda(name):
+    import torch
+    from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
+
+    mtype, L, lens, nspk, iseed, wseed = EDA_CASES[name]
+    M = _import_eda()
+    cfg = EDAConfig(model_type=mtype, n_layers=L)
+    torch.manual_seed(777)     # infer_eda.py:39-43, before construction
+    if mtype == "TransformerEda":
+        m = M.TransformerEdaModel(n_speakers=2, in_size=345, n_units=256, n_heads=4, n_layers=L, has_pos=False)
+    else:
+        m = M.EendEdaModel(n_speakers=2, in_size=345, n_units=256, n_heads=4, n_layers=L,
+                           encoder_type="conformer" if mtype == "ConformerEda" else "transformer", eda_type="lstm")
+    m.eval()
+    m.load_state_dict(to_torch(eda_state_dict(cfg, seed=wseed)), strict=True)
+    xs = eda_inputs(lens, seed=iseed)
+    perms, cap = [], {}
+    orig_randperm = torch.randperm
+
+    def rec_randperm(n, *a, **k):
+        p = orig_randperm(n, *a, **k)
+        perms.append(p.clone())
+        return p
+
+    orig_emb = m.forward_embedding
+
+    def emb_hook(src):
+        r = orig_emb(src)
+        cap["emb"] = r[1]
+        return r
+
+    m.forward_embedding = emb_hook
+    m.eda.register_forward_hook(lambda mod, inp, out: cap.__setitem__("eda", out))
+    T = max(lens)
+    act = np.zeros((len(lens), T, 14), np.float32)
+    probs = np.zeros((len(lens), 15), np.float32)
+    ys, index_error = [], np.zeros(len(lens), np.int64)
+    torch.randperm = rec_randperm
+    try:
+        with torch.no_grad():
+            for i, x in enumerate(xs):     # one chunk per infer() call, infer_eda.py:99-112
+                try:
+                    y = m.infer([torch.from_numpy(x)], infer_num_speakers=nspk, max_n_speakers=15,
+                                attractor_threshold=0.5)
+                    ys.append(y[0].numpy())
+                except IndexError:           # models.py:338-339
+                    index_error[i] = 1
+                    ys.append(np.zeros((lens[i], 0), np.float32))
+                att, pr = cap["eda"]
+                act[i, : lens[i]] = torch.sigmoid(torch.bmm(cap["emb"], att[:, :-1, :].permute(0, 2, 1)))[0].numpy()
+                probs[i] = pr[0].numpy()
+    finally:
+        torch.randperm = orig_randperm
+    nsel = np.array([y.shape[1] for y in ys], np.int64)
+    out = dict(lens=np.array(lens, np.int64), perms=np.concatenate([p.numpy() for p in perms]).astype(np.int64),
+               act=act, probs=probs, nsel=nsel, index_error=index_error,
+               ys=np.concatenate([y.reshape(-1) for y in ys]).astype(np.float32),
+               n_layers=np.int64(L), input_seed=np.int64(iseed), weight_seed=np.int64(wseed),
+               infer_num_speakers=np.int64(-1 if nspk is None else nspk))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, "perm0", perms[0][:8].tolist(), "nsel", nsel.tolist(), "index_error", index_error.tolist())
+
+
+def make_eda_batch(name="eda_tfm_batch"):
+    """One infer() call on a 2-element list of different lengths: pad_sequence(-1)
+    and no key mask (models.py:216-225) — the reference's B>1 semantics."""
+    import torch
+    from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
+    M = _import_eda()
+    cfg = EDAConfig(model_type="TransformerEda", n_layers=2)
+    torch.manual_seed(777)
+    m = M.TransformerEdaModel(n_speakers=2, in_size=345, n_units=256, n_heads=4, n_layers=2, has_pos=False)
+    m.eval()
+    m.load_state_dict(to_torch(eda_state_dict(cfg, seed=785)), strict=True)
+    lens = [180, 131]
+    xs = eda_inputs(lens, seed=15)
+    cap = {}
+    m.eda.register_forward_hook(lambda mod, inp, out: cap.__setitem__("eda", out))
+    with torch.no_grad():
+        ys = m.infer([torch.from_numpy(x) for x in xs], infer_num_speakers=None, max_n_speakers=15,
+                     attractor_threshold=0.5)
+    out = dict(lens=np.array(lens, np.int64), probs=torch.stack(cap["eda"][1]).numpy(),
+               nsel=np.array([y.shape[1] for y in ys], np.int64),
+               ys=np.concatenate([y.numpy().reshape(-1) for y in ys]).astype(np.float32))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["nsel"])
+
+
+# ----------------------------------------------------------------------------- feature.py glue
+FEATURE_CASES = {
+    # name: (n_samples, sample_rate, transform, frame_size, frame_shift, context, subsampling, seed)
+    "feat_logmel23_mn_16k": (48123, 16000, "logmel23_mn", 400, 160, 7, 10, 21),
+    "feat_logmel23_mn_16k_div": (48000, 16000, "logmel23_mn", 400, 160, 7, 10, 22),
+}
+
+
+def feature_wav(n, seed):
+    rng = np.random.default_rng(seed)
+    # int16-valued samples / 32768 like soundfile's float64 read (kaldi_data.py:82)
+    return (np.round(rng.standard_normal(n) * 3000).clip(-32768, 32767) / 32768.0).astype(np.float64)
+
+
+def make_feature(name):
+    from oracle import eend_ref
+    install_stubs()
+    lib = sys.modules["librosa"]
+    lib.stft = lambda y, n_fft, win_length, hop_length: eend_ref.librosa_stft(y, n_fft, hop_length, win_length)
+    lib.filters = types.SimpleNamespace(mel=lambda sr, n_fft, n_mels: eend_ref.slaney_mel(sr, n_fft, n_mels))
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from speaker_diarization import feature
+    n, sr, tr, fs, fsh, ctx, sub, seed = FEATURE_CASES[name]
+    wav = feature_wav(n, seed)
+    Y = feature.stft(wav, fs, fsh)
+    Y = feature.transform(Y, transform_type=tr, sample_rate=sr)
+    Y = feature.splice(Y, context_size=ctx)
+    Y = np.ascontiguousarray(Y[::sub])
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), feats=Y.astype(np.float32), seed=np.int64(seed),
+                        n_samples=np.int64(n))
+    print(name, Y.shape)
+
+
 if __name__ == "__main__":
     import torch
     torch.set_num_threads(8)
-    names = sys.argv[1:] or list(TSVAD_CASES)
+    names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES))
     for n in names:
-        make_tsvad(n)
+        if n in TSVAD_CASES:
+            make_tsvad(n)
+        elif n in EDA_CASES:
+            make_eda(n)
+        elif n == "eda_tfm_batch":
+            make_eda_batch(n)
+        else:
+            make_feature(n)

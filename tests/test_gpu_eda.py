@@ -1,0 +1,154 @@
+"""EEND-EDA on the GPU (through libsdiar's C ABI) against the reference goldens
+and the CPU oracle.  Tolerances: fp32 1e-3 (north_star), bf16 3e-2."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import eend_ref
+from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, infer_recording
+from speaker_diarization_amd.eend_eda.models import EendEdaModel, TransformerEdaModel
+from speaker_diarization_amd.feature import eend_features
+from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
+from tests.golden.make_golden import EDA_CASES, FEATURE_CASES, eda_inputs, feature_wav
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FP32_ATOL = 1e-3
+BF16_ATOL = 3e-2
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz")))
+
+
+def _model(mtype, L, wseed, precision="fp32", **kw):
+    torch.manual_seed(777)
+    if mtype == "TransformerEda":
+        m = TransformerEdaModel(n_speakers=2, in_size=345, n_heads=4, n_units=256, n_layers=L, has_pos=False,
+                                precision=precision, **kw)
+    else:
+        m = EendEdaModel(n_speakers=2, in_size=345, n_heads=4, n_units=256, n_layers=L,
+                         encoder_type="conformer" if mtype == "ConformerEda" else "transformer",
+                         precision=precision, **kw)
+    cfg = EDAConfig(model_type=mtype, n_layers=L)
+    m.load_state_dict(to_torch(eda_state_dict(cfg, seed=wseed)))
+    return m
+
+
+@pytest.mark.parametrize("name", list(FEATURE_CASES))
+def test_eend_features_match_oracle(gpu, name):
+    n, sr, tr, fs, fsh, ctx, sub, seed = FEATURE_CASES[name]
+    wav = feature_wav(n, seed)
+    got = eend_features(torch.from_numpy(wav.astype(np.float32)).cuda(), sr, fs, fsh, tr, ctx, sub)
+    got = got.cpu().numpy()
+    g = _load(name)["feats"]
+    assert np.all(got[:, 345:] == 0)
+    np.testing.assert_allclose(got[:, :345], g, atol=1e-5, rtol=0)
+
+
+def test_eend_features_real_length_and_bad_transform(gpu):
+    wav = torch.from_numpy(feature_wav(16000 * 7 + 37, 5).astype(np.float32)).cuda()
+    got = eend_features(wav).cpu().numpy()[:, :345]
+    ref = eend_ref.features(feature_wav(16000 * 7 + 37, 5))
+    np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0)
+    with pytest.raises(ValueError, match="Unknown transform_type"):
+        eend_features(wav, transform_type="logmel40")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(EDA_CASES))
+def test_eda_forward_matches_golden(gpu, name, precision):
+    mtype, L, lens, nspk, iseed, wseed = EDA_CASES[name]
+    g = _load(name)
+    m = _model(mtype, L, wseed, precision)
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    xs = eda_inputs(lens, seed=iseed)
+    offs = np.cumsum([0] + lens)
+    for i, x in enumerate(xs):
+        feats, ilens = m._pad_src([torch.from_numpy(x)])
+        perm = torch.from_numpy(g["perms"][offs[i]:offs[i + 1]])
+        act, probs = m.forward_infer(feats, ilens, [perm], 15, key_len=ilens if mtype == "ConformerEda" else None)
+        np.testing.assert_allclose(probs[0].cpu().numpy(), g["probs"][i], atol=tol)
+        np.testing.assert_allclose(act[0].cpu().numpy(), g["act"][i, : lens[i]], atol=tol)
+
+
+@pytest.mark.parametrize("name", list(EDA_CASES))
+def test_eda_infer_seeded_matches_reference_selection(gpu, name):
+    """Seeded construction + one infer() per chunk reproduces the reference's
+    permutations, selection and the TransformerEda IndexError quirk."""
+    mtype, L, lens, nspk, iseed, wseed = EDA_CASES[name]
+    g = _load(name)
+    m = _model(mtype, L, wseed)
+    xs = eda_inputs(lens, seed=iseed)
+    ys_ref = g["ys"]
+    off = 0
+    for i, x in enumerate(xs):
+        if g["index_error"][i]:
+            with pytest.raises(IndexError):
+                m.infer([torch.from_numpy(x)], infer_num_speakers=nspk, max_n_speakers=15, attractor_threshold=0.5)
+            continue
+        y = m.infer([torch.from_numpy(x)], infer_num_speakers=nspk, max_n_speakers=15,
+                    attractor_threshold=0.5)[0].cpu().numpy()
+        assert y.shape == (lens[i], g["nsel"][i])
+        np.testing.assert_allclose(y.reshape(-1), ys_ref[off: off + y.size], atol=FP32_ATOL)
+        off += y.size
+
+
+def test_eda_batched_list_matches_reference(gpu):
+    g = _load("eda_tfm_batch")
+    m = _model("TransformerEda", 2, 785)
+    lens = [int(v) for v in g["lens"]]
+    xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=15)]
+    ys = m.infer(xs, infer_num_speakers=None, max_n_speakers=15, attractor_threshold=0.5)
+    assert [y.shape[1] for y in ys] == list(g["nsel"])
+    got = np.concatenate([y.cpu().numpy().reshape(-1) for y in ys])
+    np.testing.assert_allclose(got, g["ys"], atol=FP32_ATOL)
+
+
+def test_eda_strict_load_errors(gpu):
+    torch.manual_seed(0)
+    m = TransformerEdaModel(n_speakers=2, in_size=345, n_heads=4, n_units=256, n_layers=2)
+    sd = to_torch(eda_state_dict(EDAConfig(model_type="TransformerEda", n_layers=2), seed=1))
+    bad = dict(sd)
+    bad.pop("eda.linear.bias")
+    with pytest.raises(RuntimeError, match="Error"):
+        m.load_state_dict(bad)
+    bad = dict(sd)
+    bad["extra.weight"] = torch.zeros(3)
+    with pytest.raises(RuntimeError, match="Unexpected"):
+        m.load_state_dict(bad)
+    with pytest.raises(NotImplementedError):
+        EendEdaModel(2, 345, 4, 256, 2, encoder_type="mamba")
+
+
+@pytest.mark.parametrize("mtype,nspk", [("TransformerEda", None), ("EendEda", 3), ("ConformerEda", None)])
+def test_infer_recording_matches_oracle_pipeline(gpu, mtype, nspk):
+    """infer_eda.py:92-124 end to end: wav -> features -> chunks -> T_hat (chunks
+    batched on the device, permutations drawn in chunk order)."""
+    L = 2
+    wav = feature_wav(16000 * 61 + 123, 9)
+    args = EdaInferArgs(num_speakers=nspk, chunk_size=250)
+    m = _model(mtype, L, 790, max_seqs=2, max_frames=250)
+    torch.manual_seed(4242)
+    try:
+        got = infer_recording(m, torch.from_numpy(wav.astype(np.float32)).cuda(), args)
+    except ValueError as e:      # np.vstack of chunks with different speaker counts
+        got = e
+    # oracle: the reference loop, one chunk at a time
+    cfg = EDAConfig(model_type=mtype, n_layers=L)
+    sd = to_torch(eda_state_dict(cfg, seed=790))
+    Y = eend_ref.features(wav)
+    torch.manual_seed(4242)
+    outs = []
+    for s, e in eend_ref.gen_chunk_indices(len(Y), 250):
+        perm = torch.randperm(e - s)
+        act, probs = eend_ref.infer_full(sd, cfg, [torch.from_numpy(Y[s:e].copy())], [perm])
+        outs.append(eend_ref.select(act, probs, cfg.variant, nspk, 0.5)[0].numpy())
+    if len({o.shape[1] for o in outs}) > 1:
+        assert isinstance(got, ValueError)   # the reference's np.vstack raises too (infer_eda.py:120)
+        return
+    ref = np.vstack(outs)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, atol=FP32_ATOL)
