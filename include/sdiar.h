@@ -100,7 +100,11 @@ typedef struct {
   int max_frames;       /* workspace: frames per sequence (chunk_size, 2000)                  */
   int max_n_speakers;   /* attractors decoded (15)                                            */
   int precision;        /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate            */
+  int n_speakers;       /* variant 3 only: decoder outputs                                    */
 } sd_eda_config;
+/* variant 3 is the plain EEND TransformerModel (speaker_diarization/eend/models.py:17-101,
+ * called as model([chunk], activation=torch.sigmoid) from eend/eend_infer.py:69): the same
+ * handle API; lengths/perm/probs may be NULL and act receives (S, T, n_speakers) sigmoid outputs. */
 
 int sd_eda_create(const sd_eda_config* cfg, sd_eda** out);
 int sd_eda_set_param(sd_eda* h, const char* name, const float* host_data, const int64_t* shape, int ndim);
@@ -118,6 +122,43 @@ int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S, int T, co
                    const int* key_len, const int* perm, float* probs, float* act, void* stream);
 int64_t sd_eda_device_bytes(const sd_eda* h);
 int sd_eda_destroy(sd_eda* h);
+
+/* ------------------------------------------------------------------ FS-EEND
+ * Replaces OnlineTransformerDADiarization (speaker_diarization/fs_eend/fs_eend.py:20-96):
+ *   construction  fs_eend/train.py:71-75 (config/spk_onl_tfm_enc_dec_nonautoreg_infer.yaml)
+ *   test(src, ilens, max_nspks) -> (preds, emb, attractors)   fs_eend.py:79-96, called from
+ *   fs_eend/model.py:198 with max_nspks = max_speakers + 2.
+ * The causal encoder attends to all history: the path does not shard (replicas only). */
+typedef struct sd_fseend sd_fseend;
+
+typedef struct {
+  int in_size;              /* (2 * context_recp + 1) * n_mels = 345                     */
+  int n_units;              /* 256 */
+  int n_heads;              /* 4   */
+  int enc_n_layers;         /* 4   */
+  int enc_dim_feedforward;  /* 2048 (MaskedTransformerEncoderModel default)             */
+  int dec_n_layers;         /* 2: applications of the shared fusion layer               */
+  int dec_dim_feedforward;  /* 2048 */
+  int conv_delay;           /* 9 (Conv1d kernel 19, padding 9)                           */
+  int mask_delay;           /* 0 */
+  int has_mask;             /* 1: causal encoder                                          */
+  int max_seqs;             /* workspace: sequences per call                              */
+  int max_frames;           /* workspace: frames per sequence (chunk_size 10000)          */
+  int max_nspks;            /* workspace: attractor slots (max_speakers + 2 = 6)         */
+  int precision;            /* 0 fp32, 1 bf16 MFMA                                         */
+} sd_fseend_config;
+
+int sd_fseend_create(const sd_fseend_config* cfg, sd_fseend** out);
+int sd_fseend_set_param(sd_fseend* h, const char* name, const float* host_data, const int64_t* shape, int ndim);
+int sd_fseend_finalize(sd_fseend* h);
+int sd_fseend_input_stride(const sd_fseend* h);
+/* feats: device (S, T, ld_feats) f32 = pad_sequence(src, -1) (pad columns finite);
+ * ilens_host: host int32 (S); preds: device (S, T, max_nspks); emb: device (S, T, n_units) or NULL;
+ * attractors: device (S, T, max_nspks, n_units) or NULL (both L2-normalised, as test() returns). */
+int sd_fseend_test(sd_fseend* h, const float* feats, int ld_feats, int S, int T, const int* ilens_host,
+                   int max_nspks, float* preds, float* emb, float* attractors, void* stream);
+int64_t sd_fseend_device_bytes(const sd_fseend* h);
+int sd_fseend_destroy(sd_fseend* h);
 
 /* feature.stft + feature.transform('logmel23_mn' | 'logmel23') + feature.splice + [::subsampling]
  * (speaker_diarization/feature.py:155-184, 56-73, 130-152; eend_eda/infer_eda.py:94-98).

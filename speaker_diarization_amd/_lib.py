@@ -52,6 +52,26 @@ class EdaConfig(ctypes.Structure):
         ("max_frames", c_int),
         ("max_n_speakers", c_int),
         ("precision", c_int),
+        ("n_speakers", c_int),
+    ]
+
+
+class FseendConfig(ctypes.Structure):
+    _fields_ = [
+        ("in_size", c_int),
+        ("n_units", c_int),
+        ("n_heads", c_int),
+        ("enc_n_layers", c_int),
+        ("enc_dim_feedforward", c_int),
+        ("dec_n_layers", c_int),
+        ("dec_dim_feedforward", c_int),
+        ("conv_delay", c_int),
+        ("mask_delay", c_int),
+        ("has_mask", c_int),
+        ("max_seqs", c_int),
+        ("max_frames", c_int),
+        ("max_nspks", c_int),
+        ("precision", c_int),
     ]
 
 
@@ -76,6 +96,14 @@ _SIGS = {
                                c_void_p, c_void_p]),
     "sd_eda_device_bytes": (c_int64, [c_void_p]),
     "sd_eda_destroy": (c_int, [c_void_p]),
+    "sd_fseend_create": (c_int, [POINTER(FseendConfig), POINTER(c_void_p)]),
+    "sd_fseend_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_fseend_finalize": (c_int, [c_void_p]),
+    "sd_fseend_input_stride": (c_int, [c_void_p]),
+    "sd_fseend_test": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "sd_fseend_device_bytes": (c_int64, [c_void_p]),
+    "sd_fseend_destroy": (c_int, [c_void_p]),
     "sd_eend_features": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p, c_int, c_void_p]),
     "sd_fbank_kaldi": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p]),
@@ -134,6 +162,32 @@ def check(status: int, what: str = ""):
 
 def call(name: str, *args):
     check(getattr(load(), name)(*args), name)
+
+
+def create_handle(kind: str, conf, state) -> ctypes.c_void_p:
+    """sd_<kind>_create + set_param for every state_dict entry (reference key names)
+    + finalize; the handle is destroyed again if any step fails."""
+    import numpy as np
+    lib = load()
+    h = ctypes.c_void_p()
+    call(f"sd_{kind}_create", ctypes.byref(conf), ctypes.byref(h))
+    try:
+        for k, v in state.items():
+            a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+            shape = (c_int64 * max(a.ndim, 1))(*a.shape)
+            call(f"sd_{kind}_set_param", h, k.encode(), a.ctypes.data_as(c_void_p), shape, a.ndim)
+        call(f"sd_{kind}_finalize", h)
+    except Exception:
+        getattr(lib, f"sd_{kind}_destroy")(h)
+        raise
+    return h
+
+
+def host_state(state_dict) -> dict:
+    """state_dict (torch tensors or arrays) -> {key: float32 numpy} on the host."""
+    import numpy as np
+    return {k: (v.detach().cpu().float().numpy() if hasattr(v, "detach") else np.asarray(v, dtype=np.float32))
+            for k, v in state_dict.items()}
 
 
 def ptr(t) -> int:

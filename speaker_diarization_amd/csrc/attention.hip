@@ -50,14 +50,17 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int q0 = blockIdx.x * kQB + wid * 16;
   const int myq = q0 + l15;
   const int D = a.D;
-  const io_t* base = reinterpret_cast<const io_t*>(a.qkv) + (int64_t)s * T * a.ld_qkv;
+  const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
+                       (int64_t)(s % a.seq_inner) * a.seq_inner_stride;
+  const int64_t tstr = (int64_t)a.tok_stride * a.ld_qkv;   // elements between consecutive tokens
+  const io_t* base = reinterpret_cast<const io_t*>(a.qkv) + row0 * a.ld_qkv;
   const int klen = a.key_len ? min(a.key_len[s], T) : T;
 
   // Q operand (B operand of Sᵀ = K·Qᵀ), pre-scaled.
   constexpr int QN = BF16 ? HDP / 32 : HD / 4;
   typename std::conditional<BF16, bf16x8, float>::type qf[QN];
   {
-    const io_t* qr = base + (int64_t)min(myq, T - 1) * a.ld_qkv + h * HD;
+    const io_t* qr = base + (int64_t)min(myq, T - 1) * tstr + h * HD;
     const bool qv = myq < T;
     if constexpr (BF16) {
 #pragma unroll
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       int key = k0 + kr;
       float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
       if (key < T) {
-        const io_t* r = base + (int64_t)key * a.ld_qkv + h * HD + d4;
+        const io_t* r = base + (int64_t)key * tstr + h * HD + d4;
         if constexpr (IOBF) {
           uint2 k2 = *reinterpret_cast<const uint2*>(r + D);
           uint2 v2 = *reinterpret_cast<const uint2*>(r + 2 * D);
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     const int q = q0 + qi;
     if (q >= T) continue;
     const float inv = lr > 0.f ? 1.f / lr : 0.f;
-    io_t* orow = reinterpret_cast<io_t*>(a.out) + ((int64_t)s * T + q) * a.ldo + h * HD;
+    io_t* orow = reinterpret_cast<io_t*>(a.out) + (row0 + (int64_t)q * a.tok_stride) * a.ldo + h * HD;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) st_act(orow, dt * 16 + l15, o[dt][r] * inv);
   }

@@ -11,6 +11,7 @@
 #include "kernels.h"
 #include "prof.h"
 #include "eda.h"
+#include "fseend.h"
 #include "tsvad.h"
 
 namespace sd {
@@ -25,6 +26,10 @@ struct sd_tsvad {
 
 struct sd_eda {
   std::unique_ptr<sd::EdaModel> model;
+};
+
+struct sd_fseend {
+  std::unique_ptr<sd::FsEendModel> model;
 };
 
 namespace {
@@ -139,7 +144,8 @@ int sd_tsvad_destroy(sd_tsvad* h) {
 int sd_eda_create(const sd_eda_config* c, sd_eda** out) {
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
-    SD_CHECK(c->variant >= 0 && c->variant <= 2, sd::kErrInvalid, "Unknown model type.");
+    SD_CHECK(c->variant >= 0 && c->variant <= 3, sd::kErrInvalid, "Unknown model type.");
+    SD_CHECK(c->variant != 3 || c->n_speakers > 0, sd::kErrInvalid, "n_speakers must be positive");
     SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
     SD_CHECK(c->max_seqs > 0 && c->max_frames > 0 && c->max_n_speakers >= 2, sd::kErrInvalid,
              "bad workspace sizes");
@@ -155,6 +161,7 @@ int sd_eda_create(const sd_eda_config* c, sd_eda** out) {
     t.max_seqs = c->max_seqs;
     t.max_frames = c->max_frames;
     t.max_n_speakers = c->max_n_speakers;
+    t.n_speakers = c->n_speakers;
     t.bf16 = c->precision == 1;
     auto* h = new sd_eda;
     h->model.reset(new sd::EdaModel(t));
@@ -182,7 +189,7 @@ int sd_eda_input_stride(const sd_eda* h) { return h && h->model->finalized() ? h
 int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S_, int T, const int* lengths,
                    const int* key_len, const int* perm, float* probs, float* act, void* stream) {
   return guard([&] {
-    SD_CHECK(h && feats && lengths && perm && probs && act, sd::kErrInvalid, "null argument");
+    SD_CHECK(h && feats && act, sd::kErrInvalid, "null argument");
     h->model->forward(feats, ld_feats, S_, T, lengths, key_len, perm, probs, act, S(stream));
   });
 }
@@ -190,6 +197,67 @@ int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S_, int T, c
 int64_t sd_eda_device_bytes(const sd_eda* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
 
 int sd_eda_destroy(sd_eda* h) {
+  return guard([&] { delete h; });
+}
+
+int sd_fseend_create(const sd_fseend_config* c, sd_fseend** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->max_seqs > 0 && c->max_frames > 0 && c->max_nspks > 0, sd::kErrInvalid, "bad workspace sizes");
+    SD_CHECK(c->n_units > 0 && c->n_heads > 0 && c->n_units % c->n_heads == 0, sd::kErrInvalid,
+             "n_units must be divisible by n_heads");
+    SD_CHECK(c->dec_n_layers >= 1 && c->enc_n_layers >= 0 && c->mask_delay >= 0, sd::kErrInvalid,
+             "bad layer counts");
+    sd::FsEendConfig t;
+    t.in_size = c->in_size;
+    t.n_units = c->n_units;
+    t.n_heads = c->n_heads;
+    t.enc_n_layers = c->enc_n_layers;
+    t.enc_ffn = c->enc_dim_feedforward;
+    t.dec_n_layers = c->dec_n_layers;
+    t.dec_ffn = c->dec_dim_feedforward;
+    t.conv_delay = c->conv_delay;
+    t.mask_delay = c->mask_delay;
+    t.has_mask = c->has_mask;
+    t.max_seqs = c->max_seqs;
+    t.max_frames = c->max_frames;
+    t.max_nspks = c->max_nspks;
+    t.bf16 = c->precision == 1;
+    auto* h = new sd_fseend;
+    h->model.reset(new sd::FsEendModel(t));
+    *out = h;
+  });
+}
+
+int sd_fseend_set_param(sd_fseend* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_fseend_finalize(sd_fseend* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_fseend_input_stride(const sd_fseend* h) { return h && h->model->finalized() ? h->model->in_ld() : 0; }
+
+int sd_fseend_test(sd_fseend* h, const float* feats, int ld_feats, int S_, int T, const int* ilens_host,
+                   int max_nspks, float* preds, float* emb, float* attractors, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && feats && preds, sd::kErrInvalid, "null argument");
+    h->model->forward(feats, ld_feats, S_, T, ilens_host, max_nspks, preds, emb, attractors, S(stream));
+  });
+}
+
+int64_t sd_fseend_device_bytes(const sd_fseend* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
+
+int sd_fseend_destroy(sd_fseend* h) {
   return guard([&] { delete h; });
 }
 

@@ -16,12 +16,13 @@ namespace sd {
 
 void EdaModel::finalize() {
   SD_CHECK(!finalized_, kErrState, "finalize called twice");
-  SD_CHECK(cfg_.variant >= 0 && cfg_.variant <= 2, kErrInvalid, "unknown EDA model variant");
+  SD_CHECK(cfg_.variant >= 0 && cfg_.variant <= 3, kErrInvalid, "unknown EDA model variant");
   const int E = cfg_.n_units;
   SD_CHECK(E % cfg_.n_heads == 0, kErrInvalid, "n_units must be divisible by n_heads");
   LayerLoader ld{ps_, arena_, cfg_.bf16};
-  const std::string inp = cfg_.variant == 0 ? "encoder" : "linear";
-  const std::string norm = cfg_.variant == 0 ? "encoder_norm" : "linear_norm";
+  const bool plain = cfg_.variant == 3;
+  const std::string inp = (cfg_.variant == 0 || plain) ? "encoder" : "linear";
+  const std::string norm = (cfg_.variant == 0 || plain) ? "encoder_norm" : "linear_norm";
   {
     const HostTensor& w = ps_.get(inp + ".weight");
     SD_CHECK(w.shape.size() == 2 && w.shape[0] == E && w.shape[1] == cfg_.in_size, kErrParam,
@@ -37,7 +38,7 @@ void EdaModel::finalize() {
   norm_g_ = ld.up(norm + ".weight");
   norm_b_ = ld.up(norm + ".bias");
   for (int i = 0; i < cfg_.n_layers; ++i) {
-    if (cfg_.variant == 0)
+    if (cfg_.variant == 0 || plain)
       tfm_.push_back(ld.transformer("transformer_encoder.layers." + std::to_string(i)));
     else if (cfg_.variant == 1)
       tfm_.push_back(ld.transformer("encoder.layers." + std::to_string(i)));
@@ -55,13 +56,18 @@ void EdaModel::finalize() {
     *b = arena_.upload(bias);
     *hh = arena_.upload(wh.data);
   };
-  enc_ih_ = ld.packed("eda.encoder.weight_ih_l0");
-  lstm("eda.encoder.", &enc_b_, &enc_hh_);
-  // The decoder's inputs are zeros (encoder_decoder_attractor.py:50): W_ih never contributes.
-  ps_.mark("eda.decoder.weight_ih_l0");
-  lstm("eda.decoder.", &dec_b_, &dec_hh_);
-  lin_w_ = ld.up("eda.linear.weight");
-  lin_b_ = ld.up("eda.linear.bias");
+  if (plain) {
+    dec_ = ld.linear("decoder");
+    SD_CHECK(dec_.w.N == cfg_.n_speakers, kErrParam, "size mismatch for decoder.weight");
+  } else {
+    enc_ih_ = ld.packed("eda.encoder.weight_ih_l0");
+    lstm("eda.encoder.", &enc_b_, &enc_hh_);
+    // The decoder's inputs are zeros (encoder_decoder_attractor.py:50): W_ih never contributes.
+    ps_.mark("eda.decoder.weight_ih_l0");
+    lstm("eda.decoder.", &dec_b_, &dec_hh_);
+    lin_w_ = ld.up("eda.linear.weight");
+    lin_b_ = ld.up("eda.linear.bias");
+  }
   auto extra = ps_.unused();
   if (!extra.empty()) {
     std::string msg = "Unexpected key(s) in state_dict:";
@@ -91,7 +97,8 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   SD_CHECK(S >= 1 && S <= cfg_.max_seqs, kErrInvalid, "sequences exceed max_seqs");
   SD_CHECK(T >= 1 && T <= cfg_.max_frames, kErrInvalid, "frames exceed max_frames");
   SD_CHECK(ld_in >= in_ld_ && ld_in % 4 == 0, kErrInvalid, "feature row stride must be >= in_ld and % 4");
-  SD_CHECK(lengths && perm, kErrInvalid, "lengths and perm are required");
+  const bool plain = cfg_.variant == 3;
+  SD_CHECK(plain || (lengths && perm), kErrInvalid, "lengths and perm are required");
   const int E = cfg_.n_units, rows = S * T, NA = cfg_.max_n_speakers;
   const bool bf = cfg_.bf16;
   const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf};
@@ -100,6 +107,12 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   layernorm(Y_, rows, E, E, norm_g_, norm_b_, 1e-5f, X_, E, false, st);
   for (const auto& L : tfm_) run_transformer(L, X_, S, T, E, cfg_.n_heads, key_len, w, st);
   for (const auto& L : conf_) run_conformer(L, X_, S, T, E, cfg_.n_heads, 31, key_len, w, st);
+  if (plain) {   // eend/models.py:97-99: decoder Linear, activation=sigmoid (eend_infer.py:69)
+    ConvGemmArgs p = lin(Tens{X_, false}, rows, E, dec_.w, dec_.beta, Tens{act, false}, cfg_.n_speakers);
+    p.act = kActSigmoid;
+    conv_gemm(p, bf, st);
+    return;
+  }
   // EDA: shuffle -> encoder LSTM (packed) -> decoder LSTM from (h, c)
   gather_rows(X_, S, T, E, perm, lengths, Y_, st);
   conv_gemm(lin(Tens{Y_, false}, rows, E, enc_ih_, enc_b_, Tens{G_, false}, 4 * E), bf, st);

@@ -7,7 +7,9 @@
 namespace sd {
 
 struct EdaConfig {
-  int variant = 0;          // 0 TransformerEda, 1 EendEda(transformer), 2 EendEda(conformer)
+  int variant = 0;          // 0 TransformerEda, 1 EendEda(transformer), 2 EendEda(conformer),
+                            // 3 plain EEND TransformerModel (eend/models.py:17-101)
+  int n_speakers = 2;       // variant 3: decoder Linear(n_units, n_speakers)
   int in_size = 345;
   int n_units = 256;
   int n_heads = 4;
@@ -53,6 +55,7 @@ class EdaModel {
   const float *enc_b_ = nullptr, *enc_hh_ = nullptr;
   const float *dec_b_ = nullptr, *dec_hh_ = nullptr;
   const float *lin_w_ = nullptr, *lin_b_ = nullptr;
+  ConvL dec_;   // variant 3: decoder Linear -> sigmoid
 
   float *X_ = nullptr, *Y_ = nullptr, *QKV_ = nullptr, *AO_ = nullptr, *H_ = nullptr, *partial_ = nullptr;
   float *G_ = nullptr, *Gd_ = nullptr, *att_ = nullptr, *hT_ = nullptr, *cT_ = nullptr, *lstm_work_ = nullptr;

@@ -95,7 +95,7 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
 }
 
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
-                     const EncoderWork& w, hipStream_t st) {
+                     const EncoderWork& w, hipStream_t st, int causal, int causal_delay) {
   // nn.TransformerEncoderLayer (post-LN): X fp32 residual stream; QKV/AO/H bf16 in bf16 mode.
   const int rows = S * T;
   const bool bf = w.bf16;
@@ -105,6 +105,8 @@ void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int n
   a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
   a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
   a.key_len = key_len;
+  a.causal = causal;
+  a.causal_delay = causal_delay;
   attention(a, bf, st);
   ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, y, E);
   p.res = X; p.res_ld = E;

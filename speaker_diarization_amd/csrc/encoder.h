@@ -71,8 +71,9 @@ struct EncoderWork {
 };
 
 // X: (S*T, E) fp32, updated in place.  key_len: device int32 (S) or nullptr.
+// causal: key j visible to query i iff j <= i + causal_delay (fs_eend.py:168-171 mask).
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
-                     const EncoderWork& w, hipStream_t st);
+                     const EncoderWork& w, hipStream_t st, int causal = 0, int causal_delay = 0);
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
                    const int* key_len, const EncoderWork& w, hipStream_t st);
 

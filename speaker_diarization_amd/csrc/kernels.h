@@ -74,6 +74,13 @@ struct AttnArgs {
   float scale = 1.f;
   int causal = 0, causal_delay = 0;
   const int* key_len = nullptr;
+  // Token t of sequence s lives at row (s / seq_inner) * seq_outer + (s % seq_inner) * seq_inner_stride
+  // + t * tok_stride of qkv / out.  Defaults (seq_outer 0 -> T) give contiguous sequences; the FS-EEND
+  // decoder runs its time attention over the slots of a (T, C) token grid with tok_stride C.
+  int seq_inner = 1;
+  int64_t seq_outer = 0;
+  int seq_inner_stride = 0;
+  int tok_stride = 1;
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
@@ -159,4 +166,12 @@ void fill_rows(const float* row, int D, int rows, float* y, hipStream_t st);
 // probs (S, n_att) = sigmoid(att · lw + lb); act (S, T, n_att-1) = sigmoid(emb · att[:-1]ᵀ).
 void attractor_scores(const float* emb, int S, int T, int E, const float* att, int n_att, const float* lw,
                       const float* lb, float* probs, float* act, hipStream_t st);
+
+// ---------------------------------------------------------------- fs-eend glue (fseend_ops.hip)
+void row_l2norm(const float* x, int rows, int D, float* y, hipStream_t st);   // y = x / |x| per row
+// out (T*C, D): out[t*C + c] = g[t] + p[c]
+void slot_init(const float* g, int T, int C, int D, const float* p, float* out, hipStream_t st);
+// scores (T, C) = emb[t]·att[t,c]/|att[t,c]|; write_norm: att normalised in place.
+void slot_scores(const float* emb, float* att, int T, int C, int D, float* scores, bool write_norm,
+                 hipStream_t st);
 }  // namespace sd

@@ -1,0 +1,115 @@
+"""OnlineTransformerDADiarization — drop-in for speaker_diarization/fs_eend/fs_eend.py:20-96
+(inference surface: constructor, load_state_dict, test).
+
+test(src, ilens, max_nspks) runs in libsdiar (HIP, gfx950): BatchNorm-folded
+input Linear + LayerNorm, causal transformer encoder, look-ahead Conv1d, L2
+norm, the shared fusion-layer attractor decoder on the (T, C) token grid and
+the per-frame emb·attractorᵀ scores.  FS-EEND does not shard (causal
+full-history attention): multi-GPU runs are replicas, one
+recording per GPU.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from .. import _lib
+from ..weights import FSEENDConfig, unwrap_checkpoint
+
+
+class OnlineTransformerDADiarization:
+    def __init__(self, n_speakers, in_size, n_units, n_heads, enc_n_layers, dec_n_layers, dropout, has_mask,
+                 max_seqlen, dec_dim_feedforward, conv_delay=9, mask_delay=0, decom_kernel_size=64, *,
+                 device=None, precision: str = "fp32", max_seqs: int = 1, max_frames: int = None,
+                 max_nspks: int = 6):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be bf16 or fp32, got {precision}")
+        self.cfg = FSEENDConfig(n_speakers=n_speakers, in_size=in_size, n_units=n_units, n_heads=n_heads,
+                                enc_n_layers=enc_n_layers, dec_n_layers=dec_n_layers, dropout=dropout,
+                                has_mask=has_mask, max_seqlen=max_seqlen, dec_dim_feedforward=dec_dim_feedforward,
+                                conv_delay=conv_delay, mask_delay=mask_delay)
+        self.n_speakers = n_speakers
+        self.precision = precision
+        self.max_seqs = max_seqs
+        self.max_frames = max_frames or max_seqlen
+        self.max_nspks = max_nspks
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("FS-EEND (MI355X backend) runs on a HIP device only")
+        self._h = None
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Accepts the module state_dict or the Lightning checkpoint layout
+        ({"state_dict": {"model.<key>": ...}}, fs_eend/train.py:183-191)."""
+        if not strict:
+            raise ValueError("strict=False is not supported by the MI355X backend")
+        c = self.cfg
+        conf = _lib.FseendConfig(in_size=c.in_size, n_units=c.n_units, n_heads=c.n_heads, enc_n_layers=c.enc_n_layers,
+                                 enc_dim_feedforward=c.enc_dim_feedforward, dec_n_layers=c.dec_n_layers,
+                                 dec_dim_feedforward=c.dec_dim_feedforward, conv_delay=c.conv_delay,
+                                 mask_delay=c.mask_delay, has_mask=int(bool(c.has_mask)), max_seqs=self.max_seqs,
+                                 max_frames=self.max_frames, max_nspks=self.max_nspks,
+                                 precision=1 if self.precision == "bf16" else 0)
+        h = _lib.create_handle("fseend", conf, _lib.host_state(unwrap_checkpoint(state_dict)))
+        self._release()
+        self._h = h
+        self.in_ld = _lib.load().sd_fseend_input_stride(h)
+        return self
+
+    def _release(self):
+        if self._h is not None:
+            _lib.load().sd_fseend_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def eval(self):
+        return self
+
+    def to(self, device):
+        if torch.device(device).type != "cuda":
+            raise ValueError("FS-EEND (MI355X backend) runs on a HIP device only")
+        return self
+
+    def device_bytes(self) -> int:
+        return int(_lib.load().sd_fseend_device_bytes(self._h)) if self._h is not None else 0
+
+    def test_device(self, feats, ilens: List[int], max_nspks: int = 6, want_emb: bool = True,
+                    want_attractors: bool = True):
+        """Device-level call on a padded (S, T, ld) feature tensor; returns the padded
+        (preds (S,T,C), emb (S,T,D) | None, attractors (S,T,C,D) | None)."""
+        if self._h is None:
+            raise RuntimeError("load_state_dict() must be called before test()")
+        S, T, ld = feats.shape
+        D = self.cfg.n_units
+        dev = self.device
+        preds = torch.empty(S, T, max_nspks, device=dev, dtype=torch.float32)
+        emb = torch.empty(S, T, D, device=dev, dtype=torch.float32) if want_emb else None
+        att = torch.empty(S, T, max_nspks, D, device=dev, dtype=torch.float32) if want_attractors else None
+        lens = (ctypes_int_array(ilens))
+        _lib.call("sd_fseend_test", self._h, _lib.ptr(feats.contiguous()), ld, S, T, lens, max_nspks,
+                  _lib.ptr(preds), _lib.ptr(emb), _lib.ptr(att), _lib.stream_ptr(dev))
+        return preds, emb, att
+
+    def test(self, src, ilens, max_nspks=6):
+        """fs_eend.py:79-96: list of (T_i, in_size) -> (preds [(T_i, C)], emb [(T_i, D)],
+        attractors [(T_i, C, D)])."""
+        ilens = [int(n) for n in ilens]
+        S, T = len(src), max(int(x.shape[0]) for x in src)
+        buf = torch.full((S, T, self.in_ld), -1.0, device=self.device, dtype=torch.float32)   # pad_sequence(-1)
+        for i, x in enumerate(src):
+            buf[i, : x.shape[0], : self.cfg.in_size] = x.to(self.device, torch.float32)
+        buf[:, :, self.cfg.in_size:] = 0.0
+        preds, emb, att = self.test_device(buf, ilens, max_nspks)
+        return ([preds[i, : ilens[i]] for i in range(S)], [emb[i, : ilens[i]] for i in range(S)],
+                [att[i, : ilens[i]] for i in range(S)])
+
+
+def ctypes_int_array(vals):
+    import ctypes
+    return (ctypes.c_int * len(vals))(*vals)

@@ -367,3 +367,80 @@ def _conformer_layer(k: list, p: str, e: int, ffn: int, kernel: int, group_norm:
 
 def eda_state_dict(cfg: EDAConfig, seed: int = 777):
     return synthetic_state_dict(eda_layout(cfg), seed)
+
+
+def eend_layout(cfg: EDAConfig) -> list:
+    """Key layout of the plain EEND TransformerModel (eend/models.py:17-55)."""
+    e = cfg.n_units
+    k: list = [("encoder.weight", (e, cfg.in_size), "linear"), ("encoder.bias", (e,), "small")]
+    _ln(k, "encoder_norm", e)
+    for i in range(cfg.n_layers):
+        _tfm(k, f"transformer_encoder.layers.{i}.", e, cfg.dim_feedforward)
+    k.append(("decoder.weight", (cfg.n_speakers, e), "linear"))
+    k.append(("decoder.bias", (cfg.n_speakers,), "small"))
+    return k
+
+
+# ----------------------------------------------------------------------------- FS-EEND
+@dataclass
+class FSEENDConfig:
+    """OnlineTransformerDADiarization(**configs["model"]["params"]) as fs_eend/train.py:71-75
+    builds it from config/spk_onl_tfm_enc_dec_nonautoreg_infer.yaml."""
+    n_speakers: int = None
+    in_size: int = 345                 # (2 * context_recp + 1) * n_mels
+    n_units: int = 256
+    n_heads: int = 4
+    enc_n_layers: int = 4
+    dec_n_layers: int = 2
+    dropout: float = 0.1
+    has_mask: bool = True
+    max_seqlen: int = 10000
+    dec_dim_feedforward: int = 2048
+    conv_delay: int = 9
+    mask_delay: int = 0
+    enc_dim_feedforward: int = 2048    # MaskedTransformerEncoderModel default (never passed)
+    pe_max_len: int = 5000             # PositionalEncoding default max_len
+
+
+def fseend_layout(cfg: FSEENDConfig) -> list:
+    """Key layout of OnlineTransformerDADiarization (fs_eend/fs_eend.py:20-41, 99-170,
+    207-240, 282-333).  The decoder ModuleList holds ONE layer object dec_n_layers
+    times, so its keys appear under every index with identical values."""
+    e, d = cfg.n_units, cfg.in_size
+    k: list = []
+    _bn(k, "enc.bn", d)
+    k.append(("enc.encoder.weight", (e, d), "linear"))
+    k.append(("enc.encoder.bias", (e,), "small"))
+    _ln(k, "enc.encoder_norm", e)
+    for i in range(cfg.enc_n_layers):
+        _tfm(k, f"enc.transformer_encoder.layers.{i}.", e, cfg.enc_dim_feedforward)
+    k.append(("dec.encoder.weight", (e, d), "linear"))
+    k.append(("dec.encoder.bias", (e,), "small"))
+    _ln(k, "dec.encoder_norm", e)
+    k.append(("dec.pos_enc.pe", (1, cfg.pe_max_len, e), "pe"))
+    k.append(("dec.convert.weight", (e, 2 * e), "linear"))
+    k.append(("dec.convert.bias", (e,), "small"))
+    for i in range(cfg.dec_n_layers):
+        p = f"dec.attractor_decoder.{i}."
+        _mha(k, p + "self_attn1.", e)
+        _mha(k, p + "self_attn2.", e)
+        k.append((p + "linear1.weight", (cfg.dec_dim_feedforward, e), "linear"))
+        k.append((p + "linear1.bias", (cfg.dec_dim_feedforward,), "small"))
+        k.append((p + "linear2.weight", (e, cfg.dec_dim_feedforward), "linear"))
+        k.append((p + "linear2.bias", (e,), "small"))
+        for n in ("norm11", "norm12", "norm21", "norm22"):
+            _ln(k, p + n, e)
+    k.append(("cnn.weight", (e, e, 2 * cfg.conv_delay + 1), "conv1d"))
+    k.append(("cnn.bias", (e,), "small"))
+    return k
+
+
+def fseend_state_dict(cfg: FSEENDConfig, seed: int = 777):
+    sd = synthetic_state_dict(fseend_layout(cfg), seed)
+    sd["dec.pos_enc.pe"] = sinusoid_pe(cfg.pe_max_len, cfg.n_units).reshape(1, cfg.pe_max_len, cfg.n_units)
+    # shared decoder layer: every index carries the same tensors (fs_eend.py:118)
+    for k in list(sd):
+        if k.startswith("dec.attractor_decoder.0."):
+            for i in range(1, cfg.dec_n_layers):
+                sd[k.replace(".0.", f".{i}.", 1)] = sd[k]
+    return sd

@@ -244,10 +244,73 @@ def make_feature(name):
     print(name, Y.shape)
 
 
+# ----------------------------------------------------------------------------- FS-EEND / EEND
+FSEEND_CASES = {
+    # name: (lengths of the src list, max_nspks, mask_delay, input seed, weight seed)
+    "fseend_T240": ([240], 6, 0, 31, 791),
+    "fseend_batch": ([150, 97], 6, 0, 32, 792),
+    "fseend_delay2": ([130], 5, 2, 33, 793),
+}
+EEND_CASES = {
+    # name: (n_speakers, n_layers, lengths, input seed, weight seed)
+    "eend_tfm_l2": (2, 2, [200], 41, 795),
+    "eend_tfm_batch": (3, 2, [120, 77], 42, 796),
+}
+
+
+def make_fseend(name):
+    import torch
+    from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
+    lens, C, delay, iseed, wseed = FSEEND_CASES[name]
+    d = os.path.join(REF, "speaker_diarization/fs_eend")
+    sys.path.insert(0, d)
+    import fs_eend as F  # reference module (plain torch)
+    cfg = FSEENDConfig(mask_delay=delay)
+    torch.manual_seed(0)
+    m = F.OnlineTransformerDADiarization(n_speakers=None, in_size=345, n_units=256, n_heads=4, enc_n_layers=4,
+                                         dec_n_layers=2, dropout=0.1, has_mask=True, max_seqlen=10000,
+                                         dec_dim_feedforward=2048, conv_delay=9, mask_delay=delay)
+    m.eval()
+    m.load_state_dict(to_torch(fseend_state_dict(cfg, seed=wseed)), strict=True)
+    xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
+    with torch.no_grad():
+        out, emb, att = m.test(xs, lens, max_nspks=C)
+    res = dict(lens=np.array(lens, np.int64), max_nspks=np.int64(C), mask_delay=np.int64(delay),
+               out=np.concatenate([o.numpy() for o in out]).astype(np.float32),
+               emb=np.concatenate([e.numpy() for e in emb]).astype(np.float32),
+               att_head=np.concatenate([a.numpy()[:24] for a in att]).astype(np.float32))   # first 24 frames
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **res)
+    print(name, res["out"].shape, res["att_head"].shape)
+    sys.path.remove(d)
+    sys.modules.pop("fs_eend", None)
+
+
+def make_eend(name):
+    import torch
+    from speaker_diarization_amd.weights import EDAConfig, eend_layout, synthetic_state_dict, to_torch
+    nspk, L, lens, iseed, wseed = EEND_CASES[name]
+    install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from speaker_diarization.eend import models as M
+    cfg = EDAConfig(n_speakers=nspk, n_layers=L)
+    torch.manual_seed(0)
+    m = M.TransformerModel(n_speakers=nspk, in_size=345, n_heads=4, n_units=256, n_layers=L)
+    m.eval()
+    m.load_state_dict(to_torch(synthetic_state_dict(eend_layout(cfg), wseed)), strict=True)
+    xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
+    with torch.no_grad():
+        ys = m(xs, activation=torch.sigmoid)     # eend_infer.py:69
+    res = dict(lens=np.array(lens, np.int64), ys=np.concatenate([y.numpy() for y in ys]).astype(np.float32))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **res)
+    print(name, res["ys"].shape)
+
+
 if __name__ == "__main__":
     import torch
     torch.set_num_threads(8)
-    names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES))
+    names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES)
+                             + list(FSEEND_CASES) + list(EEND_CASES))
     for n in names:
         if n in TSVAD_CASES:
             make_tsvad(n)
@@ -255,5 +318,9 @@ if __name__ == "__main__":
             make_eda(n)
         elif n == "eda_tfm_batch":
             make_eda_batch(n)
+        elif n in FSEEND_CASES:
+            make_fseend(n)
+        elif n in EEND_CASES:
+            make_eend(n)
         else:
             make_feature(n)

@@ -1,0 +1,88 @@
+"""FS-EEND and plain EEND on the GPU (libsdiar C ABI) against the reference goldens.
+Tolerances: fp32 1e-3 (north_star), bf16 3e-2."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fseend_ref
+from speaker_diarization_amd.eend.models import TransformerModel
+from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
+from speaker_diarization_amd.weights import (EDAConfig, FSEENDConfig, eend_layout, fseend_state_dict,
+                                             synthetic_state_dict, to_torch)
+from tests.golden.make_golden import EEND_CASES, FSEEND_CASES, eda_inputs
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FP32_ATOL = 1e-3
+BF16_ATOL = 3e-2
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz")))
+
+
+def _fseend(delay, wseed, precision="fp32", max_seqs=2, max_frames=512, max_nspks=6):
+    m = OnlineTransformerDADiarization(n_speakers=None, in_size=345, n_units=256, n_heads=4, enc_n_layers=4,
+                                       dec_n_layers=2, dropout=0.1, has_mask=True, max_seqlen=10000,
+                                       dec_dim_feedforward=2048, conv_delay=9, mask_delay=delay,
+                                       precision=precision, max_seqs=max_seqs, max_frames=max_frames,
+                                       max_nspks=max_nspks)
+    m.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(mask_delay=delay), seed=wseed)))
+    return m
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(FSEEND_CASES))
+def test_fseend_test_matches_golden(gpu, name, precision):
+    lens, C, delay, iseed, wseed = FSEEND_CASES[name]
+    g = _load(name)
+    m = _fseend(delay, wseed, precision)
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
+    out, emb, att = m.test(xs, lens, max_nspks=C)
+    np.testing.assert_allclose(torch.cat(out).cpu().numpy(), g["out"], atol=tol)
+    np.testing.assert_allclose(torch.cat(emb).cpu().numpy(), g["emb"], atol=tol)
+    np.testing.assert_allclose(torch.cat([a[:24] for a in att]).cpu().numpy(), g["att_head"], atol=tol)
+
+
+def test_fseend_long_causal_vs_oracle(gpu):
+    """T = 700 (several 64-query tiles of the causal time attention, ragged last tile)."""
+    T = 700
+    m = _fseend(0, 797, max_seqs=1, max_frames=T)
+    x = eda_inputs([T], seed=77)
+    out, emb, _ = m.test([torch.from_numpy(x[0])], [T], max_nspks=6)
+    sd = to_torch(fseend_state_dict(FSEENDConfig(), seed=797))
+    ro, re, _ = fseend_ref.fseend_test(sd, FSEENDConfig(), [torch.from_numpy(x[0])], [T], 6)
+    np.testing.assert_allclose(out[0].cpu().numpy(), ro[0].numpy(), atol=FP32_ATOL)
+    np.testing.assert_allclose(emb[0].cpu().numpy(), re[0].numpy(), atol=FP32_ATOL)
+
+
+def test_fseend_strict_load(gpu):
+    sd = to_torch(fseend_state_dict(FSEENDConfig(), seed=3))
+    bad = dict(sd)
+    bad.pop("dec.attractor_decoder.0.norm12.weight")
+    with pytest.raises(RuntimeError, match="Error"):
+        _fseend_empty().load_state_dict(bad)
+    lightning = {"state_dict": {"model." + k: v for k, v in sd.items()}}
+    _fseend_empty().load_state_dict(lightning)
+
+
+def _fseend_empty():
+    return OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, max_frames=64)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(EEND_CASES))
+def test_eend_matches_golden(gpu, name, precision):
+    nspk, L, lens, iseed, wseed = EEND_CASES[name]
+    g = _load(name)
+    m = TransformerModel(n_speakers=nspk, in_size=345, n_heads=4, n_units=256, n_layers=L, precision=precision)
+    m.load_state_dict(to_torch(synthetic_state_dict(eend_layout(EDAConfig(n_speakers=nspk, n_layers=L)), wseed)))
+    xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
+    ys = m(xs, activation=torch.sigmoid)
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    np.testing.assert_allclose(torch.cat(ys).cpu().numpy(), g["ys"], atol=tol)
+    with pytest.raises(AttributeError):
+        m(xs, has_mask=True, activation=torch.sigmoid)
