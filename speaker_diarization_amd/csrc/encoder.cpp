@@ -96,10 +96,12 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
 
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
                      const EncoderWork& w, hipStream_t st, int causal, int causal_delay) {
-  // nn.TransformerEncoderLayer (post-LN): X fp32 residual stream; QKV/AO/H bf16 in bf16 mode.
+  // nn.TransformerEncoderLayer, post-LN: X = LN1(X + SA(X)); X = LN2(X + FFN(X)).
+  // X is the fp32 residual stream; the sub-block outputs t (bf16 in bf16 mode) are added
+  // inside the LayerNorm kernel, so every GEMM epilogue only stores.
   const int rows = S * T;
   const bool bf = w.bf16;
-  const Tens x{X, false}, y{w.Y, false}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
+  const Tens x{X, false}, t{w.Y, bf}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
   conv_gemm(lin(x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
   AttnArgs a;
   a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
@@ -108,51 +110,43 @@ void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int n
   a.causal = causal;
   a.causal_delay = causal_delay;
   attention(a, bf, st);
-  ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, y, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, bf, st);
-  layernorm(w.Y, rows, E, E, L.n1g, L.n1b, 1e-5f, X, E, false, st);
-  p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
+  conv_gemm(lin(ao, rows, E, L.out_proj, L.out_b, t, E), bf, st);
+  add_layernorm(X, t.p, bf, rows, E, L.n1g, L.n1b, 1e-5f, false, X, false, st);
+  ConvGemmArgs p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
-  p = lin(h, rows, L.l1.N, L.l2, L.b2, y, E);
-  p.res = X; p.res_ld = E;
-  conv_gemm(p, bf, st);
-  layernorm(w.Y, rows, E, E, L.n2g, L.n2b, 1e-5f, X, E, false, st);
+  conv_gemm(lin(h, rows, L.l1.N, L.l2, L.b2, t, E), bf, st);
+  add_layernorm(X, t.p, bf, rows, E, L.n2g, L.n2b, 1e-5f, false, X, false, st);
 }
 
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
                    const int* key_len, const EncoderWork& w, hipStream_t st) {
-  // torchaudio ConformerLayer: X fp32 residual stream; LN outputs / GEMM-only intermediates bf16.
+  // torchaudio ConformerLayer (pre-LN): X fp32 residual stream.  Each sub-block's output t
+  // (into the LN-output buffer, which is dead by then) is added to X by the NEXT
+  // LayerNorm (add_layernorm writes X += t and y = LN(X)); the last one is the final LN.
   const int rows = S * T;
   const bool bf = w.bf16;
-  const Tens x{X, false}, y{w.Y, bf}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
-  auto ffn = [&](const float* lng, const float* lnb, const PackedW& w1, const float* b1,
-                 const PackedW& w2, const float* b2) {
-    layernorm(X, rows, E, E, lng, lnb, 1e-5f, y.p, E, bf, st);
+  const Tens y{w.Y, bf}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
+  auto ffn_body = [&](const PackedW& w1, const float* b1, const PackedW& w2, const float* b2) {
     ConvGemmArgs p = lin(y, rows, E, w1, b1, h, w1.N);
     p.act = kActSilu;
     conv_gemm(p, bf, st);
-    p = lin(h, rows, w1.N, w2, b2, x, E);   // weights pre-scaled by 0.5
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
+    conv_gemm(lin(h, rows, w1.N, w2, b2, y, E), bf, st);   // weights pre-scaled by 0.5
   };
-  ffn(L.f1_lng, L.f1_lnb, L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
+  // ffn1
+  layernorm(X, rows, E, E, L.f1_lng, L.f1_lnb, 1e-5f, y.p, E, bf, st);
+  ffn_body(L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
   // self attention block (key_padding_mask from lengths)
-  layernorm(X, rows, E, E, L.at_lng, L.at_lnb, 1e-5f, y.p, E, bf, st);
+  add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
   conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
   AttnArgs a;
   a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
   a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
   a.key_len = key_len;
   attention(a, bf, st);
-  {
-    ConvGemmArgs p = lin(ao, rows, E, L.out_proj, L.out_b, x, E);
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
-  }
+  conv_gemm(lin(ao, rows, E, L.out_proj, L.out_b, y, E), bf, st);
   // convolution module (no padding mask in torchaudio's conv module)
-  layernorm(X, rows, E, E, L.cv_lng, L.cv_lnb, 1e-5f, y.p, E, bf, st);
+  add_layernorm(X, y.p, bf, rows, E, L.cv_lng, L.cv_lnb, 1e-5f, true, y.p, bf, st);
   conv_gemm(lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E), bf, st);
   if (L.group_norm) {
     glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, w.partial, false, bf, st);
@@ -160,13 +154,11 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   } else {
     glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, nullptr, true, bf, st);
   }
-  {
-    ConvGemmArgs p = lin(ao, rows, E, L.pw2, L.pw2_b, x, E);
-    p.res = X; p.res_ld = E;
-    conv_gemm(p, bf, st);
-  }
-  ffn(L.f2_lng, L.f2_lnb, L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
-  layernorm(X, rows, E, E, L.fin_g, L.fin_b, 1e-5f, X, E, false, st);
+  conv_gemm(lin(ao, rows, E, L.pw2, L.pw2_b, y, E), bf, st);
+  // ffn2 + final LayerNorm
+  add_layernorm(X, y.p, bf, rows, E, L.f2_lng, L.f2_lnb, 1e-5f, true, y.p, bf, st);
+  ffn_body(L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
+  add_layernorm(X, y.p, bf, rows, E, L.fin_g, L.fin_b, 1e-5f, false, X, false, st);
 }
 
 }  // namespace sd

@@ -131,7 +131,7 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
   const int D = cfg_.n_units, nh = cfg_.n_heads;
   const int64_t n = (int64_t)S * T * C;
   const bool bf = cfg_.bf16;
-  const Tens a{A, false}, y{A2_, false}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
+  const Tens a{A, false}, t{A2_, bf}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
   const float scale = 1.f / std::sqrt((float)(D / nh));
   // (1) attention over time within each slot, causal
   conv_gemm(lin(a, (int)n, D, fus_.in1, fus_.in1_b, qkv, 3 * D), bf, st);
@@ -143,10 +143,8 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
     t.seq_inner = C; t.seq_outer = (int64_t)T * C; t.seq_inner_stride = 1; t.tok_stride = C;
     attention(t, bf, st);
   }
-  ConvGemmArgs p = lin(ao, (int)n, D, fus_.out1, fus_.out1_b, y, D);
-  p.res = A; p.res_ld = D;
-  conv_gemm(p, bf, st);
-  layernorm(A2_, (int)n, D, D, fus_.n11g, fus_.n11b, 1e-5f, A, D, false, st);
+  conv_gemm(lin(ao, (int)n, D, fus_.out1, fus_.out1_b, t, D), bf, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n11g, fus_.n11b, 1e-5f, false, A, false, st);
   // (2) attention over the C slots of each frame, no mask
   conv_gemm(lin(a, (int)n, D, fus_.in2, fus_.in2_b, qkv, 3 * D), bf, st);
   {
@@ -155,18 +153,14 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
     s.out = ao.p; s.ldo = D; s.scale = scale;
     attention(s, bf, st);
   }
-  p = lin(ao, (int)n, D, fus_.out2, fus_.out2_b, y, D);
-  p.res = A; p.res_ld = D;
-  conv_gemm(p, bf, st);
-  layernorm(A2_, (int)n, D, D, fus_.n21g, fus_.n21b, 1e-5f, A, D, false, st);
+  conv_gemm(lin(ao, (int)n, D, fus_.out2, fus_.out2_b, t, D), bf, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n21g, fus_.n21b, 1e-5f, false, A, false, st);
   // (3) feed-forward
-  p = lin(a, (int)n, D, fus_.l1, fus_.b1, h, fus_.l1.N);
+  ConvGemmArgs p = lin(a, (int)n, D, fus_.l1, fus_.b1, h, fus_.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
-  p = lin(h, (int)n, fus_.l1.N, fus_.l2, fus_.b2, y, D);
-  p.res = A; p.res_ld = D;
-  conv_gemm(p, bf, st);
-  layernorm(A2_, (int)n, D, D, fus_.n22g, fus_.n22b, 1e-5f, A, D, false, st);
+  conv_gemm(lin(h, (int)n, fus_.l1.N, fus_.l2, fus_.b2, t, D), bf, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n22g, fus_.n22b, 1e-5f, false, A, false, st);
 }
 
 void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int* lengths, int C, float* preds,

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(ConvGemmArgs p) {
         Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + l15] = acc[mt][nt][r];
   __syncthreads();
 
-  const bool lin = p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh;
+  const bool lin = (p.B == 1 && p.Ho == 1) || (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh);
   const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
   constexpr int CPR = BN / 4;
   for (int q = tid; q < BM * CPR; q += 256) {
@@ -294,6 +294,10 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st) {
     key += " M=" + std::to_string(M) + " N=" + std::to_string(p.N) + " K=" + std::to_string(p.K) +
            " taps=" + std::to_string(p.kh * p.kw) + (p.a_bf16 ? " Abf" : " Af32") + (p.pre_scale ? " pre" : "");
   ProfScope prof(key.c_str(), flops, bytes, st);
+  if (gemm_stream_supported(p)) {   // weight-resident streaming path (gemm_stream.hip)
+    conv_gemm_stream(p, st);
+    return;
+  }
   if (gemm_dma_supported(p)) {   // LDS-DMA fast path (gemm_dma.hip)
     conv_gemm_dma(p, st);
     return;

@@ -166,9 +166,71 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
         Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + l15] = acc[mt][nt][r];
   __syncthreads();
 
-  const bool lin = p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh;
+  const bool lin = (p.B == 1 && p.Ho == 1) || (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh);
   const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
   constexpr int CPR = BN / 4;
+  if (vec && !p.gate && (!p.res || (!p.res_bf16 && (p.res_ld & 3) == 0))) {
+    // Fast epilogue (row-major output): each thread owns one 4-column group, so the
+    // per-channel alpha/beta are loaded once, and all residual rows are fetched before
+    // any store (res may alias out: the in-place residual add of the encoders).
+    constexpr int RPI = 256 / CPR;      // rows per pass
+    constexpr int ITER = BM / RPI;
+    const int cg = tid % CPR, r0 = tid / CPR;
+    const int n = n0 + cg * 4;
+    if (n >= p.N) return;
+    const bool full = n + 3 < p.N;
+    float al[4], be[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = full || n + u < p.N;
+      al[u] = (p.alpha && ok) ? p.alpha[n + u] : 1.f;
+      be[u] = (p.beta && ok) ? p.beta[n + u] : 0.f;
+    }
+    float4 rv[ITER];
+    if (p.res) {
+      const float* rbase = reinterpret_cast<const float*>(p.res);
+#pragma unroll
+      for (int i = 0; i < ITER; ++i) {
+        const int m = m0 + r0 + i * RPI;
+        rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M) {
+          const float* r = rbase + (int64_t)m * p.res_ld + n;
+          if (full) rv[i] = *reinterpret_cast<const float4*>(r);
+          else {
+            rv[i].x = r[0];
+            if (n + 1 < p.N) rv[i].y = r[1];
+            if (n + 2 < p.N) rv[i].z = r[2];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int row = r0 + i * RPI;
+      const int m = m0 + row;
+      if (m >= M) break;
+      const float4 c4 = *reinterpret_cast<const float4*>(Cs + row * CLD + cg * 4);
+      float v[4] = {c4.x, c4.y, c4.z, c4.w};
+      const float r4[4] = {p.res ? rv[i].x : 0.f, p.res ? rv[i].y : 0.f, p.res ? rv[i].z : 0.f,
+                           p.res ? rv[i].w : 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = apply_act(fmaf(v[u], al[u], be[u]) + r4[u], p.act);
+      const int64_t o = (int64_t)m * p.o_sw + n;
+      if (full) {
+        if (p.out_bf16)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.out) + o) =
+              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        else
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        for (int u = 0; u < 4 && n + u < p.N; ++u) {
+          if (p.out_bf16) reinterpret_cast<uint16_t*>(p.out)[o + u] = f2bf_bits(v[u]);
+          else reinterpret_cast<float*>(p.out)[o + u] = v[u];
+        }
+      }
+    }
+    return;
+  }
   for (int q = tid; q < BM * CPR; q += 256) {
     const int row = q / CPR;
     const int cc = (q % CPR) * 4;

@@ -34,6 +34,8 @@ struct ConvGemmArgs {
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
 void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
+bool gemm_stream_supported(const ConvGemmArgs& p);            // bf16 A linear, K%64==0, K<=768, no res
+void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
 
 // Plain row-major linear layer helper: out[m*ldo + o_coff + n] = act(A[m*lda+k]·W[n][k] * alpha + beta (+res)).
@@ -58,6 +60,10 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
 // y may be bf16 (y_bf16); x is fp32 (the residual stream).
 void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
                float eps, void* y, int ldy, bool y_bf16, hipStream_t st);
+// Residual add fused into LayerNorm: v = x + t (t fp32 or bf16, rows of D); write_x: x = v;
+// y = LN(v) (y may alias x or t: each row is read completely before it is written).
+void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st);
 
 // ---------------------------------------------------------------- attention
 // Multi-head self-attention core on a packed in-projection output.

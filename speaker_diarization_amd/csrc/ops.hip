@@ -186,11 +186,15 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
 }
 
 // ------------------------------------------------------------------ LayerNorm
-template <int PER, bool YBF>
+template <int PER, bool YBF, int TM>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows, int D,
-                                                        int ldx, const float* __restrict__ g,
+                                                        int ldx, const void* __restrict__ t,
+                                                        float* __restrict__ xo, const float* __restrict__ g,
                                                         const float* __restrict__ bb, float eps,
                                                         act_t<YBF>* __restrict__ y, int ldy) {
+  // TM: 0 plain LN of x; 1 / 2: LN of x + t with t fp32 / bf16 (the residual add of the
+  // encoder blocks, fused here so the producing GEMM stores its output only); xo: the sum
+  // is also written back (pre-LN residual stream).
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -200,8 +204,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     int c = lane + i * 64;
-    v[i] = c < D ? xr[c] : 0.f;
-    s += v[i];
+    float a = c < D ? xr[c] : 0.f;
+    if constexpr (TM == 1) a += c < D ? reinterpret_cast<const float*>(t)[(int64_t)row * D + c] : 0.f;
+    if constexpr (TM == 2) a += c < D ? bf_bits2f(reinterpret_cast<const uint16_t*>(t)[(int64_t)row * D + c]) : 0.f;
+    v[i] = a;
+    s += a;
   }
   s = warp_sum(s);
   const float mean = s / (float)D;
@@ -214,6 +221,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
   q = warp_sum(q);
   const float rstd = rsqrtf(q / (float)D + eps);
+  if (xo) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + i * 64;
+      if (c < D) xo[(int64_t)row * ldx + c] = v[i];
+    }
+  }
   act_t<YBF>* yr = y + (int64_t)row * ldy;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -222,26 +236,46 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
-template <int PER>
-static void ln_launch(const float* x, int rows, int D, int ldx, const float* g, const float* b, float eps,
-                      void* y, int ldy, bool ybf, hipStream_t st) {
+template <int PER, int TM>
+static void ln_launch2(const float* x, int rows, int D, int ldx, const void* t, float* xo, const float* g,
+                       const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
   dim3 grid(cdiv(rows, 4));
   if (ybf)
-    hipLaunchKernelGGL((layernorm_kernel<PER, true>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps,
-                       reinterpret_cast<uint16_t*>(y), ldy);
+    hipLaunchKernelGGL((layernorm_kernel<PER, true, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
+                       eps, reinterpret_cast<uint16_t*>(y), ldy);
   else
-    hipLaunchKernelGGL((layernorm_kernel<PER, false>), grid, dim3(256), 0, st, x, rows, D, ldx, g, b, eps,
-                       reinterpret_cast<float*>(y), ldy);
+    hipLaunchKernelGGL((layernorm_kernel<PER, false, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
+                       eps, reinterpret_cast<float*>(y), ldy);
+}
+
+template <int PER>
+static void ln_launch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
+                      const float* g, const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
+  if (tm == 0) ln_launch2<PER, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+  else if (tm == 1) ln_launch2<PER, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+  else ln_launch2<PER, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+}
+
+static void ln_dispatch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
+                        const float* g, const float* b, float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
+  if (D <= 256) ln_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
+  else if (D <= 512) ln_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
+  else if (D <= 1024) ln_launch<16>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
+  else SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");
+  SD_LAUNCH_CHECK();
 }
 
 void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
                float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
   ProfScope prof("layernorm", 0.0, (4.0 + (y_bf16 ? 2.0 : 4.0)) * rows * D, st);
-  if (D <= 256) ln_launch<4>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
-  else if (D <= 512) ln_launch<8>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
-  else if (D <= 1024) ln_launch<16>(x, rows, D, ldx, g, b, eps, y, ldy, y_bf16, st);
-  else SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");
-  SD_LAUNCH_CHECK();
+  ln_dispatch(x, rows, D, ldx, nullptr, 0, nullptr, g, b, eps, y, ldy, y_bf16, st);
+}
+
+void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st) {
+  ProfScope prof("add_layernorm", 0.0,
+                 (4.0 + (t_bf16 ? 2.0 : 4.0) + (write_x ? 4.0 : 0.0) + (y_bf16 ? 2.0 : 4.0)) * rows * D, st);
+  ln_dispatch(x, rows, D, D, t, t_bf16 ? 2 : 1, write_x ? x : nullptr, g, b, eps, y, D, y_bf16, st);
 }
 
 // ------------------------------------------------------------------ TS-VAD glue

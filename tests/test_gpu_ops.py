@@ -42,7 +42,10 @@ def _rel_err(a, b):
 
 @pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("M,K,N,act", [(1, 32, 4, 0), (257, 384, 1152, 0), (1000, 1536, 384, 1),
-                                       (64, 512, 4, 0), (333, 96, 130, 3), (4096, 256, 2048, 2)])
+                                       (64, 512, 4, 0), (333, 96, 130, 3), (4096, 256, 2048, 2),
+                                       # weight-resident streaming path (bf16 A, K % 64 == 0, M >= 2048):
+                                       (20000, 384, 512, 3), (9001, 384, 1152, 0), (7777, 512, 384, 0),
+                                       (5003, 448, 200, 1), (3000, 768, 96, 0), (2048, 64, 130, 2)])
 def test_linear(gpu, precision, M, K, N, act):
     g = torch.Generator().manual_seed(M * 7 + N)
     x = torch.randn(M, K, generator=g)

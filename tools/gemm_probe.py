@@ -1,0 +1,44 @@
+"""GEMM probe: time conv_gemm's bf16 path (sd_op_linear, precision 2) on given shapes.
+
+    python tools/gemm_probe.py 153600x512x384 38400x2048x1536 ...
+Prints per-shape kernel time (HIP events inside libsdiar) and TF/s / GB/s.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from speaker_diarization_amd import _lib  # noqa: E402
+
+
+def probe(M, N, K, reps=10, act=0):
+    dev = torch.device("cuda", 0)
+    x = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) / K ** 0.5
+    b = torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    st = _lib.stream_ptr(dev)
+    lib = _lib.load()
+    _lib.call("sd_op_linear", _lib.ptr(x), M, K, _lib.ptr(w), _lib.ptr(b), N, act, _lib.ptr(out), 2, st)
+    torch.cuda.synchronize()
+    lib.sd_prof_reset()
+    lib.sd_prof_enable(1)
+    for _ in range(reps):
+        _lib.call("sd_op_linear", _lib.ptr(x), M, K, _lib.ptr(w), _lib.ptr(b), N, act, _lib.ptr(out), 2, st)
+    torch.cuda.synchronize()
+    lib.sd_prof_enable(0)
+    s = _lib.prof_stats()
+    g = s.get("conv_gemm_bf16")
+    us = g["ms"] / g["launches"] * 1e3
+    tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+    gbs = (M * K * 2 + N * K * 2 + M * N * 4) / (us * 1e-6) / 1e9
+    print(f"M={M:7d} N={N:5d} K={K:5d}: {us:8.1f} us  {tf:7.1f} TF/s  {gbs:7.0f} GB/s (A bf16 + W + out f32)", flush=True)
+
+
+if __name__ == "__main__":
+    shapes = sys.argv[1:] or ["153600x512x384", "153600x384x512", "153600x1152x384", "38400x2048x1536",
+                              "153600x384x384"]
+    for s in shapes:
+        M, N, K = (int(v) for v in s.split("x"))
+        probe(M, N, K)
