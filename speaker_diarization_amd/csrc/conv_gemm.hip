@@ -264,6 +264,8 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(p.lda % 4 == 0 && p.a_coff % 4 == 0, kErrInvalid, "conv_gemm: lda/a_coff must be multiples of 4");
   SD_CHECK(p.N > 0 && p.B > 0 && p.Ho > 0 && p.Wo > 0, kErrInvalid, "conv_gemm: empty problem");
   SD_CHECK(!p.gate || p.gate_seg > 0, kErrInvalid, "conv_gemm: gate_seg must be > 0");
+  SD_CHECK(!p.glu || (bf16 && gemm_stream_supported(p)), kErrInvalid,
+           "conv_gemm: the GLU epilogue exists on the bf16 streaming path only");
   if (bf16) {
     conv_gemm_bf16(p, st);
     return;

@@ -64,7 +64,24 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
   L.in_b = up(p + ".self_attn.in_proj_bias");
   { ConvL a = linear(p + ".self_attn.out_proj"); L.out_proj = a.w; L.out_b = a.beta; }
   L.cv_lng = up(p + ".conv_module.layer_norm.weight"); L.cv_lnb = up(p + ".conv_module.layer_norm.bias");
-  { ConvL a = linear(p + ".conv_module.sequential.0"); L.pw1 = a.w; L.pw1_b = a.beta; }
+  {
+    // pointwise_conv1 (2C out) with its rows interleaved [16 values | 16 gates] so a GEMM
+    // tile holds each channel's value and gate together (GLU epilogue / glu_dwconv).
+    int N, Cin, kh, kw;
+    const std::vector<float> w = ps.pack(p + ".conv_module.sequential.0.weight", N, Cin, kh, kw);
+    const std::vector<float>& b = ps.get(p + ".conv_module.sequential.0.bias").data;
+    SD_CHECK(N % 32 == 0 && (int)b.size() == N, kErrParam, "conv_module.sequential.0 shape");
+    const int C = N / 2;
+    const size_t K = w.size() / N;
+    std::vector<float> wp(w.size()), bp(N);
+    for (int r = 0; r < N; ++r) {
+      const int r2 = glu_interleave_row(r, C);
+      std::copy(w.begin() + r * K, w.begin() + (r + 1) * K, wp.begin() + r2 * K);
+      bp[r2] = b[r];
+    }
+    L.pw1 = upload_packed(arena, wp, N, Cin, kh, kw, bf16);
+    L.pw1_b = arena.upload(bp);
+  }
   {
     const HostTensor& dw = ps.get(p + ".conv_module.sequential.2.weight");  // (C, 1, k)
     SD_CHECK(dw.shape.size() == 3 && dw.shape[1] == 1, kErrParam, "depthwise conv weight shape");
@@ -147,13 +164,18 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   conv_gemm(lin(ao, rows, E, L.out_proj, L.out_b, y, E), bf, st);
   // convolution module (no padding mask in torchaudio's conv module)
   add_layernorm(X, y.p, bf, rows, E, L.cv_lng, L.cv_lnb, 1e-5f, true, y.p, bf, st);
-  conv_gemm(lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E), bf, st);
-  if (L.group_norm) {
-    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, w.partial, false, bf, st);
-    groupnorm_silu(ao.p, S, T, E, w.partial, L.gn_g, L.gn_b, 1e-5f, bf, st);
-  } else {
-    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, nullptr, true, bf, st);
+  // pointwise_conv1 + GLU: fused into the streaming GEMM's epilogue when it runs (bf16),
+  // otherwise applied by the depthwise-conv kernel on load.
+  ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
+  p1.glu = 1;
+  const bool glu_epi = bf && gemm_stream_supported(p1);
+  if (!glu_epi) {
+    p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
   }
+  conv_gemm(p1, bf, st);
+  glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
+             !glu_epi, bf, st);
+  if (L.group_norm) groupnorm_silu(ao.p, S, T, E, w.partial, L.gn_g, L.gn_b, 1e-5f, bf, st);
   conv_gemm(lin(ao, rows, E, L.pw2, L.pw2_b, y, E), bf, st);
   // ffn2 + final LayerNorm
   add_layernorm(X, y.p, bf, rows, E, L.f2_lng, L.f2_lnb, 1e-5f, true, y.p, bf, st);

@@ -27,6 +27,7 @@ constexpr int SBK = 64;           // k chunk
 constexpr int NST = 4;            // A ring stages
 constexpr int SD_ = NST - 1;      // prefetch distance
 constexpr int kStreamThreads = 512;
+constexpr int kGluEpi = 100;      // epilogue "activation" id of the GLU mode
 constexpr uint32_t kOOB = 0x80000000u;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -200,7 +201,28 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
     }
-    if (kc == KT - 1) {
+    if (kc == KT - 1 && ACT == kGluEpi) {
+      // ---- GLU epilogue: lane holds value (nt even) and gate (nt + 1) of channel
+      // ((n0 + wn*TN + nt*16) / 32) * 16 + l15; bf16 output N/2 wide.
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt += 2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = fmaf(acc[mt][nt][r], al[nt], be[nt]);
+            const float gt = fmaf(acc[mt][nt + 1][r], al[nt + 1], be[nt + 1]);
+            const int m = mb + mt * 16 + r;
+            const int ch = ((n0 + wn * TN + nt * 16) >> 5) * 16 + l15;
+            const uint32_t off = (m < M && 2 * ch < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + ch) * 2) : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b16(f2bf_bits(a / (1.f + __expf(-gt))), ro, off, 0, 0);
+          }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      issued += MT * NT * 2;
+    } else if (kc == KT - 1) {
       // ---- epilogue of tile j straight from the accumulators
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -280,7 +302,8 @@ int stream_bn(const ConvGemmArgs& p) {
 }  // namespace
 
 bool gemm_stream_supported(const ConvGemmArgs& p) {
-  if (getenv("SDIAR_NO_STREAM_GEMM")) return false;
+  static const bool disabled = getenv("SDIAR_NO_STREAM_GEMM") != nullptr;
+  if (disabled) return false;
   const int M = p.B * p.Ho * p.Wo;
   const bool row_major = p.o_sn == 1 && ((p.B == 1 && p.Ho == 1) ||
                                          (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh));
@@ -297,6 +320,13 @@ void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st) {
     SD_HIP(hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const bool wide = stream_bn(p) == 128;
+  if (p.glu) {
+    SD_CHECK(p.act == kActNone && p.out_bf16 && p.N % 32 == 0, kErrInvalid,
+             "GLU epilogue: bf16 output, no activation, N % 32 == 0");
+    wide ? launch_stream<128, kGluEpi>(p, st) : launch_stream<64, kGluEpi>(p, st);
+    SD_LAUNCH_CHECK();
+    return;
+  }
   switch (p.act) {
     case kActRelu: wide ? launch_stream<128, kActRelu>(p, st) : launch_stream<64, kActRelu>(p, st); break;
     case kActSigmoid: wide ? launch_stream<128, kActSigmoid>(p, st) : launch_stream<64, kActSigmoid>(p, st); break;

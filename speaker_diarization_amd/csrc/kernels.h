@@ -30,7 +30,16 @@ struct ConvGemmArgs {
   void* out = nullptr;               // out[b*o_sb + ho*o_sh + wo*o_sw + n*o_sn]
   bool out_bf16 = false;
   int64_t o_sb = 0, o_sh = 0, o_sw = 0, o_sn = 1;
+  // GLU epilogue (streaming path only): the N GEMM columns are 32-wide groups [a 16 | gate 16]
+  // (weights permuted by glu_interleave_rows); output channel g*16 + j = a * sigmoid(gate), N/2 wide.
+  int glu = 0;
 };
+// Row order of a GLU projection (2C, K) -> groups of [16 value rows | their 16 gate rows].
+inline int glu_interleave_row(int r, int C) {   // new row index of original row r
+  const bool gate = r >= C;
+  const int c = gate ? r - C : r;
+  return (c / 16) * 32 + (gate ? 16 : 0) + c % 16;
+}
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
 void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
@@ -109,13 +118,14 @@ void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out
                           hipStream_t st);
 
 // ---------------------------------------------------------------- conformer conv module
-// GLU over channel pairs (a = x[:, c], g = x[:, C + c]) followed by a depthwise
-// conv over time (kernel k, pad (k-1)/2, with bias).  x: (S, T, 2C); y: (S, T, C).
+// Depthwise conv over time (kernel k, pad (k-1)/2, with bias), y: (S, T, C).
+// glu_in: x is the pw1 output (S, T, 2C) with rows interleaved [16 values | 16 gates]
+// (glu_interleave_row) and the GLU is applied on load; else x is already gated (S, T, C).
 // Writes per (sequence, channel-block) partial sums for GroupNorm(1, C), or with
 // fused_silu (BatchNorm already folded into w/bias) stores SiLU(y) and no partials.
 void glu_dwconv(const void* x, int S, int T, int C, const float* w /*C x k*/,
                 const float* bias, int k, void* y, float* partial /*S x nblk x 2*/, bool fused_silu,
-                bool io_bf16, hipStream_t st);
+                bool glu_in, bool io_bf16, hipStream_t st);
 // GroupNorm(num_groups=1) over (T, C) of each sequence, affine, then SiLU (in place).
 void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
                     const float* b, float eps, bool io_bf16, hipStream_t st);

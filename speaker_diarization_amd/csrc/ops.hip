@@ -372,53 +372,108 @@ void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out
 constexpr int kDwCB = 64;    // channels per block
 constexpr int kDwTT = 64;    // time tile
 
+// One block per (sequence, 64 channels); lane = channel, so every LDS column read is
+// conflict-free and every output row store is one coalesced 64-channel segment.
+// Time is processed in tiles of kDwTT outputs: the GLU'd inputs of the tile (+ k-1
+// halo rows) are staged in LDS with 16-B vector loads, then each wave produces runs
+// of kDwR consecutive outputs from a register window (kDwR + k - 1 LDS reads for
+// kDwR * k FMAs).  The channel's k taps live in registers.
+constexpr int kDwR = 8;
+constexpr int kDwMaxK = 31;
+
 template <bool BF>
 __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __restrict__ x, int T, int C,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ bias, int k,
                                                          act_t<BF>* __restrict__ y,
-                                                         float* __restrict__ partial, int fused_silu) {
-  extern __shared__ float sm[];
+                                                         float* __restrict__ partial, int fused_silu,
+                                                         int glu_in) {
+  __shared__ float g[(kDwTT + kDwMaxK - 1) * kDwCB];
+  __shared__ float red[2][256];
   const int pad = (k - 1) / 2;
   const int s = blockIdx.y;
   const int c0 = blockIdx.x * kDwCB;
   const int nblk = gridDim.x;
-  float* g = sm;                          // [(kDwTT + k - 1)][kDwCB]
-  float* wsm = g + (kDwTT + k - 1) * kDwCB;  // [kDwCB][k]
-  __shared__ float red[2][256];
-  for (int i = threadIdx.x; i < kDwCB * k; i += blockDim.x) {
-    int cc = i / k, j = i % k;
-    wsm[i] = (c0 + cc < C) ? w[(int64_t)(c0 + cc) * k + j] : 0.f;
-  }
-  const act_t<BF>* xs = x + (int64_t)s * T * 2 * C;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = c0 + lane;
+  float wr[kDwMaxK];
+#pragma unroll
+  for (int j = 0; j < kDwMaxK; ++j) wr[j] = (j < k && c < C) ? w[(int64_t)c * k + j] : 0.f;
+  const float bv = (bias && c < C) ? bias[c] : 0.f;
+  const act_t<BF>* xs = x + (int64_t)s * T * (glu_in ? 2 : 1) * C;
   act_t<BF>* ys = y + (int64_t)s * T * C;
   float lsum = 0.f, lsq = 0.f;
-  const int cc = threadIdx.x % kDwCB;
-  const int tq = threadIdx.x / kDwCB;   // 0..3
+  constexpr int VEC = BF ? 8 : 4;             // elements per 16-B load
+  constexpr int CPR = kDwCB / VEC;            // vector chunks per row
   for (int t0 = 0; t0 < T; t0 += kDwTT) {
+    const int span = min(kDwTT, T - t0) + k - 1;
     __syncthreads();
-    const int span = kDwTT + k - 1;
-    for (int i = threadIdx.x; i < span * kDwCB; i += blockDim.x) {
-      int tt = i / kDwCB, c = i % kDwCB;
-      int t = t0 - pad + tt;
-      float v = 0.f;
-      if (t >= 0 && t < T && c0 + c < C) {
-        float a = ld_act(xs, (int64_t)t * 2 * C + c0 + c);
-        float gg = ld_act(xs, (int64_t)t * 2 * C + C + c0 + c);
-        v = a / (1.f + expf(-gg));
+    for (int i = threadIdx.x; i < span * CPR; i += blockDim.x) {
+      const int tt = i / CPR, ch = (i % CPR) * VEC;
+      const int t = t0 - pad + tt;
+      float v[VEC];
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) v[u] = 0.f;
+      if (t >= 0 && t < T && c0 + ch < C && !glu_in) {
+        const act_t<BF>* ra = xs + (int64_t)t * C + c0 + ch;   // already gated (GLU epilogue of pw1)
+        if constexpr (BF) {
+          const uint4 a4 = *reinterpret_cast<const uint4*>(ra);
+          const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v[2 * u] = __uint_as_float(aw[u] << 16);
+            v[2 * u + 1] = __uint_as_float(aw[u] & 0xffff0000u);
+          }
+        } else {
+          const float4 a4 = *reinterpret_cast<const float4*>(ra);
+          v[0] = a4.x; v[1] = a4.y; v[2] = a4.z; v[3] = a4.w;
+        }
+      } else if (t >= 0 && t < T && c0 + ch < C) {
+        // pw1 rows interleaved in 32-column groups [16 values | 16 gates] (glu_interleave_row)
+        const int cc = c0 + ch;
+        const act_t<BF>* ra = xs + (int64_t)t * 2 * C + (cc / 16) * 32 + cc % 16;
+        if constexpr (BF) {
+          const uint4 a4 = *reinterpret_cast<const uint4*>(ra);
+          const uint4 g4 = *reinterpret_cast<const uint4*>(ra + 16);
+          const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w}, gw[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float a0 = __uint_as_float(aw[u] << 16), a1 = __uint_as_float(aw[u] & 0xffff0000u);
+            const float g0 = __uint_as_float(gw[u] << 16), g1 = __uint_as_float(gw[u] & 0xffff0000u);
+            v[2 * u] = a0 / (1.f + __expf(-g0));
+            v[2 * u + 1] = a1 / (1.f + __expf(-g1));
+          }
+        } else {
+          const float4 a4 = *reinterpret_cast<const float4*>(ra);
+          const float4 g4 = *reinterpret_cast<const float4*>(ra + 16);
+          v[0] = a4.x / (1.f + __expf(-g4.x));
+          v[1] = a4.y / (1.f + __expf(-g4.y));
+          v[2] = a4.z / (1.f + __expf(-g4.z));
+          v[3] = a4.w / (1.f + __expf(-g4.w));
+        }
       }
-      g[i] = v;
+      float* dst = g + tt * kDwCB + ch;
+#pragma unroll
+      for (int u = 0; u < VEC; u += 4) *reinterpret_cast<float4*>(dst + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
     }
     __syncthreads();
-    if (c0 + cc < C) {
-      const float bv = bias ? bias[c0 + cc] : 0.f;
-      for (int tt = tq; tt < kDwTT && t0 + tt < T; tt += 4) {
+    const int nout = min(kDwTT, T - t0);
+    for (int r0 = wv * kDwR; r0 < nout; r0 += 4 * kDwR) {
+      float win[kDwR + kDwMaxK - 1];
+#pragma unroll
+      for (int i = 0; i < kDwR + kDwMaxK - 1; ++i) win[i] = (i < kDwR + k - 1) ? g[(r0 + i) * kDwCB + lane] : 0.f;
+#pragma unroll
+      for (int r = 0; r < kDwR; ++r) {
         float acc = bv;
-        for (int j = 0; j < k; ++j) acc = fmaf(wsm[cc * k + j], g[(tt + j) * kDwCB + cc], acc);
-        if (fused_silu) acc = acc / (1.f + expf(-acc));
-        st_act(ys, (int64_t)(t0 + tt) * C + c0 + cc, acc);
-        lsum += acc;
-        lsq += acc * acc;
+#pragma unroll
+        for (int j = 0; j < kDwMaxK; ++j) acc = fmaf(wr[j], win[r + j], acc);
+        if (fused_silu) acc = acc / (1.f + __expf(-acc));
+        const int t = t0 + r0 + r;
+        if (r0 + r < nout && c < C) {
+          st_act(ys, (int64_t)t * C + c, acc);
+          lsum += acc;
+          lsq += acc * acc;
+        }
       }
     }
   }
@@ -440,18 +495,19 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
 }
 
 void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
-                void* y, float* partial, bool fused_silu, bool io_bf16, hipStream_t st) {
+                void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st) {
   SD_CHECK(fused_silu || partial, kErrInvalid, "glu_dwconv: GroupNorm partials buffer required");
+  SD_CHECK(k >= 1 && k <= kDwMaxK && k % 2 == 1, kErrInvalid, "glu_dwconv: kernel size must be odd and <= 31");
+  SD_CHECK(C % 16 == 0, kErrInvalid, "glu_dwconv: channels must be a multiple of 16");
   dim3 grid(cdiv(C, kDwCB), S);
-  size_t smem = sizeof(float) * ((kDwTT + k - 1) * kDwCB + kDwCB * k);
-  ProfScope prof("glu_dwconv", 2.0 * S * T * C * k, 4.0 * S * T * 3.0 * C, st);
+  const double eb = io_bf16 ? 2.0 : 4.0;
+  ProfScope prof(glu_in ? "glu_dwconv" : "dwconv", 2.0 * S * T * C * k, eb * S * T * (glu_in ? 3.0 : 2.0) * C, st);
   if (io_bf16)
-    hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), smem, st,
-                       reinterpret_cast<const uint16_t*>(x), T, C, w, bias, k, reinterpret_cast<uint16_t*>(y),
-                       partial, (int)fused_silu);
+    hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<const uint16_t*>(x), T,
+                       C, w, bias, k, reinterpret_cast<uint16_t*>(y), partial, (int)fused_silu, (int)glu_in);
   else
-    hipLaunchKernelGGL(glu_dwconv_kernel<false>, grid, dim3(256), smem, st, reinterpret_cast<const float*>(x),
-                       T, C, w, bias, k, reinterpret_cast<float*>(y), partial, (int)fused_silu);
+    hipLaunchKernelGGL(glu_dwconv_kernel<false>, grid, dim3(256), 0, st, reinterpret_cast<const float*>(x), T, C,
+                       w, bias, k, reinterpret_cast<float*>(y), partial, (int)fused_silu, (int)glu_in);
   SD_LAUNCH_CHECK();
 }
 
