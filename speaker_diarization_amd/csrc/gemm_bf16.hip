@@ -294,6 +294,10 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st) {
     key += " M=" + std::to_string(M) + " N=" + std::to_string(p.N) + " K=" + std::to_string(p.K) +
            " taps=" + std::to_string(p.kh * p.kw) + (p.a_bf16 ? " Abf" : " Af32") + (p.pre_scale ? " pre" : "");
   ProfScope prof(key.c_str(), flops, bytes, st);
+  if (fcm_conv_supported(p)) {      // CAM++ FCM 3x3 32->32 convs (fcm_conv.hip)
+    conv_fcm3x3(p, st);
+    return;
+  }
   if (gemm_stream_supported(p)) {   // weight-resident streaming path (gemm_stream.hip)
     conv_gemm_stream(p, st);
     return;

@@ -45,6 +45,8 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA produ
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
 bool gemm_stream_supported(const ConvGemmArgs& p);            // bf16 A linear, K%64==0, K<=768, no res
 void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
+bool fcm_conv_supported(const ConvGemmArgs& p);               // bf16 3x3 32->32, pad 1, freq stride 1|2
+void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
 
 // Plain row-major linear layer helper: out[m*ldo + o_coff + n] = act(A[m*lda+k]·W[n][k] * alpha + beta (+res)).
