@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--minutes", type=float, default=None, help="meeting minutes per GPU")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64, help="reference batch (windows, zero-pad unit)")
-    ap.add_argument("--device-batch", type=int, default=256, help="windows per device launch")
+    ap.add_argument("--device-batch", type=int, default=640, help="windows per device launch (a 10-min meeting in one launch)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")

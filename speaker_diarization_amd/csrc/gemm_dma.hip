@@ -124,11 +124,52 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
 
   const int KT = (p.K + BK - 1) / BK;
   const int l15 = lane & 15, lk = lane >> 4;
+  // Optional BN-ReLU prologue (CAM dense layers: nonlinear1 before linear1): applied
+  // in place on the landed A stage, 16 B per thread-step, before the MFMAs read it.
+  // Zero-filled K-tail columns stay harmless: their weight rows are zero-filled too.
+  // Thread i always touches rows r = i/8 + 32j (r & 7 fixed) and physical chunk i & 7, so
+  // its logical chunk, hence its 8 k columns, are fixed: 2 x 2 float4 loads per k-tile.
+  const int pre_pc = tid & 7;
+  const int pre_lc = pre_pc ^ ((tid >> 3) & 7);
+  auto prologue = [&](int kt, int stg) {
+    uint16_t* As = sm + stg * STAGE;
+    const int k = kt * BK + pre_lc * 8;
+    float sc[8], sh[8];
+    if (k + 8 <= p.K) {
+      const float4 s0 = *reinterpret_cast<const float4*>(p.pre_scale + k);
+      const float4 s1 = *reinterpret_cast<const float4*>(p.pre_scale + k + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(p.pre_shift + k);
+      const float4 h1 = *reinterpret_cast<const float4*>(p.pre_shift + k + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { sc[u] = 0.f; sh[u] = 0.f; }   // K tail: A*0 + 0 (weights are 0 too)
+    }
+    for (int i = tid; i < BM * 8; i += 256) {
+      uint4* ptr = reinterpret_cast<uint4*>(As + (i >> 3) * BK + pre_pc * 8);
+      uint4 v = *ptr;
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float x0 = fmaxf(fmaf(__uint_as_float(w[u] << 16), sc[2 * u], sh[2 * u]), 0.f);
+        const float x1 = fmaxf(fmaf(__uint_as_float(w[u] & 0xffff0000u), sc[2 * u + 1], sh[2 * u + 1]), 0.f);
+        w[u] = pack_bf2(x0, x1);
+      }
+      *ptr = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  };
+  const bool pre = p.pre_scale != nullptr;
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int stg = kt & 1;
+    if (pre) {
+      prologue(kt, stg);
+      // LDS writes done, then a plain barrier (a __syncthreads() fence would add vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     if (kt + 1 < KT) issue(kt + 1, stg ^ 1);
     const uint16_t* As = sm + stg * STAGE;
     const uint16_t* Bs = As + BM * BK;
@@ -312,7 +353,7 @@ bool gemm_dma_supported(const ConvGemmArgs& p) {
   const int taps = p.kh * p.kw;
   const int64_t a_bytes = ((int64_t)p.B * p.H * p.W) * p.lda * 2;
   const int64_t w_bytes = (int64_t)p.N * p.K * 2;
-  return p.a_bf16 && !p.pre_scale && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
+  return p.a_bf16 && (!p.pre_scale || (taps == 1 && p.pre_shift)) && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
          p.a_coff % 8 == 0 && a_bytes < (int64_t)kOOB && w_bytes < (int64_t)kOOB;
 }
 

@@ -12,7 +12,7 @@ variant = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 minutes = float(sys.argv[2]) if len(sys.argv) > 2 else 10.0
 cfg = TSVADConfig(rs_len=4) if variant == 0 else TSVADConfig.ots_vad_v1(rs_len=6)
 dev = torch.device("cuda", 0)
-m = TSVADModel(cfg, device=dev, precision="bf16", max_batch=256)
+m = TSVADModel(cfg, device=dev, precision="bf16", max_batch=int(os.environ.get("SDIAR_MAX_BATCH", "256")))
 m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=777)))
 pipe = TSVADPipeline(m, 1, 64)
 mt = make_meeting(minutes * 60, 4, seed=777)
