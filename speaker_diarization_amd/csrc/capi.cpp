@@ -374,6 +374,15 @@ int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, 
     a.qkv = qkv; a.S = S_; a.T = T; a.D = D; a.nh = nh; a.ld_qkv = 3 * D;
     a.out = out; a.ldo = D; a.scale = 1.f / std::sqrt((float)(D / nh));
     a.causal = causal; a.causal_delay = causal_delay; a.key_len = key_len;
+    if (precision == 2) {   // bf16 storage: qkv and out in bf16 (the encoders' layout)
+      hipStream_t st = S(stream);
+      Scratch qb((size_t)S_ * T * 3 * D * 2, st), ob((size_t)S_ * T * D * 2, st);
+      sd::f32_to_bf16(qkv, (int64_t)S_ * T * 3 * D, qb.p, st);
+      a.qkv = qb.p; a.out = ob.p; a.io_bf16 = true;
+      sd::attention(a, true, st);
+      sd::bf16_to_f32(ob.p, (int64_t)S_ * T * D, out, st);
+      return;
+    }
     sd::attention(a, precision == 1, S(stream));
   });
 }

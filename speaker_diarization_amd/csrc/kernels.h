@@ -137,9 +137,11 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 // precomputed input projections gx (B, T, ndir*4H) (bias_ih + bias_hh folded in).
 // whh: (ndir, 4H, H) fp32.  out: (B, T, ldo) at column dir*H.
 // h0/c0 optional (ndir, B, H); hT/cT optional outputs (ndir, B, H).
+// whh_bf16 (optional, same layout in bf16 bits): bf16-MFMA recurrence (bf16 mode); the
+// cell state, gates and h stay fp32, h is rounded to bf16 only as the MFMA operand.
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
-                     float* hT, float* cT, float* work, hipStream_t st);
+                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr);
 
 // ---------------------------------------------------------------- frontend
 // Kaldi fbank (torchaudio.compliance.kaldi.fbank semantics used by
@@ -168,6 +170,7 @@ void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* 
 
 namespace sd {
 void f32_to_bf16(const float* x, int64_t n, void* y, hipStream_t st);
+void bf16_to_f32(const void* x, int64_t n, float* y, hipStream_t st);
 
 // ---------------------------------------------------------------- eend frontend + EDA glue (eend.hip)
 // librosa-style centred STFT (float64) -> log10 mel power: out (n_frames, n_mels) float64.

@@ -670,4 +670,16 @@ void f32_to_bf16(const float* x, int64_t n, void* y, hipStream_t st) {
   SD_LAUNCH_CHECK();
 }
 
+__global__ void bf16_to_f32_kernel(const uint16_t* __restrict__ x, int64_t n, float* __restrict__ y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = bf_bits2f(x[i]);
+}
+
+void bf16_to_f32(const void* x, int64_t n, float* y, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint16_t*>(x), n, y);
+  SD_LAUNCH_CHECK();
+}
+
 }  // namespace sd

@@ -177,6 +177,7 @@ void TsvadModel::finalize() {
     lstm_ih_ = upload_packed(arena_, wih, 8 * H, (int)wi0.shape[1], 1, 1, cfg_.bf16);
     lstm_b_ = arena_.upload(bias);
     lstm_hh_ = arena_.upload(whh);
+    if (cfg_.bf16) lstm_hh_bf_ = upload_packed(arena_, whh, 2 * 4 * H, H, 1, 1, true).w;
     fc_ = loader().linear("fc");
   }
   auto extra = ps_.unused();
@@ -333,7 +334,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
-                    nullptr, lstm_work_, st);
+                    nullptr, lstm_work_, st, lstm_hh_bf_);
     ConvGemmArgs f = conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);

@@ -73,6 +73,7 @@ class TsvadModel {
   std::vector<ConformerL> conf_;
   PackedW lstm_ih_;
   const float *lstm_b_ = nullptr, *lstm_hh_ = nullptr;
+  const void* lstm_hh_bf_ = nullptr;   // bf16 copy of W_hh (bf16 mode)
   ConvL fc_;
 
   // Workspace.

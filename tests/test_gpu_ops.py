@@ -124,9 +124,10 @@ def _attn_ref(qkv, S, T, D, nh, causal=0, delay=0, key_len=None):
     return (torch.softmax(s, -1) @ v).permute(0, 2, 1, 3).reshape(S * T, D)
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("S,T,D,nh,causal", [(8, 100, 384, 4, 0), (6, 150, 384, 8, 0), (1, 777, 256, 4, 0),
-                                             (2, 300, 256, 4, 1), (3, 33, 512, 4, 0)])
+                                             (2, 300, 256, 4, 1), (3, 33, 512, 4, 0), (5, 256, 256, 4, 1),
+                                             (40, 6, 256, 4, 0), (2, 129, 1024, 8, 0)])
 def test_attention(gpu, precision, S, T, D, nh, causal):
     g = torch.Generator().manual_seed(S * T)
     qkv = torch.randn(S * T, 3 * D, generator=g)
@@ -141,7 +142,8 @@ def test_attention(gpu, precision, S, T, D, nh, causal):
         assert _rel_err(out.cpu(), ref) < 2e-2
 
 
-def test_attention_key_len(gpu):
+@pytest.mark.parametrize("precision", [0, 2])
+def test_attention_key_len(gpu, precision):
     S, T, D, nh = 3, 70, 384, 8
     g = torch.Generator().manual_seed(5)
     qkv = torch.randn(S * T, 3 * D, generator=g)
@@ -149,10 +151,13 @@ def test_attention_key_len(gpu):
     ref = _attn_ref(qkv, S, T, D, nh, key_len=kl)
     out = torch.empty(S * T, D, device=gpu)
     kld = kl.to(gpu)
-    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, 0, 0, kld.data_ptr(), out.data_ptr(), 0,
+    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, 0, 0, kld.data_ptr(), out.data_ptr(), precision,
               _lib.stream_ptr(gpu))
     torch.cuda.synchronize()
-    torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 2e-2
 
 
 def test_attention_large_logits(gpu):
