@@ -30,6 +30,16 @@ WORKLOADS = {
                "CAM++_ots_vad + 6-layer Conformer + BiLSTM (ots_vad_style v1), rs_len 6 s, shift 1 s"),
     "c4": dict(variant=0, rs_len=4, minutes=60.0, desc="C4: 4-spk long-form meeting, TS-VAD CAM++ + "
                "transformer (default TSVADConfig), rs_len 4 s, shift 1 s"),
+    # secondary workloads (EEND family); not the BASELINE headline line
+    "c1": dict(kind="eda", model_type="TransformerEda", layers=2, n_spk=2, minutes=10.0, num_speakers=2,
+               desc="C1: 2-spk 16 kHz recording, EEND-EDA TransformerEda 2-layer (infer_eda.py: logmel23_mn, "
+                    "context 7, subsampling 10, 2000-frame chunks), num_speakers 2"),
+    "c3": dict(kind="eda", model_type="EendEda", layers=4, n_spk=4, minutes=10.0, num_speakers=None,
+               desc="C3: 4-spk 16 kHz recording, EEND-EDA EendEda 4-layer transformer, attractor-threshold "
+                    "speaker counting"),
+    "c5": dict(kind="fseend", n_spk=3, minutes=10.0,
+               desc="C5: 8 kHz recording, FS-EEND (4-layer causal encoder, shared 2x fusion decoder, "
+                    "logmel23, 100 ms frames), whole recording per test() call; replicas only"),
 }
 
 PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
@@ -208,5 +218,122 @@ def main():
         dist.destroy_process_group()
 
 
+def main_eend(a, wl):
+    """EEND-EDA (c1/c3) and FS-EEND (c5): wav in HBM -> frontend -> model -> activities.
+    Multi-GPU: EEND-EDA shards chunks (all-gather of activities); FS-EEND runs replicas."""
+    import torch
+    import torch.distributed as dist
+    from speaker_diarization_amd import _lib
+    from speaker_diarization_amd.synth import make_meeting
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    minutes = a.minutes if a.minutes is not None else wl["minutes"]
+    kind = wl["kind"]
+    prec = a.precision
+    if kind == "eda":
+        from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, infer_recording
+        from speaker_diarization_amd.eend_eda.models import EendEdaModel, TransformerEdaModel
+        from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
+        total_s = minutes * 60.0 * world          # weak scaling: chunks of an N x longer recording
+        meeting = make_meeting(total_s, n_spk=wl["n_spk"], seed=777)
+        torch.manual_seed(777)
+        kw = dict(n_speakers=wl["n_spk"], in_size=345, n_heads=4, n_units=256, n_layers=wl["layers"],
+                  precision=prec, max_seqs=32, max_frames=2000)
+        m = TransformerEdaModel(**kw) if wl["model_type"] == "TransformerEda" else EendEdaModel(**kw)
+        cfg = EDAConfig(model_type=wl["model_type"], n_layers=wl["layers"])
+        sd_np = eda_state_dict(cfg, seed=777)
+        m.load_state_dict(to_torch(sd_np))
+        iargs = EdaInferArgs(num_speakers=wl["num_speakers"])
+        wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+
+        def step():
+            try:
+                return infer_recording(m, wav, iargs)
+            except (ValueError, IndexError):
+                # the reference's own selection quirks on random weights: threshold mode np.vstack of
+                # chunks with different speaker counts, TransformerEda top-n IndexError (SURVEY §9.2);
+                # the device forward of every chunk has completed either way
+                return None
+        frames = meeting.wav.size // 160
+    else:
+        from speaker_diarization_amd.feature import eend_features
+        from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
+        from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
+        total_s = minutes * 60.0                   # replicas: every rank its own recording
+        meeting = make_meeting(total_s, n_spk=wl["n_spk"], seed=777 + rank, sample_rate=8000)
+        n_sub = -(-((meeting.wav.size // 80)) // 10) + 1
+        m = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=prec,
+                                           max_seqs=1, max_frames=max(n_sub, 16), max_nspks=6)
+        cfg = FSEENDConfig()
+        sd_np = fseend_state_dict(cfg, seed=777)
+        m.load_state_dict(to_torch(sd_np))
+        wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+
+        def step():
+            f = eend_features(wav, 8000, 200, 80, "logmel23", 7, 10, ld=m.in_ld)
+            return m.test_device(f[None], [f.shape[0]], 6, want_emb=False, want_attractors=False)
+        frames = meeting.wav.size // 80 * world
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernels = None
+    if not a.no_kernel_timing:
+        lib = _lib.load()
+        lib.sd_prof_reset()
+        lib.sd_prof_enable(1)
+        step()
+        torch.cuda.synchronize()
+        lib.sd_prof_enable(0)
+        kernels = _lib.prof_stats()
+    if rank == 0:
+        line = {"metric": "diarized frames/sec (10 ms hop)", "value": round(frames * a.steps / elapsed, 1),
+                "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                "ms_per_step": round(elapsed / a.steps * 1000.0, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": prec,
+                "data": "synthetic recording (speaker_diarization_amd/synth.py), seeded random weights",
+                "config": {"workload": wl["desc"], "minutes_per_gpu": minutes,
+                           "parallelism": ("chunk-shard x%d + RCCL all-gather" % world if kind == "eda" else
+                                           "replicas x%d" % world) if world > 1 else "1 GPU"}}
+        if kernels:
+            tot = sum(v["ms"] for v in kernels.values())
+            line["kernel_ms_share"] = {k: round(v["ms"] / tot, 3) for k, v in
+                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:10]}
+            dom = max(kernels, key=lambda k: kernels[k]["ms"])
+            st = kernels[dom]
+            if st["flops"] > 0:
+                ach = st["flops"] / (st["ms"] * 1e-3) / 1e12
+                pk = PEAKS["bf16" if dom.endswith("bf16") else "f32"]
+                line["roofline"] = dict(bound="mfma", achieved=round(ach, 2), peak=pk, unit="TFLOP/s",
+                                        frac=round(ach / pk, 4), traffic=None, kernel=dom)
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main()
+    _a = parse()
+    if WORKLOADS[_a.workload].get("kind") in ("eda", "fseend"):
+        main_eend(_a, WORKLOADS[_a.workload])
+    else:
+        main()
