@@ -192,6 +192,22 @@ int sd_window_cmn(const float* feats, int n_mels, const int* win_start, const in
 int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start,
                        const int* len, int dis, int chunk, int n_frames, float* out, void* stream);
 
+/* ------------------------------------------------------------------ postprocess
+ * Replaces the host loop of ts_vad2/infer.py:72-130 (postprocess): per track
+ * (one (meeting, speaker) posterior row of T frames) scipy.signal.medfilt(med_filter)
+ * -> for each threshold: >= threshold (float32 compare), change_zeros_to_ones
+ * (silence runs <= min_silence_frames become speech, :27-47), change_ones_to_zeros
+ * (speech runs <= min_speech_frames become silence, :50-70) -> speech runs as
+ * [begin, end) frame pairs.  min_*_frames = int(min_* // frame_len) as the recipe
+ * computes it.  post: device (rows, T) f32.  thresholds: HOST array (1..16).
+ * seg_begin/seg_end: device int32 (rows * n_thresholds, cap), cap >= (T+1)/2;
+ * n_seg: device int32 (rows * n_thresholds), row-major (row, threshold).
+ * RTTM formatting stays on the host (speaker_diarization_amd/ts_vad/postprocess.py).
+ * T <= 524288 frames. */
+int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, const float* thresholds,
+                            int n_thresholds, int min_silence_frames, int min_speech_frames, int cap,
+                            int* seg_begin, int* seg_end, int* n_seg, void* stream);
+
 /* ------------------------------------------------------------------ ops (parity tests)
  * precision: 0 fp32, 1 bf16 MFMA (fp32 activations), 2 bf16 MFMA on bf16 activations
  * (the input is converted first; exercises the LDS-DMA GEMM path).

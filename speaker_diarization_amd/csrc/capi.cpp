@@ -307,6 +307,30 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
   });
 }
 
+int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, const float* thresholds,
+                            int n_thresholds, int min_silence_frames, int min_speech_frames, int cap,
+                            int* seg_begin, int* seg_end, int* n_seg, void* stream) {
+  return guard([&] {
+    SD_CHECK(rows >= 0 && T >= 0, sd::kErrInvalid, "postprocess: negative shape");
+    SD_CHECK(n_thresholds >= 1 && n_thresholds <= sd::ThresholdSet::kMax, sd::kErrInvalid,
+             "postprocess: 1..16 thresholds");
+    SD_CHECK(T <= sd::segments_max_frames(), sd::kErrInvalid, "postprocess: track too long");
+    SD_CHECK(cap >= (T + 1) / 2, sd::kErrInvalid, "postprocess: cap < (T+1)/2");
+    if (rows == 0 || T == 0) {
+      if (rows > 0) SD_HIP(hipMemsetAsync(n_seg, 0, sizeof(int) * rows * n_thresholds, S(stream)));
+      return;
+    }
+    hipStream_t st = S(stream);
+    sd::ThresholdSet thr;
+    thr.n = n_thresholds;
+    for (int i = 0; i < n_thresholds; ++i) thr.v[i] = thresholds[i];
+    Scratch med((size_t)rows * T * sizeof(float), st);
+    sd::medfilt(post, rows, T, med_filter, static_cast<float*>(med.p), st);
+    sd::run_segments(static_cast<const float*>(med.p), rows, T, thr, min_silence_frames, min_speech_frames, cap,
+                     seg_begin, seg_end, n_seg, st);
+  });
+}
+
 int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, int N, int act,
                  float* out, int precision, void* stream) {
   return guard([&] {

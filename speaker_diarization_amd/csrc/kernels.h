@@ -166,6 +166,20 @@ void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16,
 namespace sd {
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
                      int dis, int chunk, int n_frames, float* out, hipStream_t st);
+
+// ---------------------------------------------------------------- postprocess.hip
+struct ThresholdSet {
+  static constexpr int kMax = 16;
+  int n = 0;
+  float v[kMax] = {};
+};
+int segments_max_frames();
+// scipy.signal.medfilt (zero padded, odd k <= 63) over each of `rows` tracks of T frames.
+void medfilt(const float* x, int rows, int T, int k, float* y, hipStream_t st);
+// Per (row, threshold): binarise, fill short silences, drop short speech, emit
+// [begin, end) runs.  seg_*: (rows * thr.n, cap); n_seg: (rows * thr.n).
+void run_segments(const float* med, int rows, int T, const ThresholdSet& thr, int lim_sil, int lim_sp, int cap,
+                  int* seg_begin, int* seg_end, int* n_seg, hipStream_t st);
 }  // namespace sd
 
 namespace sd {

@@ -1,0 +1,81 @@
+"""GPU postprocess (medfilt + run filters + segments, csrc/postprocess.hip) against
+the literal restatement of ts_vad2/infer.py:27-130 (oracle/postprocess_ref.py).
+Integer/index work: the RTTM lines must be identical, byte for byte."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import postprocess_ref
+from speaker_diarization_amd import der
+from speaker_diarization_amd.ts_vad import postprocess as pp
+
+pytestmark = pytest.mark.gpu
+
+
+def _tracks(rng, rows, T, kind):
+    if kind == "smooth":   # speech-like: slowly varying posteriors with short blips
+        x = np.cumsum(rng.normal(0, 0.08, (rows, T)), axis=1)
+        x = 1 / (1 + np.exp(-x)) + rng.normal(0, 0.05, (rows, T))
+    elif kind == "noise":
+        x = rng.uniform(0, 1, (rows, T))
+    elif kind == "exact":  # values sitting exactly on the float32 thresholds
+        x = rng.choice(np.asarray(postprocess_ref.THRESHOLDS + (0.0, 1.0), np.float32), (rows, T))
+    elif kind == "zeros":
+        x = np.zeros((rows, T))
+    else:
+        x = np.ones((rows, T))
+    return np.clip(x, 0, 1).astype(np.float32)
+
+
+def _compare(x, keys, **kw):
+    want = postprocess_ref.rttm_lines({k: x[i] for i, k in enumerate(keys)}, **kw)
+    got = pp.posteriors_to_rttm_gpu(keys, torch.from_numpy(x).cuda(), **kw)
+    assert list(got) == list(want)
+    for thr in want:
+        assert got[thr] == want[thr], (thr, len(got[thr]), len(want[thr]))
+    return got
+
+
+@pytest.mark.parametrize("kind", ["smooth", "noise", "exact", "zeros", "ones"])
+@pytest.mark.parametrize("T", [1, 7, 21, 33, 64, 100, 1000, 4097])
+def test_segments_match_reference_loop(gpu, kind, T):
+    rng = np.random.default_rng(T * 31 + len(kind))
+    x = _tracks(rng, 3, T, kind)
+    _compare(x, [f"R{T}_M1-{s}" for s in (1, 2, 3)])
+
+
+@pytest.mark.parametrize("min_silence,min_speech,med", [(0.32, 0.0, 21), (0.0, 0.0, 1), (0.5, 0.2, 11),
+                                                         (1.0, 0.6, 31)])
+def test_segments_options(gpu, min_silence, min_speech, med):
+    rng = np.random.default_rng(5)
+    x = _tracks(rng, 4, 3000, "smooth")
+    _compare(x, [f"m-{s}" for s in range(4)], min_silence=min_silence, min_speech=min_speech, med_filter=med)
+
+
+def test_meeting_scale_and_der(gpu):
+    """A 10-min meeting with 4 speakers (15000 frames at 25 Hz): identical RTTMs,
+    hence identical DER against a reference RTTM."""
+    rng = np.random.default_rng(11)
+    x = _tracks(rng, 4, 15000, "smooth")
+    keys = [f"R8001_M8004-{s}" for s in range(1, 5)]
+    got = _compare(x, keys)
+    ref_lines = got[0.8]
+    for thr in (0.3, 0.5):
+        a = der.md_eval(ref_lines, got[thr], collar=0.25)
+        b = der.md_eval(ref_lines, postprocess_ref.rttm_lines(dict(zip(keys, x)), thresholds=(thr,))[thr],
+                        collar=0.25)
+        assert a.line() == b.line()
+
+
+def test_long_track(gpu):
+    rng = np.random.default_rng(3)
+    x = _tracks(rng, 1, 200_003, "smooth")
+    beg, end, cnt = pp.segments_gpu(torch.from_numpy(x).cuda(), thresholds=(0.5,))
+    lt = postprocess_ref.change_ones_to_zeros(
+        postprocess_ref.change_zeros_to_ones(
+            __import__("scipy").signal.medfilt(x[0], 21), 0.32, 0.5, 0.04), 0.0, 0.5, 0.04)
+    a = np.asarray(lt, np.int8)
+    d = np.diff(np.concatenate([[0], a, [0]]))
+    assert cnt[0, 0] == (d == 1).sum()
+    assert np.array_equal(beg[0, 0, :cnt[0, 0]], np.flatnonzero(d == 1))
+    assert np.array_equal(end[0, 0, :cnt[0, 0]], np.flatnonzero(d == -1))

@@ -93,3 +93,15 @@ def test_rttm_segments_format():
     assert lines[0] == "SPEAKER m1 1 0.000 0.080 <NA> <NA> 2 <NA> <NA>\n"
     # reference convention: after a silence the start is taken at the frame before (infer.py:114)
     assert lines[1] == "SPEAKER m1 1 0.120 0.120 <NA> <NA> 2 <NA> <NA>\n"
+
+
+def test_host_postprocess_matches_reference_loop():
+    """posteriors_to_rttm (host path) == the literal infer.py loop, line for line."""
+    from oracle import postprocess_ref
+    rng = np.random.default_rng(4)
+    for T in (1, 30, 2000):
+        x = np.clip(1 / (1 + np.exp(-np.cumsum(rng.normal(0, 0.1, (3, T)), 1))), 0, 1).astype(np.float32)
+        x[0, ::7] = np.float32(0.35)   # exactly on a float32 threshold
+        post = {f"m{T}-{s}": x[s] for s in range(3)}
+        for kw in ({}, dict(min_speech=0.2, med_filter=5)):
+            assert pp.posteriors_to_rttm(post, **kw) == postprocess_ref.rttm_lines(post, **kw)
