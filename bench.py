@@ -165,7 +165,8 @@ def main():
             roofline = dict(bound="mfma", achieved=round(ach, 2), peak=PEAKS[dt], unit="TFLOP/s",
                             frac=round(ach / PEAKS[dt], 4), traffic=None, kernel=dom,
                             launches=st["launches"], avg_launch_ms=round(avg_ms, 4),
-                            flops_per_launch=st["flops"] / st["launches"])
+                            flops_per_launch=st["flops"] / st["launches"],
+                            algorithmic_bytes_per_launch=round(st["bytes"] / st["launches"]))
         else:
             ach = st["bytes"] / (st["ms"] * 1e-3) / 1e9
             roofline = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK, unit="GB/s",
