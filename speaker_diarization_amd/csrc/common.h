@@ -54,6 +54,17 @@ __device__ __forceinline__ uint16_t f2bf_bits(float f) {
   return (uint16_t)(u >> 16);
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// Two fp32 -> packed bf16 pair with v_cvt_pk_bf16_f32 (round-to-nearest-even, the
+// same bits as f2bf_bits for finite inputs; NaN stays NaN).
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 __device__ __forceinline__ float bf_bits2f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }

@@ -36,30 +36,6 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Wait until at most n VMEM ops are outstanding (n clamped to the 6-bit field).
-__device__ __forceinline__ void wait_vm_le(int n) {
-  if (n >= 63) wait_vm<63>();
-  else if (n >= 48) wait_vm<48>();
-  else if (n >= 40) wait_vm<40>();
-  else if (n >= 38) wait_vm<38>();
-  else if (n >= 36) wait_vm<36>();
-  else if (n >= 34) wait_vm<34>();
-  else if (n >= 32) wait_vm<32>();
-  else if (n >= 20) wait_vm<20>();
-  else if (n >= 18) wait_vm<18>();
-  else if (n >= 16) wait_vm<16>();
-  else if (n >= 12) wait_vm<12>();
-  else if (n >= 8) wait_vm<8>();
-  else if (n >= 6) wait_vm<6>();
-  else if (n >= 4) wait_vm<4>();
-  else if (n >= 2) wait_vm<2>();
-  else wait_vm<0>();
-}
-
-__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
-  return (uint32_t)f2bf_bits(a) | ((uint32_t)f2bf_bits(b) << 16);
-}
-
 template <int BN, int ACT>
 __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArgs p, int n_groups) {
   constexpr int WN = 2, WM = 4;                  // 8 waves: 4 along M x 2 along N
@@ -107,62 +83,62 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
                                                0, 0, 0);
     }
   }
-  // ---- A ring: step s = (tile s / KT, chunk s % KT); each wave fills 2 x 8 rows
-  auto issue = [&](int s) {
-    const int j = s / KT, kc = s - j * KT;
-    const int m0 = (grp + j * n_groups) * SBM;
-    uint16_t* dst = As + (size_t)(s % NST) * A_STAGE;
+  // ---- A ring.  Prefetch cursor: tile pj, chunk pkc, ring slot pslot.  a_off holds the
+  // per-lane byte offsets of this wave's two 8-row groups in the cursor's tile; the
+  // chunk advances through the scalar soffset, so a stage costs no VALU.
+  uint32_t a_off[2];
+  auto set_tile = [&](int jj) {
+    const int m0 = (grp + jj * n_groups) * SBM;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int rg = wid * 2 + i;
-      const int r = rg * 8 + lrow;
+      const int r = (wid * 2 + i) * 8 + lrow;
       const int m = m0 + r;
       const int src = lch ^ (r & 7);
-      const uint32_t off =
-          m < M ? (uint32_t)(((int64_t)m * p.lda + p.a_coff + kc * SBK + src * 8) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(dst + rg * 8 * SBK), 16, off, 0, 0, 0);
+      a_off[i] = m < M ? (uint32_t)(((int64_t)m * p.lda + p.a_coff + src * 8) * 2) : kOOB;
     }
   };
-
-  // Per-lane epilogue constants: columns n0 + wn*TN + nt*16 + l15.
-  float al[NT], be[NT];
+  int pj = 0, pkc = 0, pslot = 0;
+  set_tile(0);
+  auto issue_next = [&]() {
+    uint16_t* dst = As + (size_t)pslot * A_STAGE;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int n = n0 + wn * TN + nt * 16 + l15;
-    al[nt] = (p.alpha && n < p.N) ? p.alpha[n] : 1.f;
-    be[nt] = (p.beta && n < p.N) ? p.beta[n] : 0.f;
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(dst + (wid * 2 + i) * 8 * SBK), 16, a_off[i],
+                                               pkc * SBK * 2, 0, 0);
+    if (++pkc == KT) {
+      pkc = 0;
+      set_tile(++pj);
+    }
+    pslot = pslot == NST - 1 ? 0 : pslot + 1;
+  };
+
+  // The MFMA computes the transposed tile (W fragment as the A operand): lane l holds
+  // rows m = .. + (l & 15) and 4 CONSECUTIVE columns n = .. + 4*(l >> 4) + r, so the
+  // epilogue writes 8 B (bf16) / 16 B (f32) per lane and store instead of 4 scattered
+  // 2-B stores.  Per-lane epilogue constants for those columns:
+  float al[NT][4], be[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wn * TN + nt * 16 + lk * 4 + r;
+      al[nt][r] = (p.alpha && n < p.N) ? p.alpha[n] : 1.f;
+      be[nt][r] = (p.beta && n < p.N) ? p.beta[n] : 0.f;
+    }
+
+  // VMEM accounting (vmcnt counts loads, stores and LDS-DMA together, in issue order;
+  // every op is issued unconditionally — masked elements use an out-of-range offset —
+  // so counts are exact).  At the end of step s, "stage s+1 landed" is vmcnt <= the
+  // ops issued after it: 2 per later stage already issued, plus the epilogue stores
+  // of a tile that ended within the SD_ steps since stage s+1 was issued (KT >= SD_,
+  // so at most one).
+  int pro = 0;
+  for (; pro < SD_ && pro < total; ++pro) issue_next();
+  if (total > 0) {   // weight panel + stage 0 landed
+    if (pro == 3) wait_vm<4>();
+    else if (pro == 2) wait_vm<2>();
+    else wait_vm<0>();
   }
-
-  // Exact VMEM accounting (vmcnt counts loads, stores and LDS-DMA together, in issue
-  // order): `issued` = VMEM ops this wave has issued; pos[slot] = its value right after
-  // the stage in that ring slot was issued, so "stage t landed" is
-  // vmcnt(issued - pos[t % NST]).  Every op below is issued unconditionally (buffer
-  // ops with an out-of-range offset for masked elements) so the count is exact.
-  int issued = ((BN / 8) * KT - wid + 7) / 8;   // weight-panel DMAs of this wave
-  int pos[NST];
-#pragma unroll
-  for (int i = 0; i < NST; ++i) pos[i] = 0;
-  auto set_pos = [&](int slot, int v) {
-#pragma unroll
-    for (int i = 0; i < NST; ++i)
-      if (i == slot) pos[i] = v;
-  };
-  auto get_pos = [&](int slot) {
-    int v = 0;
-#pragma unroll
-    for (int i = 0; i < NST; ++i)
-      if (i == slot) v = pos[i];
-    return v;
-  };
-  auto issue_stage = [&](int t) {
-    issue(t);
-    issued += 2;
-    set_pos(t % NST, issued);
-  };
-
-  const int pro = total < SD_ ? total : SD_;
-  for (int t = 0; t < pro; ++t) issue_stage(t);
-  if (total > 0) wait_vm_le(issued - get_pos(0));   // weight panel + stage 0 landed
   asm volatile("s_barrier" ::: "memory");
 
   floatx4 acc[MT][NT];
@@ -174,13 +150,14 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
   const bool out_bf = p.out_bf16;
   const int64_t out_bytes = (int64_t)M * p.o_sw * (out_bf ? 2 : 4);
   const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, (int)out_bytes, 0x00020000);
-  for (int s = 0; s < total; ++s) {
-    const int j = s / KT, kc = s - j * KT;
+  int slot = 0;
+  for (int j = 0, s = 0; j < my_tiles; ++j) {
     const int m0 = (grp + j * n_groups) * SBM;
-    const int mb = m0 + wm * TM + lk * 4;            // epilogue element (mb + mt*16 + r, nb + nt*16)
-    const int nb = n0 + wn * TN + l15;
-    if (s + SD_ < total) issue_stage(s + SD_);
-    const uint16_t* Ast = As + (size_t)(s % NST) * A_STAGE;
+    const int mb = m0 + wm * TM + l15;               // epilogue rows mb + mt*16
+    const int nb = n0 + wn * TN + lk * 4;            // epilogue columns nb + nt*16 + r
+  for (int kc = 0; kc < KT; ++kc, ++s) {
+    if (s + SD_ < total) issue_next();
+    const uint16_t* Ast = As + (size_t)slot * A_STAGE;
     const uint16_t* Wst = Ws + (size_t)kc * BN * SBK;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -199,77 +176,82 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nt], af[mt], acc[mt][nt], 0, 0, 0);
     }
     if (kc == KT - 1 && ACT == kGluEpi) {
-      // ---- GLU epilogue: lane holds value (nt even) and gate (nt + 1) of channel
-      // ((n0 + wn*TN + nt*16) / 32) * 16 + l15; bf16 output N/2 wide.
+      // ---- GLU epilogue: value tile nt (even) and gate tile nt + 1 hold the same
+      // 4 channels ((n0 + wn*TN + nt*16) / 32) * 16 + 4*lk + r; bf16 output N/2 wide.
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; nt += 2)
+        for (int nt = 0; nt < NT; nt += 2) {
+          float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float a = fmaf(acc[mt][nt][r], al[nt], be[nt]);
-            const float gt = fmaf(acc[mt][nt + 1][r], al[nt + 1], be[nt + 1]);
-            const int m = mb + mt * 16 + r;
-            const int ch = ((n0 + wn * TN + nt * 16) >> 5) * 16 + l15;
-            const uint32_t off = (m < M && 2 * ch < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + ch) * 2) : kOOB;
-            __builtin_amdgcn_raw_buffer_store_b16(f2bf_bits(a / (1.f + __expf(-gt))), ro, off, 0, 0);
+            const float a = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
+            const float gt = fmaf(acc[mt][nt + 1][r], al[nt + 1][r], be[nt + 1][r]);
+            o[r] = a / (1.f + __expf(-gt));
           }
+          const int m = mb + mt * 16;
+          const int ch = ((n0 + wn * TN + nt * 16) >> 5) * 16 + lk * 4;
+          const uint32_t off = (m < M && 2 * ch < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + ch) * 2) : kOOB;
+          const u32x2_t v = {pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+        }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-      issued += MT * NT * 2;
     } else if (kc == KT - 1) {
       // ---- epilogue of tile j straight from the accumulators
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int nt = 0; nt < NT; ++nt) {
+          float x[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = fmaf(acc[mt][nt][r], al[nt], be[nt]);
-            if constexpr (ACT == kActRelu) x = fmaxf(x, 0.f);
-            if constexpr (ACT == kActSigmoid) x = 1.f / (1.f + __expf(-x));
-            if constexpr (ACT == kActSilu) x = x / (1.f + __expf(-x));
-            acc[mt][nt][r] = x;
+            x[r] = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
+            if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
+            if constexpr (ACT == kActSigmoid) x[r] = 1.f / (1.f + __expf(-x[r]));
+            if constexpr (ACT == kActSilu) x[r] = x[r] / (1.f + __expf(-x[r]));
           }
-      if (out_bf) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int m = mb + mt * 16 + r, n = nb + nt * 16;
-              const uint32_t off = (m < M && n < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + n) * 2) : kOOB;
-              __builtin_amdgcn_raw_buffer_store_b16(f2bf_bits(acc[mt][nt][r]), ro, off, 0, 0);
-            }
-      } else {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int m = mb + mt * 16 + r, n = nb + nt * 16;
-              const uint32_t off = (m < M && n < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + n) * 4) : kOOB;
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][nt][r]), ro, off, 0, 0);
-            }
-      }
+          const int m = mb + mt * 16, n = nb + nt * 16;
+          const bool ok = m < M && n < p.N;
+          if (out_bf) {
+            const uint32_t off = ok ? (uint32_t)(((int64_t)m * p.o_sw + n) * 2) : kOOB;
+            const u32x2_t v = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+            __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+          } else {
+            const uint32_t off = ok ? (uint32_t)(((int64_t)m * p.o_sw + n) * 4) : kOOB;
+            const u32x4_t v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]),
+                               __float_as_uint(x[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 0);
+          }
+        }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-      issued += MT * NT * 4;
     }
     if (s + 1 < total) {
-      wait_vm_le(issued - get_pos((s + 1) % NST));   // stage s+1 landed
+      const int later = (s + SD_ < total - 1 ? s + SD_ : total - 1) - (s + 1);   // stages issued after s+1
+      const bool st = kc == KT - 1 || (j > 0 && kc < SD_ - 1);
+      constexpr int ST = ACT == kGluEpi ? MT * NT / 2 : MT * NT;
+      if (st) {
+        if (later == 2) wait_vm<4 + ST>();
+        else if (later == 1) wait_vm<2 + ST>();
+        else wait_vm<ST>();
+      } else {
+        if (later == 2) wait_vm<4>();
+        else if (later == 1) wait_vm<2>();
+        else wait_vm<0>();
+      }
       // plain s_barrier: __syncthreads()' workgroup fence would add vmcnt(0) and drain the ring
       asm volatile("s_barrier" ::: "memory");
     }
+    slot = slot == NST - 1 ? 0 : slot + 1;
+  }
   }
 }
 
@@ -308,6 +290,8 @@ bool gemm_stream_supported(const ConvGemmArgs& p) {
   const bool row_major = p.o_sn == 1 && ((p.B == 1 && p.Ho == 1) ||
                                          (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh));
   return p.a_bf16 && !p.pre_scale && !p.gate && !p.res && p.kh * p.kw == 1 && p.K % SBK == 0 && p.lda % 8 == 0 &&
+         p.N % 4 == 0 && p.o_sw % 4 == 0 &&   // 4-column vector stores
+         p.K >= SD_ * SBK &&                  // KT >= SD_ (store accounting)
          p.a_coff % 8 == 0 && row_major && stream_bn(p) > 0 && M >= 16 * SBM &&
          (int64_t)M * p.lda * 2 < (int64_t)kOOB && (int64_t)p.N * p.K * 2 < (int64_t)kOOB &&
          (int64_t)M * p.o_sw * 4 < (int64_t)kOOB && (!p.res || (int64_t)M * p.res_ld * 4 < (int64_t)kOOB);
