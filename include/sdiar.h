@@ -215,6 +215,13 @@ int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, 
 /* nn.Linear: out (M, N) = act(x (M, K) · w (N, K)ᵀ + b). act: 0 none 1 relu 2 sigmoid 3 silu */
 int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, int N, int act,
                  float* out, int precision, void* stream);
+/* bf16 GEMM as the encoders run it: x bf16 bits (M rows, stride lda, columns
+ * [a_coff, a_coff + K)); optional per-input-channel BN-ReLU prologue
+ * x' = relu(x * pre_scale + pre_shift) (CAM++ nonlinear1, model.py dense layers);
+ * out bf16 bits (M, ldo) = act(alpha * (x' · wᵀ) + beta). */
+int sd_op_gemm_bf16(const void* x, int M, int K, int lda, int a_coff, const float* w, int N,
+                    const float* pre_scale, const float* pre_shift, const float* alpha, const float* beta,
+                    int act, void* out, int ldo, void* stream);
 /* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);
@@ -226,6 +233,10 @@ int sd_op_attention(const float* qkv, int S, int T, int D, int nh, int causal, i
                     const int* key_len, float* out, int precision, void* stream);
 int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
                     float* y, void* stream);
+/* Residual add + LayerNorm of the encoder blocks: s = x + t (t fp32, or bf16 bits when
+ * t_bf16); x <- s when write_x; y = LN(s) (bf16 bits when y_bf16). */
+int sd_op_add_layernorm(float* x, const void* t, int t_bf16, int rows, int D, const float* g, const float* b,
+                        float eps, int write_x, void* y, int y_bf16, void* stream);
 /* LSTM recurrence on precomputed gx (B, T, ndir*4H) (biases included); whh (ndir, 4H, H). */
 int sd_op_lstm(const float* gx, int B, int T, int H, int ndir, const float* whh, const int* lengths,
                float* out, float* hT, float* cT, float* work, void* stream);

@@ -112,7 +112,11 @@ _SIGS = {
                                    c_void_p, c_void_p]),
     "sd_postprocess_segments": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                         c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sd_op_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,
+                                    c_void_p, c_int, c_void_p]),
     "sd_op_linear": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "sd_op_gemm_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_conv1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_conv2d": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,

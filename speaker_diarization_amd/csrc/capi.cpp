@@ -348,6 +348,28 @@ int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, i
   });
 }
 
+int sd_op_gemm_bf16(const void* x, int M, int K, int lda, int a_coff, const float* w, int N,
+                    const float* pre_scale, const float* pre_shift, const float* alpha, const float* beta,
+                    int act, void* out, int ldo, void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    SD_CHECK(M > 0 && K > 0 && N > 0 && lda >= a_coff + K && ldo >= N, sd::kErrInvalid, "gemm_bf16: bad shape");
+    SD_CHECK((pre_scale == nullptr) == (pre_shift == nullptr), sd::kErrInvalid, "gemm_bf16: pre_scale/pre_shift");
+    Scratch wt((size_t)N * K * 2, st);
+    sd::pack_weight(w, N, K, 1, wt.p, true, st);
+    sd::ConvGemmArgs p = sd::linear_args(x, M, K, lda, wt.p, N, out, ldo);
+    p.a_bf16 = true;
+    p.a_coff = a_coff;
+    p.out_bf16 = true;
+    p.pre_scale = pre_scale;
+    p.pre_shift = pre_shift;
+    p.alpha = alpha;
+    p.beta = beta;
+    p.act = act;
+    sd::conv_gemm(p, true, st);
+  });
+}
+
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision,
                  void* stream) {
@@ -414,6 +436,13 @@ int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, 
 int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
                     float* y, void* stream) {
   return guard([&] { sd::layernorm(x, rows, D, D, g, b, eps, y, D, false, S(stream)); });
+}
+
+int sd_op_add_layernorm(float* x, const void* t, int t_bf16, int rows, int D, const float* g, const float* b,
+                        float eps, int write_x, void* y, int y_bf16, void* stream) {
+  return guard([&] {
+    sd::add_layernorm(x, t, t_bf16 != 0, rows, D, g, b, eps, write_x != 0, y, y_bf16 != 0, S(stream));
+  });
 }
 
 int sd_op_lstm(const float* gx, int B, int T, int H, int ndir, const float* whh, const int* lengths,

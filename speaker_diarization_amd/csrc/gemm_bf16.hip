@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(ConvGemmArgs p) {
         Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + l15] = acc[mt][nt][r];
   __syncthreads();
 
-  const bool lin = (p.B == 1 && p.Ho == 1) || (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh);
+  const bool lin = out_rows_linear(p);
   const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
   constexpr int CPR = BN / 4;
   for (int q = tid; q < BM * CPR; q += 256) {
@@ -300,6 +300,10 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st) {
   }
   if (gemm_stream_supported(p)) {   // weight-resident streaming path (gemm_stream.hip)
     conv_gemm_stream(p, st);
+    return;
+  }
+  if (gemm_ring_supported(p)) {     // 3-stage ring, BN-ReLU prologue (gemm_ring.hip)
+    conv_gemm_ring(p, st);
     return;
   }
   if (gemm_dma_supported(p)) {   // LDS-DMA fast path (gemm_dma.hip)

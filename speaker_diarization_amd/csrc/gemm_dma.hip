@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
         Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + l15] = acc[mt][nt][r];
   __syncthreads();
 
-  const bool lin = (p.B == 1 && p.Ho == 1) || (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh);
+  const bool lin = out_rows_linear(p);
   const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
   constexpr int CPR = BN / 4;
   if (vec && !p.gate && (!p.res || (!p.res_bf16 && (p.res_ld & 3) == 0))) {

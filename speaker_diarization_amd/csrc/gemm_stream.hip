@@ -287,8 +287,7 @@ bool gemm_stream_supported(const ConvGemmArgs& p) {
   static const bool disabled = getenv("SDIAR_NO_STREAM_GEMM") != nullptr;
   if (disabled) return false;
   const int M = p.B * p.Ho * p.Wo;
-  const bool row_major = p.o_sn == 1 && ((p.B == 1 && p.Ho == 1) ||
-                                         (p.o_sh == (int64_t)p.Wo * p.o_sw && p.o_sb == (int64_t)p.Ho * p.o_sh));
+  const bool row_major = p.o_sn == 1 && out_rows_linear(p) && a_rows_linear(p);
   return p.a_bf16 && !p.pre_scale && !p.gate && !p.res && p.kh * p.kw == 1 && p.K % SBK == 0 && p.lda % 8 == 0 &&
          p.N % 4 == 0 && p.o_sw % 4 == 0 &&   // 4-column vector stores
          p.K >= SD_ * SBK &&                  // KT >= SD_ (store accounting)

@@ -43,11 +43,23 @@ inline int glu_interleave_row(int r, int C) {   // new row index of original row
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
 void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
+bool gemm_ring_supported(const ConvGemmArgs& p);             // bf16 A/out, taps==1, K<=1024, N>=96, tall M
+void conv_gemm_ring(const ConvGemmArgs& p, hipStream_t st);
 bool gemm_stream_supported(const ConvGemmArgs& p);            // bf16 A linear, K%64==0, K<=768, no res
 void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
 bool fcm_conv_supported(const ConvGemmArgs& p);               // bf16 3x3 32->32, pad 1, freq stride 1|2
 void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
+
+// Output row (b, ho, wo) sits at linear row m = (b*Ho + ho)*Wo + wo, stride o_sw
+// (strides of size-1 dimensions do not matter).
+__host__ __device__ inline bool out_rows_linear(const ConvGemmArgs& p) {
+  return (p.Ho == 1 || p.o_sh == (int64_t)p.Wo * p.o_sw) && (p.B == 1 || p.o_sb == (int64_t)p.Ho * p.Wo * p.o_sw);
+}
+// A 1x1 conv whose input row m is output row m (stride 1, no padding): a plain GEMM on A.
+inline bool a_rows_linear(const ConvGemmArgs& p) {
+  return p.kh * p.kw == 1 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 && p.H == p.Ho && p.W == p.Wo;
+}
 
 // Plain row-major linear layer helper: out[m*ldo + o_coff + n] = act(A[m*lda+k]·W[n][k] * alpha + beta (+res)).
 ConvGemmArgs linear_args(const void* A, int M, int K, int lda, const void* Wt, int N,

@@ -236,6 +236,96 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
+// Vector LayerNorm for D % 128 == 0 (D = 128 * NV <= 1024): half a wave per row, each
+// lane owns NV float4 column groups (16-B loads/stores, 8-B bf16 t/y), so a row is
+// moved in full 512-B wave instructions with no idle lanes (the one-wave-per-row
+// kernel above leaves 1/4 of its lanes idle at D = 384 and issues 4-B accesses).
+// Same math: sum -> mean, centred sum of squares -> rstd; the reductions stay inside
+// each 32-lane half (xor masks < 32).
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NV, bool YBF, int TM>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restrict__ x, int rows, int D, int ldx,
+                                                            const void* __restrict__ t, float* __restrict__ xo,
+                                                            const float* __restrict__ g,
+                                                            const float* __restrict__ bb, float eps,
+                                                            act_t<YBF>* __restrict__ y, int ldy) {
+  const int hl = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= rows) return;   // whole 32-lane halves leave together
+  const float* xr = x + (int64_t)row * ldx;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (hl + i * 32) * 4;
+    float4 a = *reinterpret_cast<const float4*>(xr + c);
+    if constexpr (TM == 1) {
+      const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(t) + (int64_t)row * D + c);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if constexpr (TM == 2) {
+      const uint2 b = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(t) + (int64_t)row * D + c);
+      a.x += __uint_as_float(b.x << 16); a.y += __uint_as_float(b.x & 0xffff0000u);
+      a.z += __uint_as_float(b.y << 16); a.w += __uint_as_float(b.y & 0xffff0000u);
+    }
+    v[i] = a;
+    s += (a.x + a.y) + (a.z + a.w);
+  }
+  const float mean = half_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+    q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  }
+  const float rstd = rsqrtf(half_sum(q) / (float)D + eps);
+  if (xo) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      *reinterpret_cast<float4*>(xo + (int64_t)row * ldx + (hl + i * 32) * 4) = v[i];
+  }
+  act_t<YBF>* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (hl + i * 32) * 4;
+    const float4 gg = *reinterpret_cast<const float4*>(g + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(bb + c);
+    const float o0 = (v[i].x - mean) * rstd * gg.x + b4.x, o1 = (v[i].y - mean) * rstd * gg.y + b4.y;
+    const float o2 = (v[i].z - mean) * rstd * gg.z + b4.z, o3 = (v[i].w - mean) * rstd * gg.w + b4.w;
+    if constexpr (YBF)
+      *reinterpret_cast<uint2*>(yr + c) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
+    else
+      *reinterpret_cast<float4*>(yr + c) = make_float4(o0, o1, o2, o3);
+  }
+}
+
+template <int NV, int TM>
+static void lnv_launch2(const float* x, int rows, int D, int ldx, const void* t, float* xo, const float* g,
+                        const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
+  dim3 grid(cdiv(rows, 8));
+  if (ybf)
+    hipLaunchKernelGGL((layernorm_vec_kernel<NV, true, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
+                       eps, reinterpret_cast<uint16_t*>(y), ldy);
+  else
+    hipLaunchKernelGGL((layernorm_vec_kernel<NV, false, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
+                       eps, reinterpret_cast<float*>(y), ldy);
+}
+
+template <int NV>
+static void lnv_launch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
+                       const float* g, const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
+  if (tm == 0) lnv_launch2<NV, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+  else if (tm == 1) lnv_launch2<NV, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+  else lnv_launch2<NV, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+}
+
+static bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 template <int PER, int TM>
 static void ln_launch2(const float* x, int rows, int D, int ldx, const void* t, float* xo, const float* g,
                        const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
@@ -258,7 +348,21 @@ static void ln_launch(const float* x, int rows, int D, int ldx, const void* t, i
 
 static void ln_dispatch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
                         const float* g, const float* b, float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
-  if (D <= 256) ln_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
+  const bool vec = D % 128 == 0 && D <= 1024 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(xo) &&
+                   aligned16(g) && aligned16(b) && (reinterpret_cast<uintptr_t>(y) & (y_bf16 ? 7 : 15)) == 0 &&
+                   (reinterpret_cast<uintptr_t>(t) & (tm == 2 ? 7 : 15)) == 0;
+  if (vec) {
+    switch (D / 128) {
+      case 1: lnv_launch<1>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 2: lnv_launch<2>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 3: lnv_launch<3>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 4: lnv_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 5: lnv_launch<5>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 6: lnv_launch<6>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 7: lnv_launch<7>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      default: lnv_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+    }
+  } else if (D <= 256) ln_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
   else if (D <= 512) ln_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
   else if (D <= 1024) ln_launch<16>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
   else SD_CHECK(false, kErrInvalid, "layernorm: D > 1024 unsupported");

@@ -188,6 +188,67 @@ def test_layernorm(gpu, rows, D):
     torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
 
 
+def _bf16_round(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+# (M, N, K, lda, a_coff, pre, act): ring path (tall, K <= 1024, N >= 96, bf16 out), its K
+# tail / partial-N / multi-n-tile cases, the stream path (no prologue), the DMA path
+# (K > 1024 or short M).  act 1 = relu (CAM++ nonlinear2).
+GEMM_BF16_CASES = [(5000, 128, 640, 1024, 32, True, 1), (4096, 128, 256, 256, 0, True, 1),
+                   (3000, 512, 1024, 1024, 0, True, 0), (2100, 132, 360, 400, 8, True, 1),
+                   (5000, 384, 512, 512, 0, False, 0), (3000, 128, 1536, 1536, 0, True, 1),
+                   (700, 128, 256, 512, 64, True, 1)]
+
+
+@pytest.mark.parametrize("M,N,K,lda,a_coff,pre,act", GEMM_BF16_CASES)
+def test_gemm_bf16(gpu, M, N, K, lda, a_coff, pre, act):
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _bf16_round(torch.randn(M, lda, generator=g))
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    s = torch.rand(K, generator=g) + 0.5
+    h = torch.randn(K, generator=g) * 0.3
+    al = torch.rand(N, generator=g) + 0.5
+    be = torch.randn(N, generator=g) * 0.1
+    a = x[:, a_coff:a_coff + K]
+    if pre:
+        a = _bf16_round(torch.relu(a * s + h))
+    ref = (a @ _bf16_round(w).t()) * al + be
+    if act == 1:
+        ref = torch.relu(ref)
+    xd = x.to(torch.bfloat16).view(torch.int16).to(gpu)
+    out = torch.zeros(M, N, dtype=torch.int16, device=gpu)
+    _lib.call("sd_op_gemm_bf16", xd.data_ptr(), M, K, lda, a_coff, _d(w, gpu), N,
+              _d(s, gpu) if pre else None, _d(h, gpu) if pre else None, _d(al, gpu), _d(be, gpu), act,
+              out.data_ptr(), N, _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    got = out.cpu().view(torch.bfloat16).float()
+    torch.testing.assert_close(got, _bf16_round(ref), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("rows,D", [(1000, 384), (9, 256), (65, 1000), (333, 512)])
+@pytest.mark.parametrize("t_bf16,y_bf16", [(False, False), (True, True), (True, False)])
+def test_add_layernorm(gpu, rows, D, t_bf16, y_bf16):
+    g = torch.Generator().manual_seed(rows + D)
+    x = torch.randn(rows, D, generator=g) * 3 + 1
+    t = torch.randn(rows, D, generator=g)
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    t_in = _bf16_round(t) if t_bf16 else t
+    s = x + t_in
+    ref = F.layer_norm(s, (D,), w, b, 1e-5)
+    xd = x.to(gpu)
+    td = (t.to(torch.bfloat16).view(torch.int16) if t_bf16 else t).to(gpu)
+    y = torch.empty(rows, D, device=gpu, dtype=torch.int16 if y_bf16 else torch.float32)
+    _lib.call("sd_op_add_layernorm", xd.data_ptr(), td.data_ptr(), int(t_bf16), rows, D, _d(w, gpu), _d(b, gpu),
+              1e-5, 1, y.data_ptr(), int(y_bf16), _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(xd.cpu(), s, atol=1e-6, rtol=1e-6)
+    got = y.cpu().view(torch.bfloat16).float() if y_bf16 else y.cpu()
+    torch.testing.assert_close(got, _bf16_round(ref) if y_bf16 else ref, **(dict(atol=2e-2, rtol=1e-2) if y_bf16
+                                                                           else FP32_TOL))
+
+
 @pytest.mark.parametrize("B,T,H,ndir,lengths", [(64, 150, 256, 2, None), (1, 300, 256, 1, None),
                                                 (5, 40, 256, 2, [40, 17, 1, 33, 40])])
 def test_lstm(gpu, B, T, H, ndir, lengths):
