@@ -164,7 +164,204 @@ __global__ __launch_bounds__(256) void fcm_conv3x3_kernel(ConvGemmArgs p, int n_
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Row-band variant (the production path when the whole time axis fits in LDS).
+//
+// The tile above (one output row x 128 frames) reads every input row three times
+// (once per kernel row) and pads W = 598 frames to 640.  Here a persistent
+// 512-thread workgroup owns bands of R output rows x one time tile (the fewest tiles
+// of <= 19 16-frame blocks covering W: 2 x 304 for W = 598): the
+// NR = (R-1)*sh + 3 input rows of a band (+1 halo frame each side) are staged in LDS
+// once (input read (R+2)/R times instead of 3), the next band's rows are loaded into
+// registers (16-B buffer loads, zeros out of range) while the current band computes,
+// and the MFMA runs transposed (weights as the A operand) so each lane ends with 4
+// consecutive channels of one frame: 8-B bf16 stores / residual loads straight from
+// the accumulators, no LDS epilogue.
+constexpr int kBandThreads = 512;
+constexpr int kBandVecPer = 15;     // 16-B vectors per thread per band (NR * (W+2) * 4 <= 7680)
+constexpr uint32_t kFcmOOB = 0x80000000u;
+
+// Output channel held by accumulator row i of MFMA tile nt.  Rows are permuted so that
+// lane group q (rows 4q..4q+3 of both tiles) owns the 8 contiguous channels 8q..8q+7:
+// one 16-B bf16 store per lane writes a whole 64-B frame row with its 3 neighbours.
+__host__ __device__ inline int band_channel(int i, int nt) { return 8 * (i >> 2) + 4 * nt + (i & 3); }
+
+template <int R, int SH>
+__global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, int n_bands, int n_blk) {
+  // A band: (image b, R output rows from ho0, time tile tt of n_blk 16-frame blocks).
+  constexpr int NR = (R - 1) * SH + 3;
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [NR][TW+2][kPS]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int W = p.W, Wp = n_blk * 16 + 2;
+  const int n_rb = (p.Ho + R - 1) / R;
+  const int n_tt = (W + n_blk * 16 - 1) / (n_blk * 16);
+  const int n_vec = NR * Wp * 4;
+
+  bf16x8 wf[9][2];
+  {
+    const uint16_t* Wt = reinterpret_cast<const uint16_t*>(p.Wt);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        wf[t][nt] = *reinterpret_cast<const bf16x8*>(Wt + band_channel(l15, nt) * 288 + t * 32 + q * 8);
+  }
+  // Per lane: accumulator (nt, r) is channel 8q + 4nt + r, i.e. channels 8q .. 8q+7.
+  float al[2][4], be[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = band_channel(4 * q + r, nt);
+      al[nt][r] = p.alpha ? p.alpha[c] : 1.f;
+      be[nt][r] = p.beta ? p.beta[c] : 0.f;
+    }
+  const bool nhwc = p.o_sn == 1 && p.o_sw == 32 && p.o_sh == (int64_t)p.Wo * 32;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), (short)0,
+                                                                      (int)kFcmOOB, 0x00020000);
+
+  // Vector i = tid + k*512 of a band: staged pixel i >> 2 (row rr, frame px), channel
+  // group i & 3.  (i >> 2) advances by 128 per k and Wp > 128, so px wraps at most once.
+  const int px_base = (tid >> 2) % Wp, rr_base = (tid >> 2) / Wp;
+  auto load_band = [&](int band, uint4* v) {
+    const int tt = band % n_tt, bh = band / n_tt;
+    const int b = bh / n_rb, hb = (bh % n_rb) * R * SH - 1;   // first staged input row
+    const int w0 = tt * n_blk * 16 - 1;                      // first staged input frame
+    const int64_t img = (int64_t)b * p.H * W;
+    int px = px_base, rr = rr_base;
+#pragma unroll
+    for (int k = 0; k < kBandVecPer; ++k) {
+      const int i = tid + k * kBandThreads;
+      const int ch = (i & 3) * 8;
+      const int hi = hb + rr, wi = w0 + px;
+      const bool ok = i < n_vec && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)W;
+      const uint32_t off = ok ? (uint32_t)(((img + (int64_t)hi * W + wi) * p.lda + p.a_coff + ch) * 2) : kFcmOOB;
+      const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
+      v[k] = make_uint4(x.x, x.y, x.z, x.w);
+      px += 128;
+      if (px >= Wp) {
+        px -= Wp;
+        ++rr;
+      }
+    }
+  };
+
+  uint4 hv[kBandVecPer];
+  int band = blockIdx.x;
+  if (band < n_bands) load_band(band, hv);
+  for (; band < n_bands; band += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < kBandVecPer; ++k) {
+      const int i = tid + k * kBandThreads;
+      if (i < n_vec) *reinterpret_cast<uint4*>(xs + (i >> 2) * kPS + (i & 3) * 8) = hv[k];
+    }
+    __syncthreads();
+    const int next = band + gridDim.x;
+    if (next < n_bands) load_band(next, hv);   // in flight while this band computes
+
+    const int tt = band % n_tt, bh = band / n_tt;
+    const int b = bh / n_rb, ho0 = (bh % n_rb) * R;
+    const int wo0 = tt * n_blk * 16;
+    // Work items: (output row r, 16-frame block) round-robin over the 8 waves.
+    for (int it = wv; it < R * n_blk; it += kBandThreads / 64) {
+      const int r = it / n_blk, blk = it - r * n_blk;
+      const int ho = ho0 + r;
+      if (ho >= p.Ho) break;
+      floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          const int px = blk * 16 + l15 + dw;   // staged frame of output frame blk*16 + l15
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + ((r * SH + dh) * Wp + px) * kPS + q * 8);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[dh * 3 + dw][nt], af, acc[nt], 0, 0, 0);
+        }
+      const int wo = wo0 + blk * 16 + l15;
+      if (wo >= p.Wo) continue;
+      const int64_t pix = ((int64_t)b * p.Ho + ho) * p.Wo + wo;
+      const int c0 = q * 8;
+      float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (p.res) {
+        const int64_t ro = pix * p.res_ld + c0;
+        if (p.res_bf16) {
+          const uint4 r4 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(p.res) + ro);
+          const uint32_t rw[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rv[2 * u] = __uint_as_float(rw[u] << 16);
+            rv[2 * u + 1] = __uint_as_float(rw[u] & 0xffff0000u);
+          }
+        } else {
+          const float4 a4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.res) + ro);
+          const float4 b4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.res) + ro + 4);
+          rv[0] = a4.x; rv[1] = a4.y; rv[2] = a4.z; rv[3] = a4.w;
+          rv[4] = b4.x; rv[5] = b4.y; rv[6] = b4.z; rv[7] = b4.w;
+        }
+      }
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = apply_act(fmaf(acc[u >> 2][u & 3], al[u >> 2][u & 3], be[u >> 2][u & 3]) + rv[u], p.act);
+      if (nhwc && p.out_bf16) {
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.out) + pix * 32 + c0) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+      } else {
+        const int64_t ob = (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t o = ob + (int64_t)(c0 + u) * p.o_sn;
+          if (p.out_bf16) reinterpret_cast<uint16_t*>(p.out)[o] = f2bf_bits(v[u]);
+          else reinterpret_cast<float*>(p.out)[o] = v[u];
+        }
+      }
+    }
+    __syncthreads();   // xs free for the next band
+  }
+}
+
+// Time tiling: the fewest tiles whose 16-frame blocks (at most kBandMaxBlk, so a
+// staged row stays <= 306 frames) cover W, blocks spread evenly over them.
+constexpr int kBandMaxBlk = 19;
+inline int band_blocks(int W) {
+  const int nb = (W + 15) / 16;
+  const int n_tt = (nb + kBandMaxBlk - 1) / kBandMaxBlk;
+  return (nb + n_tt - 1) / n_tt;
+}
+
+template <int R, int SH>
+size_t band_lds(int n_blk) { return (size_t)((R - 1) * SH + 3) * (n_blk * 16 + 2) * kPS * 2; }
+
+template <int R, int SH>
+bool band_fits(const ConvGemmArgs& p) {
+  const int nr = (R - 1) * SH + 3;
+  const int nb = band_blocks(p.W);
+  // (n_blk*16 + 2) > 128 keeps the loader's frame index wrapping at most once per step.
+  return nb >= 8 && band_lds<R, SH>(nb) <= 156 * 1024 && nr * (nb * 16 + 2) * 4 <= kBandVecPer * kBandThreads &&
+         (int64_t)p.B * p.H * p.W * p.lda * 2 < (int64_t)kFcmOOB &&
+         (!p.res || (p.res_ld % 8 == 0)) && (p.o_sn != 1 || p.o_sw % 8 == 0);
+}
+
 int g_fcm_cu = 0;
+
+template <int R, int SH>
+void launch_band(const ConvGemmArgs& p, hipStream_t st) {
+  const int nb = band_blocks(p.W);
+  const int64_t bands = (int64_t)p.B * cdiv(p.Ho, R) * cdiv(p.W, nb * 16);
+  SD_CHECK(bands < (1ll << 31), kErrInvalid, "fcm conv: too many bands");
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, SH>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
+  const size_t smem = band_lds<R, SH>(nb);
+  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, SH>), dim3(grid), dim3(kBandThreads), smem, st, p, (int)bands, nb);
+}
 
 }  // namespace
 
@@ -180,6 +377,17 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
     int dev = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&g_fcm_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  static const bool no_band = getenv("SDIAR_NO_FCM_BAND") != nullptr;
+  if (!no_band && p.sh == 1 && band_fits<4, 1>(p)) {
+    launch_band<4, 1>(p, st);
+    SD_LAUNCH_CHECK();
+    return;
+  }
+  if (!no_band && p.sh == 2 && band_fits<2, 2>(p)) {
+    launch_band<2, 2>(p, st);
+    SD_LAUNCH_CHECK();
+    return;
   }
   const int n_wt = cdiv(p.Wo, kPx);
   const int64_t tiles = (int64_t)p.B * p.Ho * n_wt;

@@ -94,7 +94,8 @@ def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
 
 @pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("B,H,W,sh,kh,pad", [(2, 80, 50, 2, 3, 1), (1, 40, 37, 1, 3, 1), (2, 40, 21, 2, 1, 0),
-                                             (2, 20, 33, 2, 3, 1), (1, 40, 300, 1, 3, 1), (3, 9, 257, 2, 3, 1)])
+                                             (2, 20, 33, 2, 3, 1), (1, 40, 300, 1, 3, 1), (3, 9, 257, 2, 3, 1),
+                                             (2, 10, 598, 1, 3, 1), (2, 11, 600, 2, 3, 1)])
 def test_conv2d(gpu, precision, B, H, W, sh, kh, pad):
     g = torch.Generator().manual_seed(H * W)
     x = torch.randn(B, 32, H, W, generator=g)
