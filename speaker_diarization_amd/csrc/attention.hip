@@ -241,156 +241,178 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 }
 
 // Short sequences (T <= 256, bf16 compute and storage): one workgroup per (sequence,
-// head) stages the WHOLE K and Vᵀ of that head in LDS once with 16-B loads and its 4
-// waves walk the 16-query tiles — no K/V re-reads per query block, no 64-query
-// padding waste (conformer T = 150; FS-EEND slot attention T = 6).  Same S-transposed
-// MFMA formulation and online softmax as attn_kernel above.
-template <int HD>
-__global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP) {
+// group of heads).  For each head it stages the head's whole K (zero-padded to a
+// multiple of 32 in d) and V — both row-major, straight 16-B copies — in LDS, and
+// its 4 waves walk the 16-query tiles.  Both products run "transposed" so every
+// softmax statistic and output row is lane-local:
+//   S^T = K Q^T   (mfma(K frag, Q frag)): lane (g, l15) holds keys 4g+r of query l15;
+//   O^T = V^T P^T (mfma(V frag, P frag)): lane holds d = 16dt + 4g + r of query l15,
+//                 so the output leaves as 8-B bf16 stores;
+// the V^T operand comes from the row-major V image through ds_read_b64_tr_b16 (gfx950
+// transpose read), so staging needs no scattered 2-B LDS writes.  One workgroup per
+// sequence (all heads) when there are enough sequences: each QKV row is then fetched
+// by one CU instead of by nh workgroups spread over the XCDs.  LDS row strides
+// (K: HDP+16, V: HD or HD+16 elements) are bank-conflict free for the ds_read_b128
+// fragment reads and the transpose reads.
+template <int HD, bool XREMAP>
+__global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int hpw) {
   constexpr int HDP = ((HD + 31) / 32) * 32;
-  constexpr int KS = HDP + 8;         // K row stride (bf16)
+  constexpr int KS = HDP + 16;
+  constexpr int VS = HD == 48 ? HD : HD + 16;
   constexpr int QN = HDP / 32;
   constexpr int DT = HD / 16;
+  typedef short v4s __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Kb = smem;                 // [TP][KS]
-  uint16_t* Vt = smem + TP * KS;       // [HDP][TP + 8]
-  const int VS = TP + 8;
+  uint16_t* Vb = smem + TP * KS;       // [TP][VS]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, l15 = lane & 15;
-  const int s = blockIdx.x / a.nh, h = blockIdx.x % a.nh;
+  const int n_hg = (a.nh + hpw - 1) / hpw;
+  const int lid = XREMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int s = lid / n_hg, h_beg = (lid % n_hg) * hpw;
+  const int h_end = min(h_beg + hpw, a.nh);
   const int T = a.T, D = a.D;
   const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
                        (int64_t)(s % a.seq_inner) * a.seq_inner_stride;
   const int64_t tstr = (int64_t)a.tok_stride * a.ld_qkv;
-  const uint16_t* base = reinterpret_cast<const uint16_t*>(a.qkv) + row0 * a.ld_qkv + h * HD;
   const int klen = a.key_len ? min(a.key_len[s], T) : T;
-
-  // ---- stage K (rows) and Vᵀ for all keys; zero padding beyond T and HD
-  constexpr int CH = HDP / 8;          // 16-B chunks per padded row
-  for (int i = tid; i < TP * CH; i += 256) {
-    const int key = i / CH, c8 = (i % CH) * 8;
-    uint4 kv = make_uint4(0u, 0u, 0u, 0u), vv = kv;
-    if (key < T && c8 < HD) {
-      const uint16_t* r = base + (int64_t)key * tstr + c8;
-      kv = *reinterpret_cast<const uint4*>(r + D);
-      vv = *reinterpret_cast<const uint4*>(r + 2 * D);
-    }
-    *reinterpret_cast<uint4*>(Kb + key * KS + c8) = kv;
-    const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      Vt[(c8 + 2 * u) * VS + key] = (uint16_t)(vw[u] & 0xffffu);
-      Vt[(c8 + 2 * u + 1) * VS + key] = (uint16_t)(vw[u] >> 16);
-    }
-  }
-  __syncthreads();
-
   const int n_qt = (T + 15) / 16;
-  for (int qt = wid; qt < n_qt; qt += 4) {
-    const int q0 = qt * 16;
-    const int myq = q0 + l15;
-    bf16x8 qf[QN];
-    {
+  // Transpose-read lane address inside a 4-row x 16-column block: row q = (l15 >> 2),
+  // columns 4 * (l15 & 3) .. +3; block origin (keys k0 + 4g [+16], columns 16 dt).
+  const int tr_off = ((4 * g + (l15 >> 2)) * VS + 4 * (l15 & 3)) * 2;
+
+  for (int h = h_beg; h < h_end; ++h) {
+    const uint16_t* base = reinterpret_cast<const uint16_t*>(a.qkv) + row0 * a.ld_qkv + h * HD;
+    if (h > h_beg) __syncthreads();   // previous head's LDS reads done
+    // Raw Q chunks of this wave's first query tile: in flight during the K/V staging.
+    auto load_q = [&](int qt, uint4* raw) {
+      const int myq = qt * 16 + l15;
       const uint16_t* qr = base + (int64_t)min(myq, T - 1) * tstr;
 #pragma unroll
       for (int kc = 0; kc < QN; ++kc) {
         const int d0 = kc * 32 + g * 8;
-        bf16x8 v;
-        if (myq < T && d0 < HD) {
-          const uint4 q4 = *reinterpret_cast<const uint4*>(qr + d0);
-          const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+        raw[kc] = (qt < n_qt && myq < T && d0 < HD) ? *reinterpret_cast<const uint4*>(qr + d0)
+                                                     : make_uint4(0u, 0u, 0u, 0u);
+      }
+    };
+    uint4 qraw[QN];
+    load_q(wid, qraw);
+    // K/V staging: up to 8 16-B loads per thread issued back to back, then stored.
+    constexpr int CK = HDP / 8, CV = HD / 8;
+    const int nk = TP * CK, nv = TP * CV;
+    for (int r0 = 0; r0 < nk + nv; r0 += 8 * 256) {
+      uint4 st[8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            v[2 * u] = __builtin_bit_cast(__bf16, f2bf_bits(__uint_as_float(qw[u] << 16) * a.scale));
-            v[2 * u + 1] = __builtin_bit_cast(__bf16, f2bf_bits(__uint_as_float(qw[u] & 0xffff0000u) * a.scale));
+      for (int u = 0; u < 8; ++u) {
+        const int i = r0 + u * 256 + tid;
+        st[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < nk) {
+          const int key = i / CK, c8 = (i % CK) * 8;
+          if (key < T && c8 < HD) st[u] = *reinterpret_cast<const uint4*>(base + (int64_t)key * tstr + D + c8);
+        } else if (i < nk + nv) {
+          const int key = (i - nk) / CV, c8 = ((i - nk) % CV) * 8;
+          if (key < T) st[u] = *reinterpret_cast<const uint4*>(base + (int64_t)key * tstr + 2 * D + c8);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = r0 + u * 256 + tid;
+        if (i < nk) {
+          const int key = i / CK, c8 = (i % CK) * 8;
+          *reinterpret_cast<uint4*>(Kb + key * KS + c8) = st[u];
+        } else if (i < nk + nv) {
+          const int key = (i - nk) / CV, c8 = ((i - nk) % CV) * 8;
+          *reinterpret_cast<uint4*>(Vb + key * VS + c8) = st[u];
+        }
+      }
+    }
+    __syncthreads();
+
+    for (int qt = wid; qt < n_qt; qt += 4) {
+      const int q0 = qt * 16;
+      const int myq = q0 + l15;
+      bf16x8 qf[QN];
+#pragma unroll
+      for (int kc = 0; kc < QN; ++kc) {
+        const uint32_t qw[4] = {qraw[kc].x, qraw[kc].y, qraw[kc].z, qraw[kc].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          qf[kc][2 * u] = (__bf16)(__uint_as_float(qw[u] << 16) * a.scale);
+          qf[kc][2 * u + 1] = (__bf16)(__uint_as_float(qw[u] & 0xffff0000u) * a.scale);
+        }
+      }
+      load_q(qt + 4, qraw);   // next tile's Q in flight during this tile
+      floatx4 o[DT];
+#pragma unroll
+      for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      float m_run = -INFINITY, l_run = 0.f;   // statistics of query myq
+      int k_end = klen;
+      if (a.causal) k_end = min(k_end, q0 + 16 + a.causal_delay);
+      for (int k0 = 0; k0 < k_end; k0 += 32) {
+        floatx4 sc[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < QN; ++kc) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Kb[(k0 + st * 16 + l15) * KS + kc * 32 + g * 8]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], acc, 0, 0, 0);
           }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = __builtin_bit_cast(__bf16, (uint16_t)0);
+          sc[st] = acc;
         }
-        qf[kc] = v;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + st * 16 + g * 4 + r;
+            const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
+            const float v = ok ? sc[st][r] : -INFINITY;
+            sc[st][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = (m_new == -INFINITY) ? 0.f : __expf(sc[st][r] - m_new);
+            sc[st][r] = pv;
+            psum += pv;
+          }
+        psum += __shfl_xor(psum, 16, 64);
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+        // P^T operand: k-index 8g + j <-> key k0 + 4g + j (j < 4), k0 + 16 + 4g + j - 4.
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sc[j >> 2][j & 3];
+        typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
+        const uint32_t vbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)Vb) +
+                               (uint32_t)(k0 * VS * 2) + (uint32_t)tr_off;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + 16 * VS * 2 + dt * 32));
+          const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
+        }
       }
-    }
-    floatx4 o[DT];
+      if (myq < T) {
+        const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (row0 + (int64_t)myq * a.tok_stride) * a.ldo + h * HD;
 #pragma unroll
-    for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY, l_run = 0.f;
-    int k_end = klen;
-    if (a.causal) k_end = min(k_end, q0 + 16 + a.causal_delay);
-    for (int k0 = 0; k0 < k_end; k0 += 32) {
-      floatx4 sc[2];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kc = 0; kc < QN; ++kc) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Kb[(k0 + st * 16 + l15) * KS + kc * 32 + g * 8]);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], acc, 0, 0, 0);
-        }
-        sc[st] = acc;
+        for (int dt = 0; dt < DT; ++dt)
+          *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) =
+              make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
       }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + st * 16 + g * 4 + r;
-          const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
-          const float v = ok ? sc[st][r] : -INFINITY;
-          sc[st][r] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
-      float psum = 0.f;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = (m_new == -INFINITY) ? 0.f : __expf(sc[st][r] - m_new);
-          sc[st][r] = pv;
-          psum += pv;
-        }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ar = __shfl(alpha, g * 4 + r, 64);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt][r] *= ar;
-      }
-      bf16x8 pa;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pa[j] = __builtin_bit_cast(__bf16, f2bf_bits(sc[j >> 2][j & 3]));
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const uint16_t* vr = &Vt[(dt * 16 + l15) * VS + k0];
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr + g * 4);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16 + g * 4);
-        bf16x8 vb;
-        const uint32_t w[4] = {lo.x, lo.y, hi.x, hi.y};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vb[2 * j] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] & 0xffff));
-          vb[2 * j + 1] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] >> 16));
-        }
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qi = g * 4 + r;
-      const float lr = __shfl(l_run, qi, 64);
-      const int q = q0 + qi;
-      if (q >= T) continue;
-      const float inv = lr > 0.f ? 1.f / lr : 0.f;
-      uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (row0 + (int64_t)q * a.tok_stride) * a.ldo + h * HD;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) orow[dt * 16 + l15] = f2bf_bits(o[dt][r] * inv);
     }
   }
 }
@@ -398,16 +420,36 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP) {
 template <int HD>
 bool launch_short(const AttnArgs& a, bool bf16, hipStream_t st) {
   constexpr int HDP = ((HD + 31) / 32) * 32;
-  if (!bf16 || !a.io_bf16 || a.T > 256 || (a.ld_qkv % 8) || (a.D % 8) || (HD % 8)) return false;
+  constexpr int KS = HDP + 16;
+  constexpr int VS = HD == 48 ? HD : HD + 16;
+  if (!bf16 || !a.io_bf16 || a.T > 256 || (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 4) || (HD % 16)) return false;
   const int TP = (a.T + 31) / 32 * 32;
-  const size_t smem = sizeof(uint16_t) * ((size_t)TP * (HDP + 8) + (size_t)HDP * (TP + 8));
+  const size_t smem = sizeof(uint16_t) * (size_t)TP * (KS + VS);
+  // One head per workgroup (measured best at S = 2400, T = 150: more, smaller workgroups
+  // overlap their staging); XCD-aware order keeps the heads of a sequence on one L2.
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  static const int env_hpw = getenv("SDIAR_ATTN_HPW") ? atoi(getenv("SDIAR_ATTN_HPW")) : 0;
+  static const bool env_xr = getenv("SDIAR_ATTN_NO_XREMAP") == nullptr;
+  int hpw = 1;
+  if (env_hpw > 0) hpw = std::min(env_hpw, a.nh);
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_short_kernel<HD>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_short_kernel<HD, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_short_kernel<HD, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(attn_short_kernel<HD>, dim3(a.S * a.nh), dim3(256), smem, st, a, TP);
+  const dim3 grid(a.S * ((a.nh + hpw - 1) / hpw));
+  if (env_xr)
+    hipLaunchKernelGGL((attn_short_kernel<HD, true>), grid, dim3(256), smem, st, a, TP, hpw);
+  else
+    hipLaunchKernelGGL((attn_short_kernel<HD, false>), grid, dim3(256), smem, st, a, TP, hpw);
   return true;
 }
 
