@@ -189,12 +189,240 @@ __global__ __launch_bounds__(256) void lstm_step_bf16_kernel(
   }
 }
 
+// Whole-sequence bf16 kernel (H = 256), one launch for all T steps.
+//
+// The recurrence couples hidden units only within a batch row.  A GROUP of 4
+// workgroups owns BB = 16*MT batch rows of one direction; workgroup q of the group
+// keeps the W_hh rows of its 64 hidden units (4 gates x 64 = 256 rows x 256, 128 KiB
+// bf16) resident in LDS for the whole sequence, so W is read from HBM/L2 once per
+// launch instead of once per step.  Each step the 4 workgroups exchange h through a
+// double-buffered bf16 array in global memory with the write-through hand-off of the
+// MI355X guide (every payload store sc1 -> every storing wave vmcnt(0) -> barrier ->
+// one agent-scope counter add; consumer: one lane polls the counter relaxed, barrier,
+// every payload load sc1).  The product is computed transposed (z^T = W h^T): a lane
+// holds 4 consecutive hidden units of one batch row for each gate, so the gate math is
+// lane-local and gx / out / h move as 16-B / 8-B vectors; c and fp32 h stay in
+// registers.  Co-residency: the launcher keeps 4 x groups <= CUs (one workgroup per CU
+// by LDS), and every poll is bounded so a broken invariant can never hang the GPU.
+constexpr int LS_H = 256;
+constexpr int LS_WS = LS_H + 16;     // bf16 LDS row stride of the W slice (conflict-free fragment reads)
+constexpr int LS_MAXMT = 6;
+
+template <int MT>
+__global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
+    const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
+    const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
+    float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
+    uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err) {
+  constexpr int H = LS_H, BB = 16 * MT;
+  extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int q = blockIdx.x & 3;                 // unit quarter
+  const int grp = blockIdx.x >> 2;
+  const int n_bb = (B + BB - 1) / BB;
+  const int d = grp / n_bb, b0 = (grp % n_bb) * BB;
+  const int G4 = ndir * 4 * H;
+  unsigned* cnt = counters + grp;
+  const int ub = 64 * q + 16 * w + 4 * g;       // first of this lane's 4 units
+
+  // W slice -> LDS: slice row (gate, j) = W_hh row gate*H + 64q + j.
+  {
+    const uint16_t* wd = whh + (int64_t)d * 4 * H * H;
+    for (int i = tid; i < 256 * (H / 8); i += 256) {
+      const int row = i / (H / 8), k8 = (i % (H / 8)) * 8;
+      const int gate = row >> 6, j = row & 63;
+      *reinterpret_cast<uint4*>(&wsl[row * LS_WS + k8]) =
+          *reinterpret_cast<const uint4*>(wd + (int64_t)(gate * H + 64 * q + j) * H + k8);
+    }
+  }
+  // h exchange: hx[parity][d][Bp][H] bf16; h_t lives in parity (t + 1) & 1, h_{-1} in 0.
+  const int64_t plane = (int64_t)ndir * Bp * H;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * 2), 0x00020000);
+  auto hx_off = [&](int parity, int b, int u) {   // byte offset
+    return (uint32_t)(((int64_t)parity * plane + ((int64_t)d * Bp + b) * H + u) * 2);
+  };
+  float c[MT][4], hr[MT][4];
+  int len[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int b = b0 + mt * 16 + l15;
+    len[mt] = b < B ? (lengths ? lengths[b] : T) : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t si = ((int64_t)d * B + b) * H + ub + r;
+      hr[mt][r] = (b < B && h0) ? h0[si] : 0.f;
+      c[mt][r] = (b < B && c0) ? c0[si] : 0.f;
+    }
+  }
+  int max_len = 0;
+  for (int b = b0; b < min(B, b0 + BB); ++b) max_len = max(max_len, lengths ? lengths[b] : T);
+
+  // Publish this workgroup's slice of h (rows b0.., units ub..ub+3 per lane), then count.
+  auto publish = [&](int parity) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
+      __builtin_amdgcn_raw_buffer_store_b64(v, rh, hx_off(parity, b0 + mt * 16 + l15, ub), 0, 16);   // sc1
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto wait_for = [&](unsigned target) {
+    if (tid == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        // A peer that never arrives (broken co-residency) must not hang the GPU: give up
+        // after ~0.1 s, and once any workgroup gave up, every later wait returns at once.
+        if ((++spins & 1023) == 0 && (spins > (1u << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the poll
+  };
+
+  publish(0);   // h_{-1}
+  for (int step = 0; step < max_len; ++step) {
+    // gx of this step for the lane's rows: 4 gates x 4 units (float4), issued before the wait.
+    float4 gxv[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int b = b0 + mt * 16 + l15;
+      const bool live = step < len[mt];
+      const int t = d == 0 ? step : len[mt] - 1 - step;
+      const float* gr = gx + ((int64_t)(live ? b : 0) * T + (live ? t : 0)) * G4 + d * 4 * H + ub;
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate)
+        gxv[mt][gate] = live ? *reinterpret_cast<const float4*>(gr + gate * H) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
+    const int pin = step & 1;
+    floatx4 acc[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < H; k0 += 32) {
+      bf16x8 hf[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rh, hx_off(pin, b0 + mt * 16 + l15, k0 + 8 * g), 0, 16);
+        hf[mt] = __builtin_bit_cast(bf16x8, x);
+      }
+#pragma unroll
+      for (int gate = 0; gate < 4; ++gate) {
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc[mt][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mt], acc[mt][gate], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int b = b0 + mt * 16 + l15;
+      if (step >= len[mt]) continue;
+      const int t = d == 0 ? step : len[mt] - 1 - step;
+      const float gi[4] = {gxv[mt][0].x, gxv[mt][0].y, gxv[mt][0].z, gxv[mt][0].w};
+      const float gf[4] = {gxv[mt][1].x, gxv[mt][1].y, gxv[mt][1].z, gxv[mt][1].w};
+      const float gg[4] = {gxv[mt][2].x, gxv[mt][2].y, gxv[mt][2].z, gxv[mt][2].w};
+      const float go[4] = {gxv[mt][3].x, gxv[mt][3].y, gxv[mt][3].z, gxv[mt][3].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ig = 1.f / (1.f + expf(-(acc[mt][0][r] + gi[r])));
+        const float fg = 1.f / (1.f + expf(-(acc[mt][1][r] + gf[r])));
+        const float cg = tanhf(acc[mt][2][r] + gg[r]);
+        const float og = 1.f / (1.f + expf(-(acc[mt][3][r] + go[r])));
+        c[mt][r] = fg * c[mt][r] + ig * cg;
+        hr[mt][r] = og * tanhf(c[mt][r]);
+      }
+      if (out)
+        *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) =
+            make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
+    }
+    publish((step + 1) & 1);   // h_step
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int b = b0 + mt * 16 + l15;
+    if (b >= B) continue;
+    const int64_t si = ((int64_t)d * B + b) * H + ub;
+    if (hT) *reinterpret_cast<float4*>(hT + si) = make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
+    if (cT) *reinterpret_cast<float4*>(cT + si) = make_float4(c[mt][0], c[mt][1], c[mt][2], c[mt][3]);
+  }
+}
+
+template <int MT>
+void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
+                       const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
+                       uint16_t* hx, int Bp, unsigned* counters, int* err, hipStream_t st) {
+  const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int groups = ndir * cdiv(B, 16 * MT);
+  hipLaunchKernelGGL(lstm_group_bf16_kernel<MT>, dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
+                     reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
+                     counters, err);
+}
+
 }  // namespace
 
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16) {
   SD_CHECK(H % 32 == 0, kErrInvalid, "lstm: H must be a multiple of 32");
+  static const bool no_seq = getenv("SDIAR_NO_LSTM_SEQ") != nullptr;
+  if (whh_bf16 && H == LS_H && !no_seq && (ldo % 4 == 0 || !out)) {
+    // Smallest row block (16 * MT) whose 4 x groups fit one workgroup per CU.
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      SD_HIP(hipGetDevice(&dev));
+      SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    int mt = 0;
+    for (int m = 1; m <= LS_MAXMT && !mt; ++m)
+      if (4 * ndir * cdiv(B, 16 * m) <= n_cu) mt = m;
+    if (mt) {
+      const int Bp = cdiv(B, 16 * mt) * 16 * mt;
+      const int groups = ndir * cdiv(B, 16 * mt);
+      // Exchange buffers + counters: one device scratch, grown on demand.
+      static void* scratch = nullptr;
+      static size_t scratch_bytes = 0;
+      const size_t hx_bytes = (size_t)2 * ndir * Bp * H * 2;
+      const size_t ctl_bytes = ((size_t)(groups + 1) * 4 + 15) / 16 * 16;
+      if (hx_bytes + ctl_bytes > scratch_bytes) {
+        if (scratch) SD_HIP(hipFree(scratch));
+        scratch_bytes = hx_bytes + ctl_bytes;
+        SD_HIP(hipMalloc(&scratch, scratch_bytes));
+      }
+      unsigned* ctl = reinterpret_cast<unsigned*>(static_cast<char*>(scratch) + hx_bytes);
+      SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
+      uint16_t* hx = static_cast<uint16_t*>(scratch);
+      ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
+                     4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
+      int* err = reinterpret_cast<int*>(ctl + groups);
+      switch (mt) {
+        case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        case 3: launch_lstm_group<3>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        case 4: launch_lstm_group<4>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        case 5: launch_lstm_group<5>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        default: launch_lstm_group<6>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+      }
+      SD_LAUNCH_CHECK();
+      return;
+    }
+  }
   const int64_t n = (int64_t)ndir * B * H;
   float* hA = work;
   float* hB = work + n;
