@@ -55,6 +55,8 @@ void EdaModel::finalize() {
     for (size_t i = 0; i < bias.size(); ++i) bias[i] = bi.data[i] + bh.data[i];
     *b = arena_.upload(bias);
     *hh = arena_.upload(wh.data);
+    // bf16 mode: a bf16 copy feeds the group-persistent recurrence kernel (lstm.hip).
+    if (cfg_.bf16) (hh == &enc_hh_ ? enc_hh_bf_ : dec_hh_bf_) = upload_packed(arena_, wh.data, 4 * E, E, 1, 1, true).w;
   };
   if (plain) {
     dec_ = ld.linear("decoder");
@@ -116,9 +118,11 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   // EDA: shuffle -> encoder LSTM (packed) -> decoder LSTM from (h, c)
   gather_rows(X_, S, T, E, perm, lengths, Y_, st);
   conv_gemm(lin(Tens{Y_, false}, rows, E, enc_ih_, enc_b_, Tens{G_, false}, 4 * E), bf, st);
-  lstm_recurrence(G_, S, T, E, 1, enc_hh_, lengths, nullptr, nullptr, nullptr, 0, hT_, cT_, lstm_work_, st);
+  lstm_recurrence(G_, S, T, E, 1, enc_hh_, lengths, nullptr, nullptr, nullptr, 0, hT_, cT_, lstm_work_, st,
+                  enc_hh_bf_);
   fill_rows(dec_b_, 4 * E, S * NA, Gd_, st);
-  lstm_recurrence(Gd_, S, NA, E, 1, dec_hh_, nullptr, hT_, cT_, att_, E, nullptr, nullptr, lstm_work_, st);
+  lstm_recurrence(Gd_, S, NA, E, 1, dec_hh_, nullptr, hT_, cT_, att_, E, nullptr, nullptr, lstm_work_, st,
+                  dec_hh_bf_);
   attractor_scores(X_, S, T, E, att_, NA, lin_w_, lin_b_, probs, act, st);
 }
 

@@ -54,6 +54,7 @@ class EdaModel {
   PackedW enc_ih_;
   const float *enc_b_ = nullptr, *enc_hh_ = nullptr;
   const float *dec_b_ = nullptr, *dec_hh_ = nullptr;
+  const void *enc_hh_bf_ = nullptr, *dec_hh_bf_ = nullptr;   // bf16 copies (bf16 mode)
   const float *lin_w_ = nullptr, *lin_b_ = nullptr;
   ConvL dec_;   // variant 3: decoder Linear -> sigmoid
 
