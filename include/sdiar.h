@@ -203,10 +203,12 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
  * seg_begin/seg_end: device int32 (rows * n_thresholds, cap), cap >= (T+1)/2;
  * n_seg: device int32 (rows * n_thresholds), row-major (row, threshold).
  * RTTM formatting stays on the host (speaker_diarization_amd/ts_vad/postprocess.py).
+ * flags bit 0: speech iff x > threshold (EEND bin/make_rttm.py:29, medfilt of the 0/1
+ * decisions == threshold of the medfilt'd posteriors) instead of >=.
  * T <= 524288 frames. */
 int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, const float* thresholds,
                             int n_thresholds, int min_silence_frames, int min_speech_frames, int cap,
-                            int* seg_begin, int* seg_end, int* n_seg, void* stream);
+                            int* seg_begin, int* seg_end, int* n_seg, int flags, void* stream);
 
 /* ------------------------------------------------------------------ ops (parity tests)
  * precision: 0 fp32, 1 bf16 MFMA (fp32 activations), 2 bf16 MFMA on bf16 activations

@@ -72,3 +72,20 @@ def rttm_lines(post, label_rate=25, med_filter=21, min_silence=0.32, min_speech=
                 out[threshold].append("SPEAKER " + str(name) + " 1 %.3f" % (start) + " %.3f " % (duration)
                                       + "<NA> <NA> " + str(speaker_id) + " <NA> <NA>\n")
     return out
+
+
+def eend_rttm_lines(session, t_hat, threshold=0.5, frame_shift=256, subsampling=1, median=1, sampling_rate=16000):
+    """speaker_diarization/bin/make_rttm.py:27-42 for one session's T_hat (T, n_spk)."""
+    lines = []
+    a = np.where(np.asarray(t_hat, dtype=np.float32) > threshold, 1, 0)
+    if median > 1:
+        a = signal.medfilt(a, (median, 1))
+    for spkid, frames in enumerate(a.T):
+        frames = np.pad(frames, (1, 1), "constant")
+        changes, = np.where(np.diff(frames, axis=0) != 0)
+        fmt = "SPEAKER {:s} 1 {:7.2f} {:7.2f} <NA> <NA> {:s} <NA> <NA>"
+        for s, e in zip(changes[::2], changes[1::2]):
+            lines.append(fmt.format(session, s * frame_shift * subsampling / sampling_rate,
+                                    (e - s) * frame_shift * subsampling / sampling_rate,
+                                    session + "_" + str(spkid)))
+    return lines

@@ -309,7 +309,7 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
 
 int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, const float* thresholds,
                             int n_thresholds, int min_silence_frames, int min_speech_frames, int cap,
-                            int* seg_begin, int* seg_end, int* n_seg, void* stream) {
+                            int* seg_begin, int* seg_end, int* n_seg, int flags, void* stream) {
   return guard([&] {
     SD_CHECK(rows >= 0 && T >= 0, sd::kErrInvalid, "postprocess: negative shape");
     SD_CHECK(n_thresholds >= 1 && n_thresholds <= sd::ThresholdSet::kMax, sd::kErrInvalid,
@@ -323,6 +323,7 @@ int sd_postprocess_segments(const float* post, int rows, int T, int med_filter, 
     hipStream_t st = S(stream);
     sd::ThresholdSet thr;
     thr.n = n_thresholds;
+    thr.strict = flags & 1;
     for (int i = 0; i < n_thresholds; ++i) thr.v[i] = thresholds[i];
     Scratch med((size_t)rows * T * sizeof(float), st);
     sd::medfilt(post, rows, T, med_filter, static_cast<float*>(med.p), st);

@@ -183,6 +183,7 @@ void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* 
 struct ThresholdSet {
   static constexpr int kMax = 16;
   int n = 0;
+  int strict = 0;   // 1: speech iff x > thr (EEND make_rttm.py), 0: x >= thr (TS-VAD infer.py)
   float v[kMax] = {};
 };
 int segments_max_frames();

@@ -150,7 +150,7 @@ run_segments_kernel(const float* __restrict__ med, int T, ThresholdSet thr, int 
   // Binarise: one coalesced 64-frame load + ballot per wave iteration.
   const int lane = threadIdx.x & 63;
   for (int f0 = (threadIdx.x >> 6) * 64; f0 < T; f0 += kSegThreads) {
-    const bool p = f0 + lane < T && m[f0 + lane] >= th;
+    const bool p = f0 + lane < T && (thr.strict ? m[f0 + lane] > th : m[f0 + lane] >= th);
     const uint64_t b = __ballot(p);
     if (lane == 0) {
       A[f0 >> 5] = (uint32_t)b;

@@ -92,10 +92,11 @@ def run_lengths_frames(min_len: float, frame_len: float) -> int:
 
 
 def segments_gpu(post, med_filter: int = 21, thresholds=THRESHOLDS, min_silence: float = 0.32,
-                 min_speech: float = 0.0, label_rate: int = 25):
+                 min_speech: float = 0.0, label_rate: int = 25, strict: bool = False):
     """Device half of posteriors_to_rttm: post (rows, T) CUDA float32 -> per
     (row, threshold) speech runs.  Returns host arrays (begin, end, count) shaped
-    (rows, n_thr, cap), (rows, n_thr, cap), (rows, n_thr)."""
+    (rows, n_thr, cap), (rows, n_thr, cap), (rows, n_thr).  strict: speech iff
+    x > threshold (EEND make_rttm) instead of x >= threshold (TS-VAD)."""
     import torch
     from .. import _lib
     post = post.contiguous().float()
@@ -109,7 +110,7 @@ def segments_gpu(post, med_filter: int = 21, thresholds=THRESHOLDS, min_silence:
     cnt = torch.empty(rows, len(thr), dtype=torch.int32, device=dev)
     _lib.call("sd_postprocess_segments", _lib.ptr(post), rows, T, med_filter, thr.ctypes.data, len(thr),
               run_lengths_frames(min_silence, frame_len), run_lengths_frames(min_speech, frame_len), cap,
-              _lib.ptr(beg), _lib.ptr(end), _lib.ptr(cnt), _lib.stream_ptr(dev))
+              _lib.ptr(beg), _lib.ptr(end), _lib.ptr(cnt), int(strict), _lib.stream_ptr(dev))
     return beg.cpu().numpy(), end.cpu().numpy(), cnt.cpu().numpy()
 
 

@@ -79,3 +79,17 @@ def test_long_track(gpu):
     assert cnt[0, 0] == (d == 1).sum()
     assert np.array_equal(beg[0, 0, :cnt[0, 0]], np.flatnonzero(d == 1))
     assert np.array_equal(end[0, 0, :cnt[0, 0]], np.flatnonzero(d == -1))
+
+
+@pytest.mark.parametrize("T,nspk,median,thr", [(1, 2, 1, 0.5), (500, 2, 1, 0.5), (2000, 3, 11, 0.5),
+                                              (777, 4, 25, 0.3), (64, 2, 5, 0.0)])
+def test_eend_make_rttm(gpu, T, nspk, median, thr):
+    from speaker_diarization_amd import make_rttm
+    rng = np.random.default_rng(T + nspk)
+    t_hat = _tracks(rng, nspk, T, "smooth").T.copy()          # (T, n_spk)
+    t_hat[::13, 0] = np.float32(thr)                          # exactly on the threshold: not speech (>)
+    want = postprocess_ref.eend_rttm_lines("rec1", t_hat, threshold=thr, frame_shift=80, subsampling=10,
+                                           median=median, sampling_rate=8000)
+    got = make_rttm.session_lines("rec1", torch.from_numpy(t_hat).cuda(), threshold=thr, frame_shift=80,
+                                  subsampling=10, median=median, sampling_rate=8000)
+    assert got == want
