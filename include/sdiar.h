@@ -160,6 +160,25 @@ int sd_fseend_test(sd_fseend* h, const float* feats, int ld_feats, int S, int T,
 int64_t sd_fseend_device_bytes(const sd_fseend* h);
 int sd_fseend_destroy(sd_fseend* h);
 
+/* Streaming test(): the same scores as sd_fseend_test on the concatenated frames, produced
+ * chunk by chunk from K/V histories (no reference counterpart: the reference recomputes the
+ * causal forward over the whole recording, fs_eend.py:79-96 / fs_eend/model.py:198; the
+ * causal masks of every shipped config, mask_delay 0, make the two identical).  A frame's
+ * score is final 9 frames later (look-ahead Conv1d, fs_eend.py:41).  chunk: frames per push
+ * (1..32; 1 frame = 100 ms at subsampling 10); use_graph: replay each chunk's kernels as a
+ * captured hipGraph.  The stream keeps a pointer to its model handle: destroy it first. */
+typedef struct sd_fseend_stream sd_fseend_stream;
+int sd_fseend_stream_create(sd_fseend* h, int chunk, int max_frames, int max_nspks, int use_graph,
+                            sd_fseend_stream** out);
+/* feats: device (n, ld_feats) f32, 1 <= n <= chunk (n < chunk ends the input);
+ * preds: device (cap, max_nspks) f32; *n_out = frames whose scores were written. */
+int sd_fseend_stream_push(sd_fseend_stream* s, const float* feats, int ld_feats, int n, float* preds, int cap,
+                          int* n_out, void* stream);
+int sd_fseend_stream_flush(sd_fseend_stream* s, float* preds, int cap, int* n_out, void* stream);
+int sd_fseend_stream_reset(sd_fseend_stream* s, void* stream);
+int64_t sd_fseend_stream_device_bytes(const sd_fseend_stream* s);
+int sd_fseend_stream_destroy(sd_fseend_stream* s);
+
 /* feature.stft + feature.transform('logmel23_mn' | 'logmel23') + feature.splice + [::subsampling]
  * (speaker_diarization/feature.py:155-184, 56-73, 130-152; eend_eda/infer_eda.py:94-98).
  * wav: device f32 (n_samples) (soundfile values, computed in float64 like the reference);

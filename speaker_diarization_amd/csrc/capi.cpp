@@ -12,6 +12,7 @@
 #include "prof.h"
 #include "eda.h"
 #include "fseend.h"
+#include "fseend_stream.h"
 #include "tsvad.h"
 
 namespace sd {
@@ -30,6 +31,10 @@ struct sd_eda {
 
 struct sd_fseend {
   std::unique_ptr<sd::FsEendModel> model;
+};
+
+struct sd_fseend_stream {
+  std::unique_ptr<sd::FsEendStream> s;
 };
 
 namespace {
@@ -259,6 +264,51 @@ int64_t sd_fseend_device_bytes(const sd_fseend* h) { return h ? (int64_t)h->mode
 
 int sd_fseend_destroy(sd_fseend* h) {
   return guard([&] { delete h; });
+}
+
+int sd_fseend_stream_create(sd_fseend* h, int chunk, int max_frames, int max_nspks, int use_graph,
+                            sd_fseend_stream** out) {
+  return guard([&] {
+    SD_CHECK(h && out, sd::kErrInvalid, "null argument");
+    auto* s = new sd_fseend_stream;
+    try {
+      s->s.reset(new sd::FsEendStream(*h->model, chunk, max_frames, max_nspks, use_graph != 0));
+    } catch (...) {
+      delete s;
+      throw;
+    }
+    *out = s;
+  });
+}
+
+int sd_fseend_stream_push(sd_fseend_stream* s, const float* feats, int ld_feats, int n, float* preds, int cap,
+                          int* n_out, void* stream) {
+  return guard([&] {
+    SD_CHECK(s && n_out, sd::kErrInvalid, "null argument");
+    *n_out = s->s->push(feats, ld_feats, n, preds, cap, S(stream));
+  });
+}
+
+int sd_fseend_stream_flush(sd_fseend_stream* s, float* preds, int cap, int* n_out, void* stream) {
+  return guard([&] {
+    SD_CHECK(s && n_out, sd::kErrInvalid, "null argument");
+    *n_out = s->s->flush(preds, cap, S(stream));
+  });
+}
+
+int sd_fseend_stream_reset(sd_fseend_stream* s, void* stream) {
+  return guard([&] {
+    SD_CHECK(s, sd::kErrInvalid, "null handle");
+    s->s->reset(S(stream));
+  });
+}
+
+int64_t sd_fseend_stream_device_bytes(const sd_fseend_stream* s) {
+  return s ? (int64_t)s->s->device_bytes() : 0;
+}
+
+int sd_fseend_stream_destroy(sd_fseend_stream* s) {
+  return guard([&] { delete s; });
 }
 
 int sd_eend_features(const float* wav, int64_t n_samples, int frame_size, int frame_shift, int n_frames,

@@ -28,6 +28,8 @@ struct FusionL {            // TransformerEncoderFusionLayer (fs_eend.py:282-333
   const float *n11g, *n11b, *n21g, *n21b, *n22g, *n22b;
 };
 
+class FsEendStream;
+
 class FsEendModel {
  public:
   explicit FsEendModel(const FsEendConfig& c) : cfg_(c) {}
@@ -43,6 +45,7 @@ class FsEendModel {
   size_t device_bytes() const { return arena_.total(); }
 
  private:
+  friend class FsEendStream;
   float* ws(size_t n) { return static_cast<float*>(arena_.alloc(n * sizeof(float))); }
   void run_fusion(float* A, int S, int T, int C, hipStream_t st);
 

@@ -1,0 +1,69 @@
+// Chunked (streaming) FS-EEND inference with per-layer K/V histories and hipGraph replay.
+//
+// Produces the same per-frame scores as OnlineTransformerDADiarization.test()
+// (fs_eend.py:79-96) on the concatenation of the pushed frames, chunk by chunk:
+//   encoder chunk  c new feature rows -> BN-folded Linear -> LN -> enc_n_layers causal
+//                  transformer layers, each attending to its K|V history (stream_ops.hip)
+//   decoder chunk  once 9 frames of look-ahead exist (Conv1d k 19 pad 9, fs_eend.py:41,85):
+//                  conv window -> L2 norm -> slot init -> the shared fusion layer
+//                  dec_n_layers times (time attention against each application's K|V
+//                  history over the (t, slot) grid, slot attention, FFN) -> scores
+// Requires has_mask = 1 and mask_delay = 0 (every shipped config; with a positive delay
+// frame t would depend on future frames at every layer).  Each chunk's kernel sequence
+// is captured once into a hipGraph (after a first direct run that performs the kernels'
+// one-time setup) and replayed: positions live in a device cursor block.
+#pragma once
+#include "fseend.h"
+
+namespace sd {
+
+class FsEendStream {
+ public:
+  FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, bool use_graph);
+  ~FsEendStream();
+  // feats: device (n, ld) f32, 1 <= n <= chunk.  A push of n < chunk frames ends the input.
+  // Writes the scores of every frame that became final to preds (device, rows of C, capacity
+  // cap rows) and returns their number.
+  int push(const float* feats, int ld, int n, float* preds, int cap, hipStream_t st);
+  // Ends the input (if not already) and emits the remaining frames.
+  int flush(float* preds, int cap, hipStream_t st);
+  void reset(hipStream_t st);
+  int frames_in() const { return n_valid_; }
+  int frames_out() const { return n_out_; }
+  int chunk() const { return c_; }
+  size_t device_bytes() const { return arena_.total(); }
+
+ private:
+  void enc_chunk(hipStream_t st);
+  void dec_chunk(hipStream_t st);
+  void fusion_step(int app, hipStream_t st);
+  void run(int which, hipStream_t st);   // 0 encoder, 1 decoder: graph replay or direct launches
+  int emit(float* preds, int cap, int rows, hipStream_t st);
+  template <typename T>
+  T* wsb(size_t elems) { return static_cast<T*>(arena_.alloc(elems * sizeof(T))); }
+
+  FsEendModel& m_;
+  const int c_, cap_, C_;
+  const bool use_graph_;
+  const bool bf_;
+  const size_t es_;
+  DeviceArena arena_;
+  int* state_ = nullptr;               // [0] encoder frames, [1] valid frames, [2] decoder frames
+  int n_enc_ = 0, n_valid_ = 0, n_dec_ = 0, n_out_ = 0;
+  bool closed_ = false;
+  int n_wtiles_ = 0;
+  // staging (chunk-sized)
+  float *F_ = nullptr, *Y_ = nullptr, *X_ = nullptr, *W_ = nullptr, *Yc_ = nullptr, *E_ = nullptr;
+  float *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;
+  void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
+  // histories
+  std::vector<void*> kv_enc_, kv_dec_;
+  float* hist_ = nullptr;
+  // graphs
+  hipStream_t cap_st_ = nullptr;
+  hipGraph_t graph_[2] = {nullptr, nullptr};
+  hipGraphExec_t exec_[2] = {nullptr, nullptr};
+  bool ran_direct_[2] = {false, false};
+};
+
+}  // namespace sd

@@ -223,3 +223,38 @@ void slot_init(const float* g, int T, int C, int D, const float* p, float* out, 
 void slot_scores(const float* emb, float* att, int T, int C, int D, float* scores, bool write_norm,
                  hipStream_t st);
 }  // namespace sd
+
+namespace sd {
+// ---------------------------------------------------------------- streaming (stream_ops.hip)
+// Chunked causal attention against a K/V history (see stream_ops.hip).  Element offsets:
+// query i of sequence s at q + i*q_tok + s*q_seq (+ head*64); key j at k/v + j*kv_tok + s*kv_seq;
+// output like the query.  Query i sits at absolute position *pos + i and sees keys
+// j <= *pos + i + delay; keys [0, *pos + nq) must be in the history.
+struct DecodeAttnArgs {
+  const void* q = nullptr;
+  int64_t q_tok = 0, q_seq = 0;
+  const void* k = nullptr;
+  const void* v = nullptr;
+  int64_t kv_tok = 0, kv_seq = 0;
+  void* out = nullptr;
+  int64_t o_tok = 0, o_seq = 0;
+  int nseq = 1, nq = 1, nh = 1, hd = 64;
+  float scale = 1.f;
+  const int* pos = nullptr;   // device cursor
+  int delay = 0;
+  int max_keys = 0;           // history capacity: grid coverage
+  int n_wtiles = 0;           // workspace tiles per (sequence, head) >= attn_decode_tiles(max_keys)
+  float* ws = nullptr;        // nseq*nh*n_wtiles*nq*(2+hd) floats
+  bool io_bf16 = false;
+};
+int attn_decode_tiles(int max_keys);
+void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
+// dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
+void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,
+               const int* cursor, int mult, hipStream_t st);
+// dst (rows, D) = hist rows [*cursor - pad, ...), zero outside [0, *n_valid).
+void gather_window(const float* hist, int D, const int* cursor, const int* n_valid, int pad, int rows, float* dst,
+                   hipStream_t st);
+// *cursor += by; mirror (optional) = new value.
+void cursor_advance(int* cursor, int by, int* mirror, hipStream_t st);
+}  // namespace sd

@@ -66,6 +66,9 @@ bool prof_query(int i, std::string& name, long long& launches, double& flops, do
 ProfScope::ProfScope(const char* name, double flops, double bytes, hipStream_t st)
     : name_(name), flops_(flops), bytes_(bytes), st_(st) {
   if (!g_on) return;
+  // Kernels captured into a hipGraph (FS-EEND streaming) are timed per replay by the caller.
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st_, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
   on_ = true;
   SD_HIP(hipEventCreate(&a_));
   SD_HIP(hipEventCreate(&b_));

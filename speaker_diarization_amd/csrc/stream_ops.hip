@@ -1,0 +1,238 @@
+// Streaming (KV-cache) kernels for the chunked FS-EEND forward on gfx950.
+//
+// The reference computes OnlineTransformerDADiarization.test() (fs_eend.py:79-96) over a
+// whole recording with causal masks (mask_delay 0 in every shipped config,
+// fs_eend/config/*.yaml).  Causality makes the forward incremental: frame t of every
+// encoder layer depends on frames <= t only, the look-ahead Conv1d (k 19, pad 9,
+// fs_eend.py:41,85) needs 9 frames of encoder output past t, and the decoder's time
+// attention (fs_eend.py:456-467) is causal again.  The streaming runner keeps, per
+// layer, the K|V rows of every frame already seen and runs each new chunk of `c` frames
+// against them.  Every position-dependent argument is read from a device-resident
+// cursor so a chunk's whole kernel sequence can be captured once into a hipGraph and
+// replayed (no host arguments change between chunks).
+//
+//   kv_append       copy `rows` rows (width bytes) of a staging buffer into a history
+//                   buffer at row cursor*mult (the K|V half of the in-projection, or the
+//                   encoder output)
+//   attn_decode     softmax(q·kᵀ·scale)·v for nq (≤ 32) queries at absolute positions
+//                   cursor + i against all cached keys j <= cursor + i + delay:
+//                   split-K over 64-key wave tiles (lane = key for q·k, lane = head dim
+//                   for p·v), per-wave (m, l, o) partials, one combine wave per query.
+//                   fp32 arithmetic; K/V/Q/O fp32 or bf16 (the dtype of the cache).
+//                   HBM-bound: each cached key row is read once per (sequence, head).
+//   gather_window   rows [cursor - pad, cursor + c + pad) of the encoder-output history,
+//                   zero outside [0, n_valid) (the conv's zero padding and the
+//                   emb[:ilen] re-pad of fs_eend.py:83-84)
+//   cursor_advance  cursor[i] += c (+ optional mirror), the graph's last node
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kMaxQ = 32;
+constexpr int kHD = 64;
+
+// 16-B row copy; rows of `width16` uint4 units.
+__global__ __launch_bounds__(256) void kv_append_kernel(const uint4* __restrict__ src, int64_t ld_src16, int rows,
+                                                        int width16, uint4* __restrict__ dst, int64_t ld_dst16,
+                                                        const int* __restrict__ cursor, int mult) {
+  const int64_t r0 = (int64_t)(*cursor) * mult;
+  const int64_t n = (int64_t)rows * width16;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / width16;
+    const int c = (int)(i - r * width16);
+    dst[(r0 + r) * ld_dst16 + c] = src[r * ld_src16 + c];
+  }
+}
+
+template <bool IOBF>
+__device__ __forceinline__ void load_row64(const act_t<IOBF>* p, float* v) {
+  if constexpr (IOBF) {
+#pragma unroll
+    for (int j = 0; j < kHD; j += 8) {
+      const uint4 u = *reinterpret_cast<const uint4*>(p + j);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[j + 2 * e] = __uint_as_float(w[e] << 16);
+        v[j + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kHD; j += 4) {
+      const float4 u = *reinterpret_cast<const float4*>(p + j);
+      v[j] = u.x; v[j + 1] = u.y; v[j + 2] = u.z; v[j + 3] = u.w;
+    }
+  }
+}
+
+// grid (n_tiles256, nseq*nh), 256 threads: wave w of block b owns keys [(4b + w)*64, +64).
+template <bool IOBF>
+__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
+  using io_t = act_t<IOBF>;
+  __shared__ float qs[kMaxQ][kHD];
+  __shared__ float ps[4][kMaxQ][64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int sh = blockIdx.y, s = sh / a.nh, h = sh % a.nh;
+  const int pos = *a.pos;
+  const int total = pos + a.nq;                         // keys present after this chunk's append
+  const int wtile = blockIdx.x * 4 + wid;               // 64-key tile index
+  const int kbeg = blockIdx.x * 256;
+  if (kbeg >= total) return;                            // uniform over the block
+  const io_t* qb = reinterpret_cast<const io_t*>(a.q) + (int64_t)s * a.q_seq + h * kHD;
+  for (int i = tid; i < a.nq * kHD; i += 256) {
+    const int qi = i / kHD, d = i % kHD;
+    qs[qi][d] = ld_act(qb, (int64_t)qi * a.q_tok + d) * a.scale;
+  }
+  __syncthreads();
+  const int k0 = wtile * 64;
+  if (k0 >= total) return;                              // whole wave past the end (wave-uniform)
+  const int j = k0 + lane;
+  const bool kv = j < total;
+  float kr[kHD];
+  {
+    const io_t* kp = reinterpret_cast<const io_t*>(a.k) + (int64_t)min(j, total - 1) * a.kv_tok +
+                     (int64_t)s * a.kv_seq + h * kHD;
+    load_row64<IOBF>(kp, kr);
+  }
+  float* part = a.ws + ((int64_t)sh * a.n_wtiles + wtile) * a.nq * (2 + kHD);
+  for (int qi = 0; qi < a.nq; ++qi) {
+    float sc = 0.f;
+#pragma unroll
+    for (int d = 0; d < kHD; ++d) sc = fmaf(qs[qi][d], kr[d], sc);
+    const bool vis = kv && j <= pos + qi + a.delay;
+    sc = vis ? sc : -INFINITY;
+    const float m = warp_max(sc);
+    const float p = (m == -INFINITY || !vis) ? 0.f : __expf(sc - m);
+    const float l = warp_sum(p);
+    ps[wid][qi][lane] = p;   // read back by the same wave only (LDS ops of a wave stay in order)
+    if (lane == 0) {
+      part[qi * (2 + kHD)] = m;
+      part[qi * (2 + kHD) + 1] = l;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // p·v: lane = head dim, loop over the wave's 64 keys (V rows read coalesced).
+  float acc[kMaxQ];
+#pragma unroll
+  for (int qi = 0; qi < kMaxQ; ++qi) acc[qi] = 0.f;
+  const io_t* vb = reinterpret_cast<const io_t*>(a.v) + (int64_t)s * a.kv_seq + h * kHD + lane;
+  const int nk = min(64, total - k0);
+  for (int kk = 0; kk < nk; ++kk) {
+    const float vv = ld_act(vb, (int64_t)(k0 + kk) * a.kv_tok);
+#pragma unroll
+    for (int qi = 0; qi < kMaxQ; ++qi)
+      if (qi < a.nq) acc[qi] = fmaf(ps[wid][qi][kk], vv, acc[qi]);
+  }
+#pragma unroll
+  for (int qi = 0; qi < kMaxQ; ++qi)
+    if (qi < a.nq) part[qi * (2 + kHD) + 2 + lane] = acc[qi];
+}
+
+// grid (nseq*nh), block 64*nq: wave qi combines the partials of query qi.
+template <bool IOBF>
+__global__ __launch_bounds__(256) void attn_combine_kernel(DecodeAttnArgs a) {
+  using io_t = act_t<IOBF>;
+  const int sh = blockIdx.x, s = sh / a.nh, h = sh % a.nh;
+  const int qi = blockIdx.y * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (qi >= a.nq) return;
+  const int pos = *a.pos;
+  const int total = pos + a.nq;
+  const int nt = cdiv(total, 64);
+  const float* part = a.ws + (int64_t)sh * a.n_wtiles * a.nq * (2 + kHD) + qi * (2 + kHD);
+  const int64_t tstride = (int64_t)a.nq * (2 + kHD);
+  float M = -INFINITY;
+  for (int t = 0; t < nt; ++t) M = fmaxf(M, part[t * tstride]);
+  float L = 0.f, o = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    const float m = part[t * tstride];
+    if (m == -INFINITY) continue;
+    const float w = __expf(m - M);
+    L = fmaf(w, part[t * tstride + 1], L);
+    o = fmaf(w, part[t * tstride + 2 + lane], o);
+  }
+  io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
+  st_act(ob, lane, o / L);
+}
+
+__global__ __launch_bounds__(256) void gather_window_kernel(const float* __restrict__ hist, int D,
+                                                            const int* __restrict__ cursor,
+                                                            const int* __restrict__ n_valid, int pad, int rows,
+                                                            float* __restrict__ dst) {
+  const int base = *cursor - pad, nv = *n_valid;
+  const int64_t n = (int64_t)rows * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / D), d = (int)(i - (int64_t)r * D);
+    const int src = base + r;
+    dst[i] = (src >= 0 && src < nv) ? hist[(int64_t)src * D + d] : 0.f;
+  }
+}
+
+__global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
+  if (threadIdx.x == 0) {
+    const int v = *cursor + by;
+    *cursor = v;
+    if (mirror) *mirror = v;
+  }
+}
+
+}  // namespace
+
+void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,
+               const int* cursor, int mult, hipStream_t st) {
+  SD_CHECK(width_bytes % 16 == 0 && ld_src_bytes % 16 == 0 && ld_dst_bytes % 16 == 0, kErrInvalid,
+           "kv_append: rows must be 16-byte multiples");
+  SD_CHECK(((uintptr_t)src | (uintptr_t)dst) % 16 == 0, kErrInvalid, "kv_append: unaligned buffers");
+  if (rows <= 0) return;
+  const int w16 = width_bytes / 16;
+  const int64_t n = (int64_t)rows * w16;
+  ProfScope prof("kv_append", 0.0, 2.0 * rows * width_bytes, st);
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(kv_append_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const uint4*>(src),
+                     ld_src_bytes / 16, rows, w16, static_cast<uint4*>(dst), ld_dst_bytes / 16, cursor, mult);
+  SD_LAUNCH_CHECK();
+}
+
+int attn_decode_tiles(int max_keys) { return cdiv(max_keys, 256) * 4; }
+
+void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
+  SD_CHECK(a.hd == kHD, kErrInvalid, "attn_decode: head dim must be 64");
+  SD_CHECK(a.nq >= 1 && a.nq <= kMaxQ, kErrInvalid, "attn_decode: 1..32 queries per sequence");
+  SD_CHECK(a.n_wtiles >= attn_decode_tiles(a.max_keys), kErrInvalid, "attn_decode: workspace too small");
+  const int nsh = a.nseq * a.nh;
+  // bytes: upper bound (full cache), the graph does not know the cursor
+  ProfScope prof("attn_decode", 4.0 * a.max_keys * kHD * nsh * a.nq,
+                 2.0 * a.max_keys * kHD * nsh * (a.io_bf16 ? 2 : 4), st);
+  const dim3 g1(cdiv(a.max_keys, 256), nsh), g2(nsh, cdiv(a.nq, 4));
+  if (a.io_bf16) {
+    hipLaunchKernelGGL(attn_decode_kernel<true>, g1, dim3(256), 0, st, a);
+    SD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(attn_combine_kernel<true>, g2, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(attn_decode_kernel<false>, g1, dim3(256), 0, st, a);
+    SD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(attn_combine_kernel<false>, g2, dim3(256), 0, st, a);
+  }
+  SD_LAUNCH_CHECK();
+}
+
+void gather_window(const float* hist, int D, const int* cursor, const int* n_valid, int pad, int rows, float* dst,
+                   hipStream_t st) {
+  const int64_t n = (int64_t)rows * D;
+  ProfScope prof("gather_window", 0.0, 8.0 * n, st);
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(gather_window_kernel, dim3(blocks), dim3(256), 0, st, hist, D, cursor, n_valid, pad, rows, dst);
+  SD_LAUNCH_CHECK();
+}
+
+void cursor_advance(int* cursor, int by, int* mirror, hipStream_t st) {
+  hipLaunchKernelGGL(cursor_advance_kernel, dim3(1), dim3(64), 0, st, cursor, by, mirror);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

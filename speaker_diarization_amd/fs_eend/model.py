@@ -4,12 +4,15 @@
 test(src, ilens, max_nspks) runs in libsdiar (HIP, gfx950): BatchNorm-folded
 input Linear + LayerNorm, causal transformer encoder, look-ahead Conv1d, L2
 norm, the shared fusion-layer attractor decoder on the (T, C) token grid and
-the per-frame emb·attractorᵀ scores.  FS-EEND does not shard (causal
+the per-frame emb·attractorᵀ scores.  stream(chunk) returns an FsEendStream that
+produces the same scores chunk by chunk from per-layer K/V histories (every
+chunk's kernels replayed as one hipGraph).  FS-EEND does not shard (causal
 full-history attention): multi-GPU runs are replicas, one
 recording per GPU.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List
 
 import torch
@@ -108,6 +111,85 @@ class OnlineTransformerDADiarization:
         preds, emb, att = self.test_device(buf, ilens, max_nspks)
         return ([preds[i, : ilens[i]] for i in range(S)], [emb[i, : ilens[i]] for i in range(S)],
                 [att[i, : ilens[i]] for i in range(S)])
+
+
+    def stream(self, chunk: int = 1, max_frames: int = None, max_nspks: int = 6, use_graph: bool = True):
+        """Streaming counterpart of test() for one recording: push feature rows as they arrive,
+        receive each frame's (max_nspks) scores once its 9-frame look-ahead is available."""
+        if self._h is None:
+            raise RuntimeError("load_state_dict() must be called before stream()")
+        return FsEendStream(self, chunk, max_frames or self.max_frames, max_nspks, use_graph)
+
+
+class FsEendStream:
+    """Chunked FS-EEND scoring (libsdiar sd_fseend_stream_*).  push(x) accepts any number of
+    (n, in_size) rows (buffered into chunks of `chunk` frames) and returns the (m, C) scores of
+    the frames that became final; flush() ends the input and returns the rest.  Concatenated,
+    the outputs equal test([x_all], [T])[0][0] (fs_eend.py:79-96)."""
+
+    def __init__(self, model: "OnlineTransformerDADiarization", chunk: int, max_frames: int, max_nspks: int,
+                 use_graph: bool):
+        self.model = model
+        self.chunk = int(chunk)
+        self.C = int(max_nspks)
+        self.max_frames = int(max_frames)
+        self.device = model.device
+        h = ctypes.c_void_p()
+        _lib.call("sd_fseend_stream_create", model._h, self.chunk, self.max_frames, self.C, int(bool(use_graph)),
+                  ctypes.byref(h))
+        self._s = h
+        self._pending = torch.zeros(0, model.cfg.in_size, device=self.device)
+        self._buf = torch.zeros(self.chunk, model.in_ld, device=self.device, dtype=torch.float32)
+        # one push emits at most ceil((chunk + 9) / chunk) chunks; flush up to ceil(9 / chunk) + 1
+        self._out = torch.empty((self.chunk + 9) * 2 + self.chunk, self.C, device=self.device, dtype=torch.float32)
+
+    def device_bytes(self) -> int:
+        return int(_lib.load().sd_fseend_stream_device_bytes(self._s))
+
+    def _push_rows(self, rows) -> torch.Tensor:
+        n = int(rows.shape[0])
+        self._buf.zero_()
+        self._buf[:n, : self.model.cfg.in_size] = rows
+        cnt = ctypes.c_int()
+        _lib.call("sd_fseend_stream_push", self._s, _lib.ptr(self._buf), self.model.in_ld, n, _lib.ptr(self._out),
+                  self._out.shape[0], ctypes.byref(cnt), _lib.stream_ptr(self.device))
+        return self._out[: cnt.value].clone()
+
+    def push(self, x) -> torch.Tensor:
+        x = x.to(self.device, torch.float32).reshape(-1, self.model.cfg.in_size)
+        data = torch.cat([self._pending, x], 0)
+        outs = []
+        full = data.shape[0] // self.chunk * self.chunk
+        for i in range(0, full, self.chunk):
+            outs.append(self._push_rows(data[i : i + self.chunk]))
+        self._pending = data[full:]
+        return torch.cat(outs, 0) if outs else self._out[:0].clone()
+
+    def flush(self) -> torch.Tensor:
+        outs = []
+        if self._pending.shape[0] > 0:
+            outs.append(self._push_rows(self._pending))
+            self._pending = self._pending[:0]
+        cnt = ctypes.c_int()
+        _lib.call("sd_fseend_stream_flush", self._s, _lib.ptr(self._out), self._out.shape[0], ctypes.byref(cnt),
+                  _lib.stream_ptr(self.device))
+        outs.append(self._out[: cnt.value].clone())
+        return torch.cat(outs, 0)
+
+    def reset(self):
+        self._pending = self._pending[:0]
+        _lib.call("sd_fseend_stream_reset", self._s, _lib.stream_ptr(self.device))
+
+    def close(self):
+        if getattr(self, "_s", None) is not None:
+            _lib.load().sd_fseend_stream_destroy(self._s)
+        self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def ctypes_int_array(vals):

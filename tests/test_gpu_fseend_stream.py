@@ -1,0 +1,152 @@
+"""Streaming FS-EEND (sd_fseend_stream_*: K/V histories + hipGraph replay) against the
+whole-recording test() path, the CPU oracle and the reference golden vector.
+
+The reference has no streaming entry point: it recomputes OnlineTransformerDADiarization.test()
+(fs_eend.py:79-96) over the whole recording.  With its causal masks (mask_delay 0 in every
+shipped config) the concatenated stream output must equal that forward.  Tolerances: fp32
+1e-3 (north_star), bf16 3e-2; graph replay vs direct launches: bit-identical."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fseend_ref
+from speaker_diarization_amd._lib import SdiarError
+from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
+from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
+from tests.golden.make_golden import FSEEND_CASES, eda_inputs
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FP32_ATOL = 1e-3
+BF16_ATOL = 3e-2
+
+
+def _model(wseed, precision="fp32", max_frames=2048, delay=0):
+    m = OnlineTransformerDADiarization(n_speakers=None, in_size=345, n_units=256, n_heads=4, enc_n_layers=4,
+                                       dec_n_layers=2, dropout=0.1, has_mask=True, max_seqlen=10000,
+                                       dec_dim_feedforward=2048, conv_delay=9, mask_delay=delay,
+                                       precision=precision, max_seqs=1, max_frames=max_frames, max_nspks=6)
+    m.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(mask_delay=delay), seed=wseed)))
+    return m
+
+
+def _stream_all(m, x, chunk, C=6, use_graph=True, pieces=None):
+    s = m.stream(chunk=chunk, max_frames=x.shape[0] + 64, max_nspks=C, use_graph=use_graph)
+    outs = []
+    if pieces is None:
+        pieces = [chunk] * (x.shape[0] // chunk + 1)
+    i = 0
+    for p in pieces:
+        if i >= x.shape[0]:
+            break
+        outs.append(s.push(x[i : i + p]))
+        i += p
+    if i < x.shape[0]:
+        outs.append(s.push(x[i:]))
+    outs.append(s.flush())
+    return torch.cat(outs, 0), s
+
+
+@pytest.mark.parametrize("chunk", [1, 4, 7, 32])
+def test_stream_matches_test_fp32(gpu, chunk):
+    T = 157
+    m = _model(801)
+    x = torch.from_numpy(eda_inputs([T], seed=81)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    out, _ = _stream_all(m, x, chunk)
+    assert out.shape == (T, 6)
+    np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
+
+
+def test_stream_matches_oracle_and_golden(gpu):
+    lens, C, delay, iseed, wseed = FSEEND_CASES["fseend_T240"]
+    g = dict(np.load(os.path.join(GOLD, "fseend_T240.npz")))
+    m = _model(wseed)
+    xs = eda_inputs(lens, seed=iseed)
+    out, _ = _stream_all(m, torch.from_numpy(xs[0]).to(gpu), 5, C=C)
+    np.testing.assert_allclose(out.cpu().numpy(), g["out"], atol=FP32_ATOL)
+    sd = to_torch(fseend_state_dict(FSEENDConfig(), seed=wseed))
+    ro, _, _ = fseend_ref.fseend_test(sd, FSEENDConfig(), [torch.from_numpy(xs[0])], lens, C)
+    np.testing.assert_allclose(out.cpu().numpy(), ro[0].numpy(), atol=FP32_ATOL)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_replay_is_bit_identical(gpu, precision):
+    T = 120
+    m = _model(802, precision)
+    x = torch.from_numpy(eda_inputs([T], seed=82)[0]).to(gpu)
+    a, _ = _stream_all(m, x, 3, use_graph=True)
+    b, _ = _stream_all(m, x, 3, use_graph=False)
+    assert torch.equal(a, b)
+
+
+def test_stream_bf16_vs_test(gpu):
+    T = 300
+    m = _model(803, "bf16")
+    x = torch.from_numpy(eda_inputs([T], seed=83)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    out, _ = _stream_all(m, x, 8)
+    np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=BF16_ATOL)
+    sd = to_torch(fseend_state_dict(FSEENDConfig(), seed=803))
+    ro, _, _ = fseend_ref.fseend_test(sd, FSEENDConfig(), [x.cpu()], [T], 6)
+    np.testing.assert_allclose(out.cpu().numpy(), ro[0].numpy(), atol=BF16_ATOL)
+
+
+def test_stream_long_many_key_tiles(gpu):
+    """T = 1100 frames: several 256-key attention blocks and ragged last tiles."""
+    T = 1100
+    m = _model(804, max_frames=T)
+    x = torch.from_numpy(eda_inputs([T], seed=84)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    out, _ = _stream_all(m, x, 16)
+    np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
+
+
+@pytest.mark.parametrize("T", [1, 5, 9, 10, 28])
+def test_short_recordings_flush(gpu, T):
+    """Shorter than the 9-frame look-ahead: every score comes out of flush()."""
+    m = _model(805, max_frames=64)
+    x = torch.from_numpy(eda_inputs([T], seed=85 + T)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    out, _ = _stream_all(m, x, 4)
+    np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
+
+
+def test_ragged_pushes_and_reset(gpu):
+    T = 90
+    m = _model(806)
+    x = torch.from_numpy(eda_inputs([T], seed=86)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    s = m.stream(chunk=4, max_frames=256)
+    for _ in range(2):   # second pass after reset() reuses the histories and captured graphs
+        outs, i = [], 0
+        for p in [1, 6, 13, 2, 30, 11, 27]:
+            outs.append(s.push(x[i : i + p]))
+            i += p
+        outs.append(s.flush())
+        out = torch.cat(outs)
+        np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
+        s.reset()
+
+
+def test_stream_errors(gpu):
+    m = _model(807, max_frames=64)
+    with pytest.raises(ValueError):
+        m.stream(chunk=33)
+    with pytest.raises(ValueError):
+        m.stream(chunk=4, max_nspks=7)
+    s = m.stream(chunk=4, max_frames=8)
+    x = torch.from_numpy(eda_inputs([20], seed=87)[0]).to(gpu)
+    s.push(x[:8])
+    with pytest.raises(ValueError, match="max_frames"):
+        s.push(x[8:12])
+    s2 = m.stream(chunk=4, max_frames=64)
+    s2.push(x[:4])
+    s2.flush()
+    with pytest.raises(SdiarError, match="ended"):
+        s2.push(x[4:8])
+    md = _model(808, max_frames=64, delay=2)
+    with pytest.raises(ValueError, match="mask_delay"):
+        md.stream(chunk=4)
