@@ -40,6 +40,10 @@ WORKLOADS = {
     "c5": dict(kind="fseend", n_spk=3, minutes=10.0,
                desc="C5: 8 kHz recording, FS-EEND (4-layer causal encoder, shared 2x fusion decoder, "
                     "logmel23, 100 ms frames), whole recording per test() call; replicas only"),
+    "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
+                desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
+                     "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
+                     "waits for every chunk's scores; replicas only"),
 }
 
 PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
@@ -59,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--chunk", type=int, default=None, help="c5s: model frames per streaming push")
+    ap.add_argument("--no-graph", action="store_true", help="c5s: direct launches instead of hipGraph replay")
     return ap.parse_args()
 
 
@@ -332,9 +338,117 @@ def main_eend(a, wl):
         dist.destroy_process_group()
 
 
+def main_stream(a, wl):
+    """C5 latency mode: one recording per GPU streamed chunk by chunk through the C ABI
+    (sd_fseend_stream_push on device feature rows); every push is synchronised, as a
+    live caller waiting for each chunk's scores would be.  value = 10 ms frames/s of the
+    streamed recording (N replicas: summed); per-chunk latency percentiles alongside."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from speaker_diarization_amd import _lib
+    from speaker_diarization_amd.feature import eend_features
+    from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
+    from speaker_diarization_amd.synth import make_meeting
+    from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    minutes = a.minutes if a.minutes is not None else wl["minutes"]
+    chunk = a.chunk or wl["chunk"]
+    meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank, sample_rate=8000)
+    wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+    m = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=a.precision,
+                                       max_seqs=1, max_frames=64, max_nspks=6)
+    m.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(), seed=777)))
+    feats = eend_features(wav, 8000, 200, 80, "logmel23", 7, 10, ld=m.in_ld).contiguous()
+    T = feats.shape[0]
+    lib = _lib.load()
+    s = ctypes.c_void_p()
+    _lib.call("sd_fseend_stream_create", m._h, chunk, T + chunk, 6, 0 if a.no_graph else 1, ctypes.byref(s))
+    preds = torch.empty(T + 64, 6, device=dev)
+    sp = _lib.stream_ptr(dev)
+    cnt = ctypes.c_int()
+    base, row_bytes = feats.data_ptr(), m.in_ld * 4
+    lat = []
+
+    def step(record):
+        lib.sd_fseend_stream_reset(s, sp)
+        out = 0
+        for i in range(0, T, chunk):
+            n = min(chunk, T - i)
+            t0 = time.perf_counter()
+            _lib.check(lib.sd_fseend_stream_push(s, base + i * row_bytes, m.in_ld, n, preds.data_ptr() + out * 24,
+                                                 preds.shape[0] - out, ctypes.byref(cnt), sp))
+            torch.cuda.synchronize()
+            if record:
+                lat.append(time.perf_counter() - t0)
+            out += cnt.value
+        _lib.check(lib.sd_fseend_stream_flush(s, preds.data_ptr() + out * 24, preds.shape[0] - out,
+                                              ctypes.byref(cnt), sp))
+        torch.cuda.synchronize()
+        assert out + cnt.value == T, (out, cnt.value, T)
+
+    for _ in range(a.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # parity spot check of this very run against the whole-recording forward of the first
+    # 2000 frames (its last 9 frames see zero look-ahead there, so they are not compared)
+    Tc = min(T, 2000)
+    m2 = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=a.precision,
+                                        max_seqs=1, max_frames=Tc, max_nspks=6)
+    m2.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(), seed=777)))
+    full, _, _ = m2.test_device(feats[None, :Tc], [Tc], 6, want_emb=False, want_attractors=False)
+    nc = Tc - 9 if Tc < T else Tc
+    err = float((full[0, :nc] - preds[:nc]).abs().max())
+    lib.sd_fseend_stream_destroy(s)
+    L = np.array(lat) * 1e3
+    frames = meeting.wav.size // 80 * world
+    if rank == 0:
+        line = {"metric": "diarized frames/sec (10 ms hop)", "value": round(frames * a.steps / elapsed, 1),
+                "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                "ms_per_step": round(elapsed / a.steps * 1000.0, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
+                "data": "synthetic 8 kHz recording (speaker_diarization_amd/synth.py), seeded random weights",
+                "config": {"workload": wl["desc"], "minutes_per_gpu": minutes, "chunk_frames": chunk,
+                           "chunk_audio_ms": chunk * 100, "model_frames": T,
+                           "hipgraph": not a.no_graph,
+                           "parallelism": "replicas x%d" % world if world > 1 else "1 GPU"},
+                "latency_ms": {"p50": round(float(np.percentile(L, 50)), 4),
+                               "p90": round(float(np.percentile(L, 90)), 4),
+                               "p99": round(float(np.percentile(L, 99)), 4),
+                               "max": round(float(L.max()), 4), "mean": round(float(L.mean()), 4)},
+                "real_time_factor": round(float(L.mean()) / (chunk * 100.0), 5),
+                "max_abs_diff_vs_test": err}
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     _a = parse()
-    if WORKLOADS[_a.workload].get("kind") in ("eda", "fseend"):
+    if WORKLOADS[_a.workload].get("kind") == "fseend_stream":
+        main_stream(_a, WORKLOADS[_a.workload])
+    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend"):
         main_eend(_a, WORKLOADS[_a.workload])
     else:
         main()

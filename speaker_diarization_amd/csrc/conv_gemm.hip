@@ -266,6 +266,10 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(!p.gate || p.gate_seg > 0, kErrInvalid, "conv_gemm: gate_seg must be > 0");
   SD_CHECK(!p.glu || (bf16 && gemm_stream_supported(p)), kErrInvalid,
            "conv_gemm: the GLU epilogue exists on the bf16 streaming path only");
+  if (gemm_skinny_supported(p)) {   // <= 16 rows: weight streaming (streaming FS-EEND chunks)
+    conv_gemm_skinny(p, bf16, st);
+    return;
+  }
   if (bf16) {
     conv_gemm_bf16(p, st);
     return;

@@ -51,7 +51,7 @@ class FsEendStream {
   int* state_ = nullptr;               // [0] encoder frames, [1] valid frames, [2] decoder frames
   int n_enc_ = 0, n_valid_ = 0, n_dec_ = 0, n_out_ = 0;
   bool closed_ = false;
-  int n_wtiles_ = 0;
+  int n_blocks_ = 0;
   // staging (chunk-sized)
   float *F_ = nullptr, *Y_ = nullptr, *X_ = nullptr, *W_ = nullptr, *Yc_ = nullptr, *E_ = nullptr;
   float *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;

@@ -1,0 +1,208 @@
+// Skinny GEMM (M <= 16 output rows) for the streaming FS-EEND chunks on gfx950.
+//
+// A chunk of c frames turns every linear layer into an (c or c*C rows) x K x N product:
+// the weights (N*K) dominate the bytes, an MFMA tile of 64-128 rows would be >90 % padding,
+// and the tile kernels give each workgroup a 128-column panel -> 2-16 workgroups for
+// N = 256..2048.  Here the A rows (M*K, a few KB) are staged once per workgroup in LDS as
+// fp32, and each wave streams NC weight rows (16-B loads, coalesced along K) against them,
+// so the grid has N/NC waves and the kernel runs at the weight-streaming rate.  The
+// look-ahead Conv1d (k 19, stride 1, no padding in the streaming window) is the same
+// product: output row m's im2col row is the contiguous span A[m*Cin, m*Cin + 19*Cin).
+//
+// Epilogue = conv_gemm's: v = acc*alpha[n] + beta[n] (+res[m*res_ld + n]), activation,
+// out[b*o_sb + ho*o_sh + wo*o_sw + n*o_sn] (fp32 or bf16).  fp32 arithmetic throughout.
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kSkinnyLdsFloats = 16384;   // 64 KiB of staged A
+
+template <int NC, bool WBF>
+__device__ __forceinline__ void skinny_load(const ConvGemmArgs& p, int n0, int kv0, int nv, uint4 (&w)[NC][4]) {
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int64_t row = (int64_t)min(n0 + j, p.N - 1) * p.K;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int kv = kv0 + b * 64;
+      if (kv < nv) {
+        if constexpr (WBF) w[j][b] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.Wt) + row + kv * 8);
+        else w[j][b] = *reinterpret_cast<const uint4*>(static_cast<const float*>(p.Wt) + row + kv * 4);
+      } else {
+        w[j][b] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
+}
+
+template <int MMAX, int NC, bool WBF>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M, int a_rs) {
+  extern __shared__ float As[];
+  constexpr int VE = WBF ? 8 : 4;   // weight elements per 16-B load
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int K = p.K, nv = K / VE;
+  const int n0 = (blockIdx.x * 4 + wid) * NC;
+  const bool active = n0 < p.N;
+  // Issue the first weight batch and the epilogue operands before staging A, so their
+  // latency overlaps the staging round trip.
+  uint4 cur[NC][4];
+  if (active) skinny_load<NC, WBF>(p, n0, lane, nv, cur);
+  const int me = lane / NC, mj = lane % NC, mn = min(n0 + mj, p.N - 1);
+  const bool owner = active && me < M && n0 + mj < p.N;
+  float ea = 1.f, eb = 0.f, er = 0.f;
+  if (owner) {
+    if (p.alpha) ea = p.alpha[mn];
+    if (p.beta) eb = p.beta[mn];
+    if (p.res)
+      er = p.res_bf16 ? bf_bits2f(static_cast<const uint16_t*>(p.res)[(int64_t)me * p.res_ld + mn])
+                      : static_cast<const float*>(p.res)[(int64_t)me * p.res_ld + mn];
+  }
+  const int span = (M - 1) * a_rs + K;
+  if (p.a_bf16) {
+    const uint16_t* a = static_cast<const uint16_t*>(p.A) + p.a_coff;
+    for (int i = tid; i < span; i += 256) As[i] = bf_bits2f(a[i]);
+  } else {
+    const float* a = static_cast<const float*>(p.A) + p.a_coff;
+    for (int i = tid; i < span; i += 256) As[i] = a[i];
+  }
+  __syncthreads();
+  if (!active) return;
+  float acc[MMAX][NC];
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m)
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc[m][j] = 0.f;
+  for (int kv0 = lane; kv0 < nv; kv0 += 256) {
+    uint4 nxt[NC][4];
+    const bool more = kv0 + 256 < nv;
+    if (more) skinny_load<NC, WBF>(p, n0, kv0 + 256, nv, nxt);   // next batch in flight during the FMAs
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int kv = kv0 + b * 64;
+      if (kv < nv) {
+        float w[NC][VE];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const uint32_t q[4] = {cur[j][b].x, cur[j][b].y, cur[j][b].z, cur[j][b].w};
+          if constexpr (WBF) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[j][2 * e] = __uint_as_float(q[e] << 16);
+              w[j][2 * e + 1] = __uint_as_float(q[e] & 0xffff0000u);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[j][e] = __uint_as_float(q[e]);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < MMAX; ++m) {
+          if (m < M) {
+            const float* ar = As + m * a_rs + kv * VE;
+            float av[VE];
+#pragma unroll
+            for (int e = 0; e < VE; e += 4) {
+              const float4 t = *reinterpret_cast<const float4*>(ar + e);
+              av[e] = t.x; av[e + 1] = t.y; av[e + 2] = t.z; av[e + 3] = t.w;
+            }
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+#pragma unroll
+              for (int e = 0; e < VE; ++e) acc[m][j] = fmaf(av[e], w[j][e], acc[m][j]);
+          }
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) cur[j][b] = nxt[j][b];
+    }
+  }
+  // reduce over the wave; lane (m*NC + j) owns element (m, n0 + j)
+  float mine = 0.f;
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) {
+    if (m < M) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const float s = warp_sum(acc[m][j]);
+        if (lane == m * NC + j) mine = s;
+      }
+    }
+  }
+  if (!owner) return;
+  float v = apply_act(mine * ea + eb + er, p.act);
+  const int hw = p.Ho * p.Wo;
+  const int b = me / hw, r = me % hw, ho = r / p.Wo, wo = r % p.Wo;
+  const int64_t o = (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw + (int64_t)mn * p.o_sn;
+  if (p.out_bf16) static_cast<uint16_t*>(p.out)[o] = f2bf_bits(v);
+  else static_cast<float*>(p.out)[o] = v;
+}
+
+// A(m, k) = A[a_coff + m*a_rs + k]: a plain linear (row stride lda), or a stride-1
+// unpadded 1-D conv whose taps are consecutive rows (Cin == lda).
+int skinny_row_stride(const ConvGemmArgs& p) {
+  if (a_rows_linear(p)) return p.lda;
+  if (p.B == 1 && p.H == 1 && p.Ho == 1 && p.kh == 1 && p.sw == 1 && p.dw == 1 && p.pw == 0 && p.ph == 0 &&
+      p.Cin == p.lda && p.W >= p.Wo + p.kw - 1)
+    return p.lda;
+  return -1;
+}
+
+template <int MMAX, int NC>
+void launch_skinny(const ConvGemmArgs& p, int M, int rs, bool wbf, hipStream_t st) {
+  const int span = (M - 1) * rs + p.K;
+  const size_t lds = (size_t)span * sizeof(float);
+  const dim3 grid(cdiv(p.N, 4 * NC));
+  static bool attr_set[2] = {false, false};   // once per instantiation, before any graph capture
+  if (!attr_set[wbf]) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MMAX, NC, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kSkinnyLdsFloats * 4));
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_skinny_kernel<MMAX, NC, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kSkinnyLdsFloats * 4));
+    attr_set[wbf] = true;
+  }
+  if (wbf) {
+    hipLaunchKernelGGL((gemm_skinny_kernel<MMAX, NC, true>), grid, dim3(256), lds, st, p, M, rs);
+  } else {
+    hipLaunchKernelGGL((gemm_skinny_kernel<MMAX, NC, false>), grid, dim3(256), lds, st, p, M, rs);
+  }
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+bool gemm_skinny_supported(const ConvGemmArgs& p) {
+  const int M = p.B * p.Ho * p.Wo;
+  if (M < 1 || M > 16 || p.pre_scale || p.gate || p.glu) return false;
+  if (p.K % 8 != 0) return false;
+  const int rs = skinny_row_stride(p);
+  if (rs < 0) return false;
+  if (((int64_t)(M - 1) * rs + p.K) > kSkinnyLdsFloats) return false;
+  return p.a_coff % 4 == 0 && rs % 4 == 0;
+}
+
+void conv_gemm_skinny(const ConvGemmArgs& p, bool wbf, hipStream_t st) {
+  const int M = p.B * p.Ho * p.Wo;
+  const int rs = skinny_row_stride(p);
+  ProfScope prof(wbf ? "gemm_skinny_bf16" : "gemm_skinny_f32", 2.0 * M * p.N * (double)p.K,
+                 (wbf ? 2.0 : 4.0) * p.N * p.K + 4.0 * M * (p.K + p.N), st);
+  // 4 weight rows per wave once there are >= 512 waves' worth of columns, else 1.
+  const bool nc4 = p.N >= 2048;
+  if (M == 1) {
+    if (nc4) launch_skinny<1, 4>(p, M, rs, wbf, st); else launch_skinny<1, 1>(p, M, rs, wbf, st);
+  } else if (M <= 8) {
+    if (nc4) launch_skinny<8, 4>(p, M, rs, wbf, st); else launch_skinny<8, 1>(p, M, rs, wbf, st);
+  } else {
+    if (nc4) launch_skinny<16, 4>(p, M, rs, wbf, st); else launch_skinny<16, 1>(p, M, rs, wbf, st);
+  }
+}
+
+}  // namespace sd

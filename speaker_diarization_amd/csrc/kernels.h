@@ -50,6 +50,8 @@ void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
 bool fcm_conv_supported(const ConvGemmArgs& p);               // bf16 3x3 32->32, pad 1, freq stride 1|2
 void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
+bool gemm_skinny_supported(const ConvGemmArgs& p);            // <= 16 rows, linear or stride-1 1-D conv
+void conv_gemm_skinny(const ConvGemmArgs& p, bool w_bf16, hipStream_t st);
 
 // Output row (b, ho, wo) sits at linear row m = (b*Ho + ho)*Wo + wo, stride o_sw
 // (strides of size-1 dimensions do not matter).
@@ -243,11 +245,11 @@ struct DecodeAttnArgs {
   const int* pos = nullptr;   // device cursor
   int delay = 0;
   int max_keys = 0;           // history capacity: grid coverage
-  int n_wtiles = 0;           // workspace tiles per (sequence, head) >= attn_decode_tiles(max_keys)
-  float* ws = nullptr;        // nseq*nh*n_wtiles*nq*(2+hd) floats
+  int n_blocks = 0;           // workspace partials per (sequence, head) >= attn_decode_blocks(max_keys)
+  float* ws = nullptr;        // nseq*nh*n_blocks*nq*(2+hd) floats
   bool io_bf16 = false;
 };
-int attn_decode_tiles(int max_keys);
+int attn_decode_blocks(int max_keys);
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,

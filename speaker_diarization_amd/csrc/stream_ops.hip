@@ -16,8 +16,9 @@
 //                   encoder output)
 //   attn_decode     softmax(q·kᵀ·scale)·v for nq (≤ 32) queries at absolute positions
 //                   cursor + i against all cached keys j <= cursor + i + delay:
-//                   split-K over 64-key wave tiles (lane = key for q·k, lane = head dim
-//                   for p·v), per-wave (m, l, o) partials, one combine wave per query.
+//                   a fixed grid of <= 32 blocks per (sequence, head) whose waves stride
+//                   over 64-key tiles with an online softmax, block-merged partials, one
+//                   combine wave per query (fixed grid: replayable for any cursor).
 //                   fp32 arithmetic; K/V/Q/O fp32 or bf16 (the dtype of the cache).
 //                   HBM-bound: each cached key row is read once per (sequence, head).
 //   gather_window   rows [cursor - pad, cursor + c + pad) of the encoder-output history,
@@ -71,91 +72,143 @@ __device__ __forceinline__ void load_row64(const act_t<IOBF>* p, float* v) {
   }
 }
 
-// grid (n_tiles256, nseq*nh), 256 threads: wave w of block b owns keys [(4b + w)*64, +64).
-template <bool IOBF>
+// grid (nblk, nseq*nh), 256 threads.  Wave w of block b walks the 64-key tiles
+// t = 4b + w, 4b + w + 4*nblk, ... below the device cursor's key count with an online
+// softmax per query (lane = key for q·k; lane = (key parity, head-dim pair) for p·v, so
+// each lane issues 32 independent 4/8-B V loads per tile), the 4 waves merge in LDS and
+// the block writes one (m, l, o[64]) partial per query.
+template <bool IOBF, int QMAX>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
   using io_t = act_t<IOBF>;
-  __shared__ float qs[kMaxQ][kHD];
-  __shared__ float ps[4][kMaxQ][64];
+  __shared__ float qs[QMAX][kHD];
+  __shared__ float ps[4][QMAX][64];
+  __shared__ float wm[4][QMAX], wl[4][QMAX];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int sh = blockIdx.y, s = sh / a.nh, h = sh % a.nh;
+  const int nq = a.nq;
   const int pos = *a.pos;
-  const int total = pos + a.nq;                         // keys present after this chunk's append
-  const int wtile = blockIdx.x * 4 + wid;               // 64-key tile index
-  const int kbeg = blockIdx.x * 256;
-  if (kbeg >= total) return;                            // uniform over the block
+  const int total = pos + nq;                           // keys present after this chunk's append
   const io_t* qb = reinterpret_cast<const io_t*>(a.q) + (int64_t)s * a.q_seq + h * kHD;
-  for (int i = tid; i < a.nq * kHD; i += 256) {
+  for (int i = tid; i < nq * kHD; i += 256) {
     const int qi = i / kHD, d = i % kHD;
     qs[qi][d] = ld_act(qb, (int64_t)qi * a.q_tok + d) * a.scale;
   }
   __syncthreads();
-  const int k0 = wtile * 64;
-  if (k0 >= total) return;                              // whole wave past the end (wave-uniform)
-  const int j = k0 + lane;
-  const bool kv = j < total;
-  float kr[kHD];
-  {
-    const io_t* kp = reinterpret_cast<const io_t*>(a.k) + (int64_t)min(j, total - 1) * a.kv_tok +
-                     (int64_t)s * a.kv_seq + h * kHD;
-    load_row64<IOBF>(kp, kr);
-  }
-  float* part = a.ws + ((int64_t)sh * a.n_wtiles + wtile) * a.nq * (2 + kHD);
-  for (int qi = 0; qi < a.nq; ++qi) {
-    float sc = 0.f;
+  const io_t* kb = reinterpret_cast<const io_t*>(a.k) + (int64_t)s * a.kv_seq + h * kHD;
+  const io_t* vb = reinterpret_cast<const io_t*>(a.v) + (int64_t)s * a.kv_seq + h * kHD;
+  const int half = lane >> 5, d2 = (lane & 31) * 2;
+  float m_run[QMAX], l_run[QMAX], o0[QMAX], o1[QMAX];
 #pragma unroll
-    for (int d = 0; d < kHD; ++d) sc = fmaf(qs[qi][d], kr[d], sc);
-    const bool vis = kv && j <= pos + qi + a.delay;
-    sc = vis ? sc : -INFINITY;
-    const float m = warp_max(sc);
-    const float p = (m == -INFINITY || !vis) ? 0.f : __expf(sc - m);
-    const float l = warp_sum(p);
-    ps[wid][qi][lane] = p;   // read back by the same wave only (LDS ops of a wave stay in order)
-    if (lane == 0) {
-      part[qi * (2 + kHD)] = m;
-      part[qi * (2 + kHD) + 1] = l;
+  for (int qi = 0; qi < QMAX; ++qi) { m_run[qi] = -INFINITY; l_run[qi] = 0.f; o0[qi] = 0.f; o1[qi] = 0.f; }
+  for (int t = blockIdx.x * 4 + wid; t * 64 < total; t += gridDim.x * 4) {
+    const int k0 = t * 64, j = k0 + lane;
+    const bool kv = j < total;
+    float kr[kHD];
+    load_row64<IOBF>(kb + (int64_t)min(j, total - 1) * a.kv_tok, kr);
+    // V operands for this tile: keys k0 + 2i + half, dims d2, d2 + 1
+    float v0[32], v1[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int key = min(k0 + 2 * i + half, total - 1);
+      const io_t* vr = vb + (int64_t)key * a.kv_tok + d2;
+      if constexpr (IOBF) {
+        const uint32_t u = *reinterpret_cast<const uint32_t*>(vr);
+        v0[i] = __uint_as_float(u << 16);
+        v1[i] = __uint_as_float(u & 0xffff0000u);
+      } else {
+        const float2 u = *reinterpret_cast<const float2*>(vr);
+        v0[i] = u.x;
+        v1[i] = u.y;
+      }
+    }
+#pragma unroll
+    for (int qi = 0; qi < QMAX; ++qi) {
+      if (qi < nq) {
+        float sc = 0.f;
+#pragma unroll
+        for (int d = 0; d < kHD; ++d) sc = fmaf(qs[qi][d], kr[d], sc);
+        const bool vis = kv && j <= pos + qi + a.delay;
+        sc = vis ? sc : -INFINITY;
+        const float mn = fmaxf(m_run[qi], warp_max(sc));
+        const float p = (!vis || mn == -INFINITY) ? 0.f : __expf(sc - mn);
+        const float corr = (m_run[qi] == -INFINITY) ? 0.f : __expf(m_run[qi] - mn);
+        l_run[qi] = l_run[qi] * corr + warp_sum(p);
+        o0[qi] *= corr;
+        o1[qi] *= corr;
+        m_run[qi] = mn;
+        ps[wid][qi][lane] = p;   // read back by the same wave only (a wave's LDS ops stay in order)
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int qi = 0; qi < QMAX; ++qi) {
+      if (qi < nq) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const float p = ps[wid][qi][2 * i + half];
+          o0[qi] = fmaf(p, v0[i], o0[qi]);
+          o1[qi] = fmaf(p, v1[i], o1[qi]);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // merge the two key-parity halves, park the wave's partial in LDS
+#pragma unroll
+  for (int qi = 0; qi < QMAX; ++qi) {
+    if (qi < nq) {
+      o0[qi] += __shfl_xor(o0[qi], 32, 64);
+      o1[qi] += __shfl_xor(o1[qi], 32, 64);
+      if (half == 0) {
+        ps[wid][qi][d2] = o0[qi];
+        ps[wid][qi][d2 + 1] = o1[qi];
+      }
+      if (lane == 0) {
+        wm[wid][qi] = m_run[qi];
+        wl[wid][qi] = l_run[qi];
+      }
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  // p·v: lane = head dim, loop over the wave's 64 keys (V rows read coalesced).
-  float acc[kMaxQ];
+  __syncthreads();
+  float* part = a.ws + ((int64_t)sh * gridDim.x + blockIdx.x) * nq * (2 + kHD);
+  for (int i = tid; i < nq * kHD; i += 256) {
+    const int qi = i / kHD, d = i % kHD;
+    float M = -INFINITY;
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) acc[qi] = 0.f;
-  const io_t* vb = reinterpret_cast<const io_t*>(a.v) + (int64_t)s * a.kv_seq + h * kHD + lane;
-  const int nk = min(64, total - k0);
-  for (int kk = 0; kk < nk; ++kk) {
-    const float vv = ld_act(vb, (int64_t)(k0 + kk) * a.kv_tok);
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, wm[w][qi]);
+    float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int qi = 0; qi < kMaxQ; ++qi)
-      if (qi < a.nq) acc[qi] = fmaf(ps[wid][qi][kk], vv, acc[qi]);
+    for (int w = 0; w < 4; ++w) {
+      const float e = (wm[w][qi] == -INFINITY) ? 0.f : __expf(wm[w][qi] - M);
+      L = fmaf(e, wl[w][qi], L);
+      O = fmaf(e, ps[w][qi][d], O);
+    }
+    part[qi * (2 + kHD) + 2 + d] = O;
+    if (d == 0) {
+      part[qi * (2 + kHD)] = M;
+      part[qi * (2 + kHD) + 1] = L;
+    }
   }
-#pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi)
-    if (qi < a.nq) part[qi * (2 + kHD) + 2 + lane] = acc[qi];
 }
 
-// grid (nseq*nh), block 64*nq: wave qi combines the partials of query qi.
+// grid (nseq*nh, cdiv(nq, 4)), 256 threads: wave -> query, lane -> head dim; merges the
+// nblk (<= 64) block partials (lane-parallel max / weights, shuffled weights for o).
 template <bool IOBF>
-__global__ __launch_bounds__(256) void attn_combine_kernel(DecodeAttnArgs a) {
+__global__ __launch_bounds__(256) void attn_combine_kernel(DecodeAttnArgs a, int nblk) {
   using io_t = act_t<IOBF>;
   const int sh = blockIdx.x, s = sh / a.nh, h = sh % a.nh;
   const int qi = blockIdx.y * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (qi >= a.nq) return;
-  const int pos = *a.pos;
-  const int total = pos + a.nq;
-  const int nt = cdiv(total, 64);
-  const float* part = a.ws + (int64_t)sh * a.n_wtiles * a.nq * (2 + kHD) + qi * (2 + kHD);
-  const int64_t tstride = (int64_t)a.nq * (2 + kHD);
-  float M = -INFINITY;
-  for (int t = 0; t < nt; ++t) M = fmaxf(M, part[t * tstride]);
-  float L = 0.f, o = 0.f;
-  for (int t = 0; t < nt; ++t) {
-    const float m = part[t * tstride];
-    if (m == -INFINITY) continue;
-    const float w = __expf(m - M);
-    L = fmaf(w, part[t * tstride + 1], L);
-    o = fmaf(w, part[t * tstride + 2 + lane], o);
-  }
+  const int64_t bstride = (int64_t)a.nq * (2 + kHD);
+  const float* part = a.ws + (int64_t)sh * nblk * bstride + qi * (2 + kHD);
+  const float mv = lane < nblk ? part[lane * bstride] : -INFINITY;
+  const float lv = lane < nblk ? part[lane * bstride + 1] : 0.f;
+  const float M = warp_max(mv);
+  const float w = (mv == -INFINITY) ? 0.f : __expf(mv - M);
+  const float L = warp_sum(w * lv);
+  float o = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < nblk; ++b) o = fmaf(__shfl(w, b, 64), part[b * bstride + 2 + lane], o);
   io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
   st_act(ob, lane, o / L);
 }
@@ -198,27 +251,31 @@ void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes,
   SD_LAUNCH_CHECK();
 }
 
-int attn_decode_tiles(int max_keys) { return cdiv(max_keys, 256) * 4; }
+int attn_decode_blocks(int max_keys) { return std::min(cdiv(max_keys, 256), 32); }
+
+template <bool IOBF>
+static void launch_decode(const DecodeAttnArgs& a, int nblk, hipStream_t st) {
+  const int nsh = a.nseq * a.nh;
+  const dim3 g1(nblk, nsh), g2(nsh, cdiv(a.nq, 4));
+  if (a.nq == 1) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 1>), g1, dim3(256), 0, st, a);
+  else if (a.nq <= 8) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 8>), g1, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_decode_kernel<IOBF, 32>), g1, dim3(256), 0, st, a);
+  SD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_combine_kernel<IOBF>, g2, dim3(256), 0, st, a, nblk);
+  SD_LAUNCH_CHECK();
+}
 
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
   SD_CHECK(a.hd == kHD, kErrInvalid, "attn_decode: head dim must be 64");
   SD_CHECK(a.nq >= 1 && a.nq <= kMaxQ, kErrInvalid, "attn_decode: 1..32 queries per sequence");
-  SD_CHECK(a.n_wtiles >= attn_decode_tiles(a.max_keys), kErrInvalid, "attn_decode: workspace too small");
+  const int nblk = attn_decode_blocks(a.max_keys);
+  SD_CHECK(a.n_blocks >= nblk, kErrInvalid, "attn_decode: workspace too small");
   const int nsh = a.nseq * a.nh;
-  // bytes: upper bound (full cache), the graph does not know the cursor
+  // bytes: upper bound (full history), the graph does not know the cursor
   ProfScope prof("attn_decode", 4.0 * a.max_keys * kHD * nsh * a.nq,
                  2.0 * a.max_keys * kHD * nsh * (a.io_bf16 ? 2 : 4), st);
-  const dim3 g1(cdiv(a.max_keys, 256), nsh), g2(nsh, cdiv(a.nq, 4));
-  if (a.io_bf16) {
-    hipLaunchKernelGGL(attn_decode_kernel<true>, g1, dim3(256), 0, st, a);
-    SD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(attn_combine_kernel<true>, g2, dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(attn_decode_kernel<false>, g1, dim3(256), 0, st, a);
-    SD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(attn_combine_kernel<false>, g2, dim3(256), 0, st, a);
-  }
-  SD_LAUNCH_CHECK();
+  if (a.io_bf16) launch_decode<true>(a, nblk, st);
+  else launch_decode<false>(a, nblk, st);
 }
 
 void gather_window(const float* hist, int D, const int* cursor, const int* n_valid, int pad, int rows, float* dst,

@@ -45,7 +45,10 @@ def _rel_err(a, b):
                                        (64, 512, 4, 0), (333, 96, 130, 3), (4096, 256, 2048, 2),
                                        # weight-resident streaming path (bf16 A, K % 64 == 0, M >= 2048):
                                        (20000, 384, 512, 3), (9001, 384, 1152, 0), (7777, 512, 384, 0),
-                                       (5003, 448, 200, 1), (3000, 768, 96, 0), (2048, 64, 130, 2)])
+                                       (5003, 448, 200, 1), (3000, 768, 96, 0), (2048, 64, 130, 2),
+                                       # skinny weight-streaming path (M <= 16, streaming FS-EEND chunks):
+                                       (1, 2048, 256, 0), (6, 256, 2048, 1), (16, 768, 256, 3),
+                                       (12, 352, 256, 0), (3, 4864, 256, 0), (9, 256, 768, 2)])
 def test_linear(gpu, precision, M, K, N, act):
     g = torch.Generator().manual_seed(M * 7 + N)
     x = torch.randn(M, K, generator=g)
@@ -74,6 +77,8 @@ def test_linear(gpu, precision, M, K, N, act):
     (3, 150, 384, 768, 1, 1, 0, 1),    # conformer pointwise
     (2, 50, 64, 130, 3, 1, 1, 1),      # Cin % 64 == 0 multi-tap, N tail
     (2, 299, 136, 32, 1, 1, 0, 1),     # K tail (136 = 2*64 + 8)
+    (1, 19, 256, 256, 19, 1, 0, 1),    # FS-EEND look-ahead conv, streaming window of 1 frame (skinny)
+    (1, 26, 256, 256, 19, 1, 0, 1),    # ... 8 frames
 ])
 def test_conv1d(gpu, precision, B, T, Cin, Cout, k, stride, pad, dil):
     g = torch.Generator().manual_seed(B * T + Cout)
