@@ -32,11 +32,13 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
   F_ = wsb<float>((size_t)c_ * m.in_ld_);
   Y_ = wsb<float>((size_t)c_ * D);
   X_ = wsb<float>((size_t)c_ * D);
+  X2_ = wsb<float>((size_t)c_ * D);
   W_ = wsb<float>((size_t)(c_ + 18) * D);
   Yc_ = wsb<float>((size_t)c_ * D);
   E_ = wsb<float>((size_t)c_ * D);
   G_ = wsb<float>((size_t)c_ * D);
   A_ = wsb<float>((size_t)rd * D);
+  A2_ = wsb<float>((size_t)rd * D);
   P_ = wsb<float>((size_t)rd);
   QKV_ = arena_.alloc(rd * 3 * D * es_);
   AO_ = arena_.alloc(rd * D * es_);
@@ -60,18 +62,72 @@ FsEendStream::~FsEendStream() {
   if (cap_st_) (void)hipStreamDestroy(cap_st_);
 }
 
+namespace {
+
+// Post-LN residual handed to the next GEMM: its A rows are LN(x + t)*g + b, and the result
+// becomes the residual stream `out` (x and out ping-pong).  t == nullptr: plain LN of x.
+struct PendingLn {
+  const float* x = nullptr;
+  const void* t = nullptr;
+  const float* g = nullptr;
+  const float* b = nullptr;
+  float* out = nullptr;
+};
+
+struct KvEpi {
+  void* dst = nullptr;
+  const int* cursor = nullptr;
+  int mult = 1;
+  int64_t ld = 0;   // elements
+};
+
+// Runs p, taking its A rows from `ln` when given and storing columns [D, 3D) to the K|V
+// history when `kv` is given: fused into the skinny kernel when it applies, else
+// add_layernorm / kv_append around a plain GEMM (same results).
+void gemm_fused(ConvGemmArgs p, const PendingLn* ln, const KvEpi* kv, int D, bool bf, hipStream_t st) {
+  const int M = p.B * p.Ho * p.Wo;
+  ConvGemmArgs q = p;
+  if (ln) {
+    q.ln_x = ln->x; q.ln_t = ln->t; q.ln_t_bf16 = bf; q.ln_g = ln->g; q.ln_b = ln->b; q.ln_out = ln->out;
+    q.A = ln->out; q.a_bf16 = false; q.lda = p.K;
+  }
+  if (kv) {
+    q.kv_out = kv->dst; q.kv_cursor = kv->cursor; q.kv_mult = kv->mult; q.kv_col0 = D; q.kv_ld = kv->ld;
+  }
+  if ((ln || kv) && gemm_skinny_supported(q)) {
+    conv_gemm(q, bf, st);
+    return;
+  }
+  if (ln) {
+    if (ln->t) add_layernorm(const_cast<float*>(ln->x), ln->t, bf, M, p.K, ln->g, ln->b, 1e-5f, false, ln->out, false, st);
+    else layernorm(ln->x, M, p.K, p.K, ln->g, ln->b, 1e-5f, ln->out, p.K, false, st);
+    p.A = ln->out; p.a_bf16 = false; p.lda = p.K;
+  }
+  conv_gemm(p, bf, st);
+  if (kv) {
+    const size_t es = bf ? 2 : 4;
+    kv_append(static_cast<char*>(p.out) + D * es, p.o_sw * es, M, 2 * D * es, kv->dst, kv->ld * es, kv->cursor,
+              kv->mult, st);
+  }
+}
+
+}  // namespace
+
 void FsEendStream::enc_chunk(hipStream_t st) {
-  // MaskedTransformerEncoderModel.forward (fs_eend.py:178-204) on the chunk's c rows.
+  // MaskedTransformerEncoderModel.forward (fs_eend.py:178-204) on the chunk's c rows.  Every
+  // post-LN (norm1/norm2, fs_eend.py via nn.TransformerEncoderLayer) is applied while the
+  // next GEMM stages its rows; the K|V halves of the in-projection go straight to the history.
   const FsEendModel& m = m_;
   const int D = m.cfg_.n_units, nh = m.cfg_.n_heads, c = c_;
-  const Tens x{X_, false}, qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
+  const Tens qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
   conv_gemm(lin(Tens{F_, false}, c, m.in_ld_, m.in_.w, m.in_.beta, Tens{Y_, false}, D), bf_, st);
-  layernorm(Y_, c, D, D, m.norm_g_, m.norm_b_, 1e-5f, X_, D, false, st);
+  float* xb[2] = {X_, X2_};
+  int xi = 0;
+  PendingLn ln{Y_, nullptr, m.norm_g_, m.norm_b_, xb[0]};   // encoder_norm (fs_eend.py:197)
   for (size_t l = 0; l < m.enc_.size(); ++l) {
     const TransformerL& L = m.enc_[l];
-    conv_gemm(lin(x, c, D, L.in_proj, L.in_b, qkv, 3 * D), bf_, st);
-    kv_append(static_cast<char*>(QKV_) + D * es_, 3 * D * es_, c, 2 * D * es_, kv_enc_[l], 2 * D * es_, state_, 1,
-              st);
+    const KvEpi kv{kv_enc_[l], state_, 1, 2 * D};
+    gemm_fused(lin(Tens{xb[xi], false}, c, D, L.in_proj, L.in_b, qkv, 3 * D), &ln, &kv, D, bf_, st);
     DecodeAttnArgs a;
     a.q = QKV_; a.q_tok = 3 * D;
     a.k = kv_enc_[l]; a.v = static_cast<char*>(kv_enc_[l]) + D * es_; a.kv_tok = 2 * D;
@@ -80,63 +136,29 @@ void FsEendStream::enc_chunk(hipStream_t st) {
     a.pos = state_; a.delay = 0; a.max_keys = cap_; a.n_blocks = n_blocks_; a.ws = ws_; a.io_bf16 = bf_;
     attn_decode(a, st);
     conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
-    add_layernorm(X_, T_, bf_, c, D, L.n1g, L.n1b, 1e-5f, false, X_, false, st);
-    ConvGemmArgs p = lin(x, c, D, L.l1, L.b1, h, L.l1.N);
+    ln = PendingLn{xb[xi], T_, L.n1g, L.n1b, xb[xi ^ 1]};
+    xi ^= 1;
+    ConvGemmArgs p = lin(Tens{xb[xi], false}, c, D, L.l1, L.b1, h, L.l1.N);
     p.act = kActRelu;
-    conv_gemm(p, bf_, st);
+    gemm_fused(p, &ln, nullptr, D, bf_, st);
     conv_gemm(lin(h, c, L.l1.N, L.l2, L.b2, t, D), bf_, st);
-    add_layernorm(X_, T_, bf_, c, D, L.n2g, L.n2b, 1e-5f, false, X_, false, st);
+    ln = PendingLn{xb[xi], T_, L.n2g, L.n2b, xb[xi ^ 1]};
+    xi ^= 1;
   }
-  kv_append(X_, D * 4, c, D * 4, hist_, D * 4, state_, 1, st);
-  cursor_advance(state_ + 0, c, state_ + 1, st);
-}
-
-void FsEendStream::fusion_step(int app, hipStream_t st) {
-  // TransformerEncoderFusionLayer.forward (fs_eend.py:456-478) on the chunk's (t, slot) rows.
-  const FsEendModel& m = m_;
-  const FusionL& f = m.fus_;
-  const int D = m.cfg_.n_units, nh = m.cfg_.n_heads, C = C_;
-  const int n = c_ * C;
-  const Tens a{A_, false}, qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
-  const float scale = 1.f / std::sqrt((float)(D / nh));
-  // (1) time attention per slot against this application's history (causal)
-  conv_gemm(lin(a, n, D, f.in1, f.in1_b, qkv, 3 * D), bf_, st);
-  kv_append(static_cast<char*>(QKV_) + D * es_, 3 * D * es_, n, 2 * D * es_, kv_dec_[app], 2 * D * es_, state_ + 2,
-            C, st);
-  {
-    DecodeAttnArgs d;
-    d.q = QKV_; d.q_tok = (int64_t)C * 3 * D; d.q_seq = 3 * D;
-    d.k = kv_dec_[app]; d.v = static_cast<char*>(kv_dec_[app]) + D * es_;
-    d.kv_tok = (int64_t)C * 2 * D; d.kv_seq = 2 * D;
-    d.out = AO_; d.o_tok = (int64_t)C * D; d.o_seq = D;
-    d.nseq = C; d.nq = c_; d.nh = nh; d.hd = D / nh; d.scale = scale;
-    d.pos = state_ + 2; d.delay = 0; d.max_keys = cap_; d.n_blocks = n_blocks_; d.ws = ws_; d.io_bf16 = bf_;
-    attn_decode(d, st);
-  }
-  conv_gemm(lin(ao, n, D, f.out1, f.out1_b, t, D), bf_, st);
-  add_layernorm(A_, T_, bf_, n, D, f.n11g, f.n11b, 1e-5f, false, A_, false, st);
-  // (2) attention over the C slots of each frame
-  conv_gemm(lin(a, n, D, f.in2, f.in2_b, qkv, 3 * D), bf_, st);
-  {
-    AttnArgs s;
-    s.qkv = QKV_; s.io_bf16 = bf_; s.S = c_; s.T = C; s.D = D; s.nh = nh; s.ld_qkv = 3 * D;
-    s.out = AO_; s.ldo = D; s.scale = scale;
-    attention(s, bf_, st);
-  }
-  conv_gemm(lin(ao, n, D, f.out2, f.out2_b, t, D), bf_, st);
-  add_layernorm(A_, T_, bf_, n, D, f.n21g, f.n21b, 1e-5f, false, A_, false, st);
-  // (3) feed-forward
-  ConvGemmArgs p = lin(a, n, D, f.l1, f.b1, h, f.l1.N);
-  p.act = kActRelu;
-  conv_gemm(p, bf_, st);
-  conv_gemm(lin(h, n, f.l1.N, f.l2, f.b2, t, D), bf_, st);
-  add_layernorm(A_, T_, bf_, n, D, f.n22g, f.n22b, 1e-5f, false, A_, false, st);
+  // last norm2 -> encoder-output history row, cursor advance (encoder frames and valid frames)
+  stream_enc_finish(ln.x, ln.t, bf_, ln.g, ln.b, 1e-5f, c, D, hist_, state_ + 0, state_ + 1, st);
 }
 
 void FsEendStream::dec_chunk(hipStream_t st) {
-  // fs_eend.py:83-90 for frames [n_dec, n_dec + c): conv window, L2 norm, decoder, scores.
+  // fs_eend.py:83-90 for frames [n_dec, n_dec + c): conv window, L2 norm, decoder
+  // (MaskedTransformerDecoderModel.forward :125-134 with TransformerEncoderFusionLayer
+  // :456-478 applied dec_n_layers times), scores.  Post-LNs fold into the next GEMM.
   const FsEendModel& m = m_;
-  const int D = m.cfg_.n_units, c = c_;
+  const FusionL& f = m.fus_;
+  const int D = m.cfg_.n_units, nh = m.cfg_.n_heads, c = c_, C = C_;
+  const int n = c * C;
+  const Tens qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
+  const float scale = 1.f / std::sqrt((float)(D / nh));
   gather_window(hist_, D, state_ + 2, state_ + 1, 9, c + 18, W_, st);
   {
     ConvGemmArgs p;
@@ -151,10 +173,50 @@ void FsEendStream::dec_chunk(hipStream_t st) {
   }
   row_l2norm(Yc_, c, D, E_, st);
   conv_gemm(lin(Tens{E_, false}, c, D, m.conv_emb_, nullptr, Tens{G_, false}, D), bf_, st);
-  slot_init(G_, c, C_, D, m.slot_bias_, A_, st);
-  for (int i = 0; i < m.cfg_.dec_n_layers; ++i) fusion_step(i, st);
-  slot_scores(E_, A_, c, C_, D, P_, false, st);
-  cursor_advance(state_ + 2, c, nullptr, st);
+  float* ab[2] = {A_, A2_};
+  int ai = 0;
+  slot_init(G_, c, C, D, m.slot_bias_, ab[0], st);
+  PendingLn ln;
+  bool pending = false;
+  for (int app = 0; app < m.cfg_.dec_n_layers; ++app) {
+    // (1) time attention per slot against this application's history (causal)
+    const KvEpi kv{kv_dec_[app], state_ + 2, C, 2 * D};
+    gemm_fused(lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D), pending ? &ln : nullptr, &kv, D, bf_, st);
+    {
+      DecodeAttnArgs d;
+      d.q = QKV_; d.q_tok = (int64_t)C * 3 * D; d.q_seq = 3 * D;
+      d.k = kv_dec_[app]; d.v = static_cast<char*>(kv_dec_[app]) + D * es_;
+      d.kv_tok = (int64_t)C * 2 * D; d.kv_seq = 2 * D;
+      d.out = AO_; d.o_tok = (int64_t)C * D; d.o_seq = D;
+      d.nseq = C; d.nq = c; d.nh = nh; d.hd = D / nh; d.scale = scale;
+      d.pos = state_ + 2; d.delay = 0; d.max_keys = cap_; d.n_blocks = n_blocks_; d.ws = ws_; d.io_bf16 = bf_;
+      attn_decode(d, st);
+    }
+    conv_gemm(lin(ao, n, D, f.out1, f.out1_b, t, D), bf_, st);
+    ln = PendingLn{ab[ai], T_, f.n11g, f.n11b, ab[ai ^ 1]};
+    ai ^= 1;
+    // (2) attention over the C slots of each frame
+    gemm_fused(lin(Tens{ab[ai], false}, n, D, f.in2, f.in2_b, qkv, 3 * D), &ln, nullptr, D, bf_, st);
+    {
+      AttnArgs s;
+      s.qkv = QKV_; s.io_bf16 = bf_; s.S = c; s.T = C; s.D = D; s.nh = nh; s.ld_qkv = 3 * D;
+      s.out = AO_; s.ldo = D; s.scale = scale;
+      attention(s, bf_, st);
+    }
+    conv_gemm(lin(ao, n, D, f.out2, f.out2_b, t, D), bf_, st);
+    ln = PendingLn{ab[ai], T_, f.n21g, f.n21b, ab[ai ^ 1]};
+    ai ^= 1;
+    // (3) feed-forward
+    ConvGemmArgs p = lin(Tens{ab[ai], false}, n, D, f.l1, f.b1, h, f.l1.N);
+    p.act = kActRelu;
+    gemm_fused(p, &ln, nullptr, D, bf_, st);
+    conv_gemm(lin(h, n, f.l1.N, f.l2, f.b2, t, D), bf_, st);
+    ln = PendingLn{ab[ai], T_, f.n22g, f.n22b, ab[ai ^ 1]};
+    ai ^= 1;
+    pending = true;
+  }
+  // last norm22 + slot scores + decoder cursor advance
+  stream_dec_finish(ln.x, ln.t, bf_, ln.g, ln.b, 1e-5f, c, C, D, E_, P_, state_ + 2, st);
 }
 
 void FsEendStream::run(int which, hipStream_t st) {

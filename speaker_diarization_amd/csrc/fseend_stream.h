@@ -36,7 +36,6 @@ class FsEendStream {
  private:
   void enc_chunk(hipStream_t st);
   void dec_chunk(hipStream_t st);
-  void fusion_step(int app, hipStream_t st);
   void run(int which, hipStream_t st);   // 0 encoder, 1 decoder: graph replay or direct launches
   int emit(float* preds, int cap, int rows, hipStream_t st);
   template <typename T>
@@ -54,7 +53,7 @@ class FsEendStream {
   int n_blocks_ = 0;
   // staging (chunk-sized)
   float *F_ = nullptr, *Y_ = nullptr, *X_ = nullptr, *W_ = nullptr, *Yc_ = nullptr, *E_ = nullptr;
-  float *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;
+  float *X2_ = nullptr, *A2_ = nullptr, *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

@@ -63,7 +63,58 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M,
                       : static_cast<const float*>(p.res)[(int64_t)me * p.res_ld + mn];
   }
   const int span = (M - 1) * a_rs + K;
-  if (p.a_bf16) {
+  if (p.ln_g) {
+    // LayerNorm prologue (post-LN residual of the previous sub-block), one wave per row
+    for (int m = wid; m < M; m += 4) {
+      const float* xr = p.ln_x + (int64_t)m * K;
+      float4 v[4];
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = i * 256 + lane * 4;
+        if (c < K) {
+          float4 a = *reinterpret_cast<const float4*>(xr + c);
+          if (p.ln_t) {
+            if (p.ln_t_bf16) {
+              const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.ln_t) + (int64_t)m * K + c);
+              a.x += __uint_as_float(u.x << 16); a.y += __uint_as_float(u.x & 0xffff0000u);
+              a.z += __uint_as_float(u.y << 16); a.w += __uint_as_float(u.y & 0xffff0000u);
+            } else {
+              const float4 u = *reinterpret_cast<const float4*>(static_cast<const float*>(p.ln_t) + (int64_t)m * K + c);
+              a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+            }
+          }
+          v[i] = a;
+          sum += (a.x + a.y) + (a.z + a.w);
+        }
+      }
+      const float mean = warp_sum(sum) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i * 256 + lane * 4 < K) {
+          const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+          q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+        }
+      }
+      const float rstd = rsqrtf(warp_sum(q) / (float)K + p.ln_eps);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = i * 256 + lane * 4;
+        if (c < K) {
+          const float4 gg = *reinterpret_cast<const float4*>(p.ln_g + c);
+          const float4 bb = *reinterpret_cast<const float4*>(p.ln_b + c);
+          float4 y;
+          y.x = (v[i].x - mean) * rstd * gg.x + bb.x;
+          y.y = (v[i].y - mean) * rstd * gg.y + bb.y;
+          y.z = (v[i].z - mean) * rstd * gg.z + bb.z;
+          y.w = (v[i].w - mean) * rstd * gg.w + bb.w;
+          *reinterpret_cast<float4*>(As + m * K + c) = y;
+          if (blockIdx.x == 0) *reinterpret_cast<float4*>(p.ln_out + (int64_t)m * K + c) = y;
+        }
+      }
+    }
+  } else if (p.a_bf16) {
     const uint16_t* a = static_cast<const uint16_t*>(p.A) + p.a_coff;
     for (int i = tid; i < span; i += 256) As[i] = bf_bits2f(a[i]);
   } else {
@@ -144,11 +195,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M,
   const int64_t o = (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw + (int64_t)mn * p.o_sn;
   if (p.out_bf16) static_cast<uint16_t*>(p.out)[o] = f2bf_bits(v);
   else static_cast<float*>(p.out)[o] = v;
+  if (p.kv_out && mn >= p.kv_col0) {
+    const int64_t ko = ((int64_t)(*p.kv_cursor) * p.kv_mult + me) * p.kv_ld + (mn - p.kv_col0);
+    if (p.out_bf16) static_cast<uint16_t*>(p.kv_out)[ko] = f2bf_bits(v);
+    else static_cast<float*>(p.kv_out)[ko] = v;
+  }
 }
 
 // A(m, k) = A[a_coff + m*a_rs + k]: a plain linear (row stride lda), or a stride-1
 // unpadded 1-D conv whose taps are consecutive rows (Cin == lda).
 int skinny_row_stride(const ConvGemmArgs& p) {
+  if (p.ln_g) return p.K;   // LN prologue: dense rows of K built in LDS
   if (a_rows_linear(p)) return p.lda;
   if (p.B == 1 && p.H == 1 && p.Ho == 1 && p.kh == 1 && p.sw == 1 && p.dw == 1 && p.pw == 0 && p.ph == 0 &&
       p.Cin == p.lda && p.W >= p.Wo + p.kw - 1)
@@ -186,6 +243,8 @@ bool gemm_skinny_supported(const ConvGemmArgs& p) {
   const int rs = skinny_row_stride(p);
   if (rs < 0) return false;
   if (((int64_t)(M - 1) * rs + p.K) > kSkinnyLdsFloats) return false;
+  if (p.ln_g && (p.K % 256 != 0 || p.K > 1024 || !p.ln_x || !p.ln_b || !p.ln_out || p.ln_out == p.ln_x))
+    return false;
   return p.a_coff % 4 == 0 && rs % 4 == 0;
 }
 

@@ -33,6 +33,22 @@ struct ConvGemmArgs {
   // GLU epilogue (streaming path only): the N GEMM columns are 32-wide groups [a 16 | gate 16]
   // (weights permuted by glu_interleave_rows); output channel g*16 + j = a * sigmoid(gate), N/2 wide.
   int glu = 0;
+  // Skinny path only (gemm_skinny_supported; streaming FS-EEND).  LayerNorm prologue: the staged
+  // A rows are LN(ln_x + ln_t)*ln_g + ln_b over K (ln_x fp32 rows of K, ln_t fp32/bf16 or null);
+  // workgroup 0 also stores them to ln_out (the next residual stream; must not alias ln_x).
+  const float* ln_x = nullptr;
+  const void* ln_t = nullptr;
+  bool ln_t_bf16 = false;
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 1e-5f;
+  float* ln_out = nullptr;
+  // K/V history epilogue: columns n >= kv_col0 are also stored (out dtype) at
+  // kv_out[(*kv_cursor * kv_mult + m) * kv_ld + n - kv_col0].
+  void* kv_out = nullptr;
+  const int* kv_cursor = nullptr;
+  int kv_mult = 1, kv_col0 = 0;
+  int64_t kv_ld = 0;
 };
 // Row order of a GLU projection (2C, K) -> groups of [16 value rows | their 16 gate rows].
 inline int glu_interleave_row(int r, int C) {   // new row index of original row r
@@ -259,4 +275,12 @@ void gather_window(const float* hist, int D, const int* cursor, const int* n_val
                    hipStream_t st);
 // *cursor += by; mirror (optional) = new value.
 void cursor_advance(int* cursor, int by, int* mirror, hipStream_t st);
+// Encoder chunk tail: v = LN(x + t)*g + b for rows < c (D % 256 == 0, D <= 1024); v -> hist row
+// (*cursor + r); then *cursor += c and *mirror = *cursor.
+void stream_enc_finish(const float* x, const void* t, bool t_bf16, const float* g, const float* b, float eps, int c,
+                       int D, float* hist, int* cursor, int* mirror, hipStream_t st);
+// Decoder chunk tail: a = LN(x + t)*g + b for the c*C (frame, slot) rows, scores[f, s] =
+// emb[f]·a/|a| (fs_eend.py:88-90); then *cursor += c.
+void stream_dec_finish(const float* x, const void* t, bool t_bf16, const float* g, const float* b, float eps, int c,
+                       int C, int D, const float* emb, float* scores, int* cursor, hipStream_t st);
 }  // namespace sd

@@ -226,6 +226,104 @@ __global__ __launch_bounds__(256) void gather_window_kernel(const float* __restr
   }
 }
 
+// One wave per row: v = LN(x + t)*g + b over D (D % 256 == 0, <= 1024); 4 floats per lane per 256.
+__device__ __forceinline__ void ln_row(const float* xr, const void* t, bool t_bf16, int64_t toff, const float* g,
+                                       const float* b, float eps, int D, int lane, float4 (&y)[4]) {
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    if (c < D) {
+      float4 a = *reinterpret_cast<const float4*>(xr + c);
+      if (t) {
+        if (t_bf16) {
+          const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(t) + toff + c);
+          a.x += __uint_as_float(u.x << 16); a.y += __uint_as_float(u.x & 0xffff0000u);
+          a.z += __uint_as_float(u.y << 16); a.w += __uint_as_float(u.y & 0xffff0000u);
+        } else {
+          const float4 u = *reinterpret_cast<const float4*>(static_cast<const float*>(t) + toff + c);
+          a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+        }
+      }
+      y[i] = a;
+      sum += (a.x + a.y) + (a.z + a.w);
+    }
+  }
+  const float mean = warp_sum(sum) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i * 256 + lane * 4 < D) {
+      const float dx = y[i].x - mean, dy = y[i].y - mean, dz = y[i].z - mean, dw = y[i].w - mean;
+      q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    if (c < D) {
+      const float4 gg = *reinterpret_cast<const float4*>(g + c);
+      const float4 bb = *reinterpret_cast<const float4*>(b + c);
+      y[i].x = (y[i].x - mean) * rstd * gg.x + bb.x;
+      y[i].y = (y[i].y - mean) * rstd * gg.y + bb.y;
+      y[i].z = (y[i].z - mean) * rstd * gg.z + bb.z;
+      y[i].w = (y[i].w - mean) * rstd * gg.w + bb.w;
+    }
+  }
+}
+
+// Single workgroup: every wave reads the cursor before the barrier, thread 0 advances it after.
+__global__ __launch_bounds__(256) void enc_finish_kernel(const float* __restrict__ x, const void* t, int t_bf16,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, int c, int D, float* __restrict__ hist,
+                                                         int* cursor, int* mirror) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cur = *cursor;
+  for (int r = wid; r < c; r += 4) {
+    float4 y[4];
+    ln_row(x + (int64_t)r * D, t, t_bf16, (int64_t)r * D, g, b, eps, D, lane, y);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = i * 256 + lane * 4;
+      if (col < D) *reinterpret_cast<float4*>(hist + (int64_t)(cur + r) * D + col) = y[i];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *cursor = cur + c;
+    if (mirror) *mirror = cur + c;
+  }
+}
+
+// One wave per (frame, slot) row; workgroup 0 / thread 0 advances the decoder cursor (no
+// thread of this kernel reads it).
+__global__ __launch_bounds__(256) void dec_finish_kernel(const float* __restrict__ x, const void* t, int t_bf16,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, int c, int C, int D, const float* __restrict__ emb,
+                                                         float* __restrict__ scores, int* cursor) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *cursor += c;
+  if (r >= c * C) return;
+  float4 y[4];
+  ln_row(x + (int64_t)r * D, t, t_bf16, (int64_t)r * D, g, b, eps, D, lane, y);
+  const float* e = emb + (int64_t)(r / C) * D;
+  float dot = 0.f, sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 256 + lane * 4;
+    if (col < D) {
+      const float4 ev = *reinterpret_cast<const float4*>(e + col);
+      dot += (ev.x * y[i].x + ev.y * y[i].y) + (ev.z * y[i].z + ev.w * y[i].w);
+      sq += (y[i].x * y[i].x + y[i].y * y[i].y) + (y[i].z * y[i].z + y[i].w * y[i].w);
+    }
+  }
+  dot = warp_sum(dot);
+  sq = warp_sum(sq);
+  if (lane == 0) scores[r] = dot / sqrtf(sq);
+}
+
 __global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
   if (threadIdx.x == 0) {
     const int v = *cursor + by;
@@ -284,6 +382,24 @@ void gather_window(const float* hist, int D, const int* cursor, const int* n_val
   ProfScope prof("gather_window", 0.0, 8.0 * n, st);
   const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
   hipLaunchKernelGGL(gather_window_kernel, dim3(blocks), dim3(256), 0, st, hist, D, cursor, n_valid, pad, rows, dst);
+  SD_LAUNCH_CHECK();
+}
+
+void stream_enc_finish(const float* x, const void* t, bool t_bf16, const float* g, const float* b, float eps, int c,
+                       int D, float* hist, int* cursor, int* mirror, hipStream_t st) {
+  SD_CHECK(D % 256 == 0 && D <= 1024, kErrInvalid, "stream_enc_finish: D must be 256/512/768/1024");
+  ProfScope prof("stream_finish", 8.0 * c * D, 12.0 * c * D, st);
+  hipLaunchKernelGGL(enc_finish_kernel, dim3(1), dim3(256), 0, st, x, t, (int)t_bf16, g, b, eps, c, D, hist, cursor,
+                     mirror);
+  SD_LAUNCH_CHECK();
+}
+
+void stream_dec_finish(const float* x, const void* t, bool t_bf16, const float* g, const float* b, float eps, int c,
+                       int C, int D, const float* emb, float* scores, int* cursor, hipStream_t st) {
+  SD_CHECK(D % 256 == 0 && D <= 1024, kErrInvalid, "stream_dec_finish: D must be 256/512/768/1024");
+  ProfScope prof("stream_finish", 12.0 * c * C * D, 8.0 * c * C * D, st);
+  hipLaunchKernelGGL(dec_finish_kernel, dim3(cdiv(c * C, 4)), dim3(256), 0, st, x, t, (int)t_bf16, g, b, eps, c, C, D,
+                     emb, scores, cursor);
   SD_LAUNCH_CHECK();
 }
 
