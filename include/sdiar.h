@@ -77,6 +77,31 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_s
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 int sd_tsvad_destroy(sd_tsvad* h);
 
+/* ------------------------------------------------------------------ CAM++ embeddings
+ * Replaces CAMPPlus (egs/alimeeting/ts_vad2/cam_pplus_wespeaker.py:311-399) as the target-speaker
+ * embedding extractor of generate_chunk_speaker_embedding_from_modelscope_for_diarization.py:
+ *   construction  :256-260 (CAMPPLUS_COMMON: feat_dim 80, embedding_size 192)
+ *   forward(x) / forward(x, get_time_out=True)  :264 / cam_pplus_wespeaker.py:388-399
+ * State-dict keys are the standalone module's (head.*, xvector.*). */
+typedef struct sd_campp sd_campp;
+
+typedef struct {
+  int feat_dim;        /* 80 */
+  int embedding_size;  /* 192 (CAMPPLUS_COMMON) / 512 (CAMPPLUS_VOX)                     */
+  int max_batch;       /* workspace: chunks per forward (extract_embed batch_size 96)      */
+  int max_frames;      /* workspace: fbank frames per chunk (598 for 6 s)                  */
+  int precision;       /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA trunk (the pooled head stays fp32) */
+} sd_campp_config;
+
+int sd_campp_create(const sd_campp_config* cfg, sd_campp** out);
+int sd_campp_set_param(sd_campp* h, const char* name, const float* host_data, const int64_t* shape, int ndim);
+int sd_campp_finalize(sd_campp* h);
+/* feats: device (B, T, 80) fbank; emb: device (B, embedding_size) or NULL; time_out: device
+ * (B, (T-1)/2+1, 512) channel-last = xvector[:-2] output transposed, or NULL (one of the two). */
+int sd_campp_forward(sd_campp* h, const float* feats, int B, int T, float* emb, float* time_out, void* stream);
+int64_t sd_campp_device_bytes(const sd_campp* h);
+int sd_campp_destroy(sd_campp* h);
+
 /* ------------------------------------------------------------------ EEND-EDA
  * Replaces TransformerEdaModel (speaker_diarization/eend_eda/models.py:161-347) and
  * EendEdaModel (models.py:466-652) with LstmEncoderDedecoderAttractor
@@ -197,6 +222,11 @@ int sd_eend_features(const float* wav, int64_t n_samples, int frame_size, int fr
  * out: device (n_frames, n_mels), n_frames = 1 + (n_samples - 400) / 160. */
 int sd_fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
                    const float* mel_fb, int n_mels, float* out, void* stream);
+/* Same with the window chosen: window_type 0 hamming (TS-VAD FBank, ts_vad_dataset.py:45-52),
+ * 1 povey (kaldi.fbank's default, used by the embedding extractor's FBank,
+ * generate_chunk_speaker_embedding_from_modelscope_for_diarization.py:317-331, in_scale 1). */
+int sd_fbank_kaldi_ex(const float* wav, int64_t n_samples, float in_scale, int n_frames, const float* mel_fb,
+                      int n_mels, int window_type, float* out, void* stream);
 /* Window slicing + per-window mean normalisation (mean_nor=True, :55) + the
  * collater's zero pad to the batch max (ts_vad_dataset.py:664-701).
  * win_start / win_n: device int32 (n_win). out: device (n_win, T_out, n_mels). */

@@ -29,8 +29,10 @@ def mel_banks(n_mels=80, sr=16000.0, n_fft=512, low=20.0, high=0.0):
     return np.pad(w, ((0, 0), (0, 1)))
 
 
-def fbank(wav, n_mels=80, sr=16000, scale=float(1 << 15), dither=0.0, rng=None):
-    """wav: (N,) float in [-1, 1) -> (1 + (N-400)//160, n_mels) float32."""
+def fbank(wav, n_mels=80, sr=16000, scale=float(1 << 15), dither=0.0, rng=None, window="hamming"):
+    """wav: (N,) float in [-1, 1) -> (1 + (N-400)//160, n_mels) float32.
+    window "povey" (kaldi's default, hann^0.85) is the embedding extractor's
+    (generate_chunk_speaker_embedding_from_modelscope_for_diarization.py:326-327)."""
     x = np.asarray(wav, np.float64) * scale
     fl, fs, nfft = 400, 160, 512
     if len(x) < fl:
@@ -43,11 +45,24 @@ def fbank(wav, n_mels=80, sr=16000, scale=float(1 << 15), dither=0.0, rng=None):
     fr = fr - fr.mean(axis=1, keepdims=True)
     prev = np.concatenate([fr[:, :1], fr[:, :-1]], axis=1)
     fr = fr - 0.97 * prev
-    win = 0.54 - 0.46 * np.cos(2 * math.pi * np.arange(fl) / (fl - 1))
+    cw = np.cos(2 * math.pi * np.arange(fl) / (fl - 1))
+    if window == "hamming":
+        win = 0.54 - 0.46 * cw
+    elif window == "povey":
+        win = (0.5 - 0.5 * cw) ** 0.85
+    else:
+        raise ValueError(f"Invalid window type {window}")
     fr = fr * win
     spec = np.abs(np.fft.rfft(fr, n=nfft, axis=1)) ** 2
     e = spec @ mel_banks(n_mels, sr, nfft).T
     return np.log(np.maximum(e, np.finfo(np.float32).eps)).astype(np.float32)
+
+
+def embed_fbank(wav_slice, n_mels=80):
+    """FBank(80, mean_nor=True)(wav) of the embedding extractor
+    (generate_chunk_..._for_diarization.py:307-331): povey window, dither 0, no 2^15 scale."""
+    f = fbank(wav_slice, n_mels, scale=1.0, window="povey")
+    return (f - f.mean(axis=0, keepdims=True)).astype(np.float32)
 
 
 def window_fbank(wav_slice, n_mels=80):

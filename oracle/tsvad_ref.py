@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -72,6 +73,37 @@ def campplus_time_out(sd, fbank, pre="speech_encoder."):
         # TransitLayer.forward (213-216)
         x = F.conv1d(F.relu(_bn(x, sd, q + "nonlinear.batchnorm")), sd[q + "linear.weight"], sd.get(q + "linear.bias"))
     return F.relu(_bn(x, sd, xv + "out_nonlinear.batchnorm"))
+
+
+def campplus_embedding(sd, fbank, pre=""):
+    """CAMPPlus.forward(x) (get_time_out=False, cam_pplus_wespeaker.py:388-399): xvector[:-2]
+    -> StatsPool (mean, unbiased std over time, :28-39) -> DenseLayer(1024 -> E, batchnorm_)
+    (:219-233).  (B, T, 80) -> (B, E)."""
+    x = campplus_time_out(sd, fbank, pre)
+    stats = torch.cat([x.mean(dim=-1), x.std(dim=-1, unbiased=True)], dim=-1)
+    y = F.conv1d(stats.unsqueeze(-1), sd[pre + "xvector.dense.linear.weight"]).squeeze(-1)
+    return _bn(y, sd, pre + "xvector.dense.nonlinear.batchnorm")
+
+
+def embedding_chunks(n_samples, length_embedding=6.0, step_embedding=1.0, sr=16000):
+    """Chunk plan of extract_embed (generate_chunk_..._for_diarization.py:271-299): starts
+    range(0, N - L, step) when N > L (so a chunk ending exactly at N is never taken), else the
+    whole file as one chunk.  Returns [(start, stop)]."""
+    L, S = int(length_embedding * sr), int(step_embedding * sr)
+    if n_samples > L:
+        return [(s, s + L) for s in range(0, n_samples - L, S)]
+    return [(0, n_samples)]
+
+
+def extract_embed(sd, wav, length_embedding=6.0, step_embedding=1.0, batch_size=96):
+    """extract_embed (:271-304) with FBank(80, mean_nor=True) (:307-331, :336): wav float64
+    in [-1, 1) -> (n_chunks, E) float32 (the tensor torch.save writes, :351)."""
+    from oracle.fbank_ref import embed_fbank
+    feats = [embed_fbank(wav[a:b]) for a, b in embedding_chunks(len(wav), length_embedding, step_embedding)]
+    out = []
+    for i in range(0, len(feats), batch_size):
+        out.append(campplus_embedding(sd, torch.from_numpy(np.stack(feats[i:i + batch_size]))))
+    return torch.cat(out)
 
 
 # ----------------------------------------------------------------------------- encoders

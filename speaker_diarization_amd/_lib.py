@@ -75,6 +75,16 @@ class FseendConfig(ctypes.Structure):
     ]
 
 
+class CamppConfig(ctypes.Structure):
+    _fields_ = [
+        ("feat_dim", c_int),
+        ("embedding_size", c_int),
+        ("max_batch", c_int),
+        ("max_frames", c_int),
+        ("precision", c_int),
+    ]
+
+
 _SIGS = {
     "sd_last_error": (c_char_p, []),
     "sd_version": (c_int, []),
@@ -88,6 +98,12 @@ _SIGS = {
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
+    "sd_campp_create": (c_int, [POINTER(CamppConfig), POINTER(c_void_p)]),
+    "sd_campp_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_campp_finalize": (c_int, [c_void_p]),
+    "sd_campp_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sd_campp_device_bytes": (c_int64, [c_void_p]),
+    "sd_campp_destroy": (c_int, [c_void_p]),
     "sd_eda_create": (c_int, [POINTER(EdaConfig), POINTER(c_void_p)]),
     "sd_eda_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_eda_finalize": (c_int, [c_void_p]),
@@ -113,6 +129,7 @@ _SIGS = {
     "sd_eend_features": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p, c_int, c_void_p]),
     "sd_fbank_kaldi": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "sd_fbank_kaldi_ex": (c_int, [c_void_p, c_int64, c_float, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sd_window_cmn": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sd_overlap_average": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                    c_void_p, c_void_p]),

@@ -14,6 +14,7 @@
 #include "fseend.h"
 #include "fseend_stream.h"
 #include "tsvad.h"
+#include "campp.h"
 
 namespace sd {
 static thread_local std::string g_err;
@@ -27,6 +28,10 @@ struct sd_tsvad {
 
 struct sd_eda {
   std::unique_ptr<sd::EdaModel> model;
+};
+
+struct sd_campp {
+  std::unique_ptr<sd::CamppModel> model;
 };
 
 struct sd_fseend {
@@ -339,6 +344,62 @@ int sd_fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fr
              sd::kErrInvalid, "fbank: n_frames exceeds the samples");
     sd::fbank_kaldi(wav, n_samples, in_scale, n_frames, mel_fb, n_mels, out, S(stream));
   });
+}
+
+int sd_fbank_kaldi_ex(const float* wav, int64_t n_samples, float in_scale, int n_frames, const float* mel_fb,
+                      int n_mels, int window_type, float* out, void* stream) {
+  return guard([&] {
+    SD_CHECK(n_frames >= 0 && (n_frames == 0 || n_samples >= 400 + (int64_t)(n_frames - 1) * 160),
+             sd::kErrInvalid, "fbank: n_frames exceeds the samples");
+    sd::fbank_kaldi(wav, n_samples, in_scale, n_frames, mel_fb, n_mels, out, S(stream), window_type);
+  });
+}
+
+int sd_campp_create(const sd_campp_config* c, sd_campp** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->feat_dim == 80, sd::kErrInvalid, "CAM++ FCM head supports feat_dim 80 only");
+    SD_CHECK(c->embedding_size > 0, sd::kErrInvalid, "embedding_size must be positive");
+    SD_CHECK(c->max_batch > 0 && c->max_frames >= 8, sd::kErrInvalid, "bad workspace sizes");
+    sd::CamppConfig t;
+    t.feat_dim = c->feat_dim;
+    t.embedding_size = c->embedding_size;
+    t.max_batch = c->max_batch;
+    t.max_frames = c->max_frames;
+    t.bf16 = c->precision == 1;
+    auto* h = new sd_campp;
+    h->model.reset(new sd::CamppModel(t));
+    *out = h;
+  });
+}
+
+int sd_campp_set_param(sd_campp* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_campp_finalize(sd_campp* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_campp_forward(sd_campp* h, const float* feats, int B, int T, float* emb, float* time_out, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && feats && (emb || time_out), sd::kErrInvalid, "null argument");
+    h->model->forward(feats, B, T, emb, time_out, S(stream));
+  });
+}
+
+int64_t sd_campp_device_bytes(const sd_campp* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
+
+int sd_campp_destroy(sd_campp* h) {
+  return guard([&] { delete h; });
 }
 
 int sd_window_cmn(const float* feats, int n_mels, const int* win_start, const int* win_n, int n_win,

@@ -3,7 +3,7 @@
 // Semantics follow torchaudio.compliance.kaldi.fbank as called from
 // ts_vad2/ts_vad_dataset.py:39-52 (FBank.__call__): waveform * 2^15, frames of
 // 400 samples every 160 (snip_edges=True), per-frame DC removal, pre-emphasis
-// 0.97 (first sample against itself), symmetric Hamming window, zero pad to 512,
+// 0.97 (first sample against itself), symmetric Hamming (or povey) window, zero pad to 512,
 // |rFFT|^2, HTK-mel triangular banks (host-built, 80 x 257), log(max(e, FLT_EPS)).
 // dither is 0 here: the reference's default dither=1.0 adds fresh noise per
 // call, so parity is defined at dither 0.
@@ -31,7 +31,7 @@ __device__ __forceinline__ int bitrev9(int x) { return __brev((unsigned)x) >> (3
 __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                     float in_scale, int n_frames,
                                                     const float* __restrict__ mel_fb, int n_mels,
-                                                    const float2* __restrict__ twiddle,
+                                                    const float2* __restrict__ twiddle, int window,
                                                     float* __restrict__ out) {
   __shared__ float2 buf[kFramesPerBlock][kNfft];
   __shared__ float pw[kFramesPerBlock][kBins + 3];
@@ -68,7 +68,10 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
     if (n < kFrameLen) {
       float cur = buf[w][n].x;
       float prev = n > 0 ? buf[w][n - 1].x : cur;
-      float win = 0.54f - 0.46f * cospif(2.f * (float)n / (float)(kFrameLen - 1));
+      const float cw = cospif(2.f * (float)n / (float)(kFrameLen - 1));
+      // hamming (ts_vad_dataset.py:50) or povey = hann^0.85 (kaldi default, used by the
+      // embedding extractor, generate_chunk_speaker_embedding_...py:326-327).
+      float win = window == 0 ? 0.54f - 0.46f * cw : powf(0.5f - 0.5f * cw, 0.85f);
       val = (cur - 0.97f * prev) * win;
     }
     y[i] = val;
@@ -116,7 +119,8 @@ float2* g_twiddle = nullptr;
 }  // namespace
 
 void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
-                 const float* mel_fb, int n_mels, float* out, hipStream_t st) {
+                 const float* mel_fb, int n_mels, float* out, hipStream_t st, int window) {
+  SD_CHECK(window == 0 || window == 1, kErrInvalid, "fbank window_type must be hamming (0) or povey (1)");
   if (!g_twiddle) {
     float2 h[kNfft / 2];
     for (int k = 0; k < kNfft / 2; ++k) {
@@ -129,7 +133,7 @@ void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fram
   if (n_frames <= 0) return;
   ProfScope prof("fbank_kaldi", 0.0, 4.0 * ((double)n_frames * kShift + (double)n_frames * n_mels), st);
   hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(n_frames, kFramesPerBlock)), dim3(256), 0, st, wav,
-                     n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, out);
+                     n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, window, out);
   SD_LAUNCH_CHECK();
 }
 

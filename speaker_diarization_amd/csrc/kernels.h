@@ -95,6 +95,11 @@ void fcm_conv1(const float* fbank, int B, int T, int F, const float* w /*32x9*/,
 void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int seg_len,
                  const float* w1, const float* b1, int C1, const float* w2, const float* b2,
                  int C2, float* gate, hipStream_t st);
+// CAM++ out_nonlinear + StatsPool (cam_pplus_wespeaker.py:28-39, 372-379):
+// v = relu(x * s + h) over x (B, T, C) channel-last (C % 64 == 0);
+// stats (B, 2C) = [mean_t v | unbiased std_t v] (nullable); tout (B, T, C) = v (nullable).
+void stats_pool(const void* x, bool x_bf16, int B, int T, int C, const float* s, const float* h,
+                float* stats, float* tout, hipStream_t st);
 
 // ---------------------------------------------------------------- norms
 // y = LN(x) * g + b over the last dim D; rows of x at stride ldx, y at ldy.
@@ -179,7 +184,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
 // pre-emphasis 0.97, hamming, 512-point power spectrum, HTK mel, log(max(.,eps)).
 void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_frames,
                  const float* mel_fb /*n_mels x 257*/, int n_mels, float* out,
-                 hipStream_t st);
+                 hipStream_t st, int window = 0 /*0 hamming, 1 povey*/);
 
 // Per-window CMN + zero pad: out[w, j, :] = feats[start_w + j, :] - mean_w for j < n_w,
 // 0 for n_w <= j < T_out (ts_vad_dataset.py:55 + collater padding :676).

@@ -1,7 +1,7 @@
 // Native TS-VAD inference runner (owns folded weights + workspace).
 #pragma once
 #include <vector>
-#include "encoder.h"
+#include "campp.h"
 
 namespace sd {
 
@@ -22,14 +22,6 @@ struct TsvadConfig {
   int conformer_ffn = 512;
   int conformer_kernel = 31;
   int lstm_hidden = 256;
-};
-
-struct DenseL {
-  ConvL bottleneck;       // nonlinear1 (prologue) -> linear1 (1x1) -> nonlinear2 (epilogue, relu)
-  ConvL local;            // cam_layer.linear_local (k3, dilation)
-  int dil = 1;
-  const float *c1w = nullptr, *c1b = nullptr, *c2w = nullptr, *c2b = nullptr;
-  int c1 = 0, c2 = 0;
 };
 
 class TsvadModel {
@@ -55,15 +47,7 @@ class TsvadModel {
   DeviceArena arena_;
   bool finalized_ = false;
 
-  // CAM++
-  ConvL fcm_conv1_;  // fp32 3x3 Cin=1 weights (32x9) + folded bn
-  struct ResBlock { ConvL c1, c2, sc; bool has_sc; int stride; };
-  std::vector<ResBlock> fcm_blocks_;
-  ConvL fcm_conv2_;
-  ConvL tdnn_;
-  std::vector<std::vector<DenseL>> dense_;
-  std::vector<ConvL> transit_;
-  const float *out_nl_s_ = nullptr, *out_nl_h_ = nullptr;
+  CamTrunk cam_;     // speech_encoder.* (CAM++ get_time_out=True)
   ConvL down_;
   const float *gsp_w_ = nullptr, *gsp_b_ = nullptr;
   const float* pe_ = nullptr;
@@ -77,8 +61,6 @@ class TsvadModel {
   ConvL fc_;
 
   // Workspace.
-  float *fcmA_ = nullptr, *fcmB_ = nullptr, *fcmC_ = nullptr, *x0_ = nullptr;
-  float *d_[3] = {nullptr, nullptr, nullptr}, *x4_ = nullptr, *tmp_ = nullptr, *gate_ = nullptr;
   float *mix_ = nullptr, *mixg_ = nullptr;
   float *X_ = nullptr, *Y_ = nullptr, *QKV_ = nullptr, *AO_ = nullptr, *H_ = nullptr;
   float *X2_ = nullptr, *partial_ = nullptr, *lstm_work_ = nullptr;

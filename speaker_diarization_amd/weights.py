@@ -75,9 +75,10 @@ def _bn(keys: list, prefix: str, c: int, affine: bool = True):
     keys.append((prefix + ".num_batches_tracked", (), "nbt"))
 
 
-def campplus_layout(prefix: str = "speech_encoder.") -> list:
+def campplus_layout(prefix: str = "speech_encoder.", embedding_size: int = 192) -> list:
     """Key layout of CAMPPlus(feat_dim=80, embedding_size=192)
-    (cam_pplus_wespeaker.py:311-386)."""
+    (cam_pplus_wespeaker.py:311-386).  prefix "" is the standalone embedding
+    extractor (generate_chunk_speaker_embedding_from_modelscope_for_diarization.py:60-66)."""
     k: list = []
     p = prefix + "head."
     k.append((p + "conv1.weight", (32, 1, 3, 3), "conv2d"))
@@ -115,8 +116,8 @@ def campplus_layout(prefix: str = "speech_encoder.") -> list:
         k.append((f"{x}transit{b + 1}.linear.weight", (ch // 2, ch, 1), "kaiming"))
         ch //= 2
     _bn(k, x + "out_nonlinear.batchnorm", ch)
-    k.append((x + "dense.linear.weight", (192, ch * 2, 1), "kaiming"))
-    _bn(k, x + "dense.nonlinear.batchnorm", 192, affine=False)
+    k.append((x + "dense.linear.weight", (embedding_size, ch * 2, 1), "kaiming"))
+    _bn(k, x + "dense.nonlinear.batchnorm", embedding_size, affine=False)
     return k
 
 
@@ -261,6 +262,11 @@ def synthetic_state_dict(layout: list, seed: int = 777, extras: Dict[str, np.nda
 
 def tsvad_state_dict(cfg: TSVADConfig, seed: int = 777):
     return synthetic_state_dict(tsvad_layout(cfg), seed)
+
+
+def campplus_state_dict(seed: int = 777, embedding_size: int = 192):
+    """Seeded weights for a standalone CAMPPlus (keys head.*, xvector.*)."""
+    return synthetic_state_dict(campplus_layout("", embedding_size), seed)
 
 
 def to_torch(sd):

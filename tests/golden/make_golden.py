@@ -98,6 +98,115 @@ def make_tsvad(name):
         sys.modules.pop(mod, None)
 
 
+# ----------------------------------------------------------------------------- CAM++ embeddings
+CAMPP_CASES = {
+    # name: (B, T_fbank, embedding_size, input seed, weight seed)
+    "campp_emb": (3, 598, 192, 51, 801),
+    "campp_emb_vox": (2, 200, 512, 52, 802),
+}
+# extract_embed over whole wav files: (seconds per file, batch_size, wav seed, weight seed)
+CAMPP_EXTRACT = {"campp_extract": ([9.5, 4.0], 3, 53, 803)}
+
+
+def campp_inputs(B, T, seed):
+    return np.random.default_rng(seed).standard_normal((B, T, 80)).astype(np.float32)
+
+
+def _import_campp():
+    install_stubs()
+    d = os.path.join(REF, "egs/alimeeting/ts_vad2")
+    if d not in sys.path:
+        sys.path.insert(0, d)
+    import cam_pplus_wespeaker as C  # reference CAMPPlus
+    return C
+
+
+def make_campp(name):
+    import torch
+    from speaker_diarization_amd.weights import campplus_state_dict, to_torch
+    B, T, E, iseed, wseed = CAMPP_CASES[name]
+    C = _import_campp()
+    torch.manual_seed(0)
+    m = C.CAMPPlus(feat_dim=80, embedding_size=E)
+    m.eval()
+    m.load_state_dict(to_torch(campplus_state_dict(wseed, E)), strict=True)
+    x = torch.from_numpy(campp_inputs(B, T, iseed))
+    with torch.no_grad():
+        emb = m(x)
+        tout = m(x, get_time_out=True)
+    # time_out (B, 512, T'): the first 64 frames keep the fixture small
+    out = dict(emb=emb.numpy().astype(np.float32), time_out=tout[:, :, :64].numpy().astype(np.float32))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, {k: v.shape for k, v in out.items()})
+
+
+def embed_wav(seconds, seed, sr=16000):
+    """int16-valued speech-like noise (what soundfile returns for a 16-bit wav)."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * sr)
+    env = 0.3 + 0.7 * np.abs(np.sin(np.arange(n) / sr * 2.1))
+    return (np.round(rng.standard_normal(n) * 2500 * env).clip(-32768, 32767) / 32768.0).astype(np.float64)
+
+
+def make_campp_extract(name):
+    """Runs the reference extract_embed (generate_chunk_..._for_diarization.py:271-304) on
+    wav files written to a temp dir, with the downloaded model replaced by the seeded
+    CAMPPlus and kaldi.fbank by the restated oracle (torchaudio is absent: unpinned)."""
+    import tempfile
+    import wave as wave_mod
+    import torch
+    from oracle import fbank_ref
+    from speaker_diarization_amd.weights import campplus_state_dict, to_torch
+    secs, bs, wseed_wav, wseed = CAMPP_EXTRACT[name]
+    C = _import_campp()
+
+    def kaldi_fbank(waveform, num_mel_bins=23, sample_frequency=16000.0, dither=0.0, window_type="povey", **kw):
+        assert dither == 0.0 and not kw, kw
+        x = waveform[0].numpy().astype(np.float64)
+        return torch.from_numpy(fbank_ref.fbank(x, num_mel_bins, int(sample_frequency), scale=1.0,
+                                                window=window_type))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kaldi_fbank
+
+    def sf_read(path, start=0, stop=None):
+        with wave_mod.open(path, "rb") as w:
+            a = np.frombuffer(w.readframes(w.getnframes()), np.int16).astype(np.float64) / 32768.0
+        return a[start:stop], 16000
+
+    sys.modules["soundfile"].read = sf_read
+    for n in ("modelscope", "modelscope.hub", "modelscope.hub.snapshot_download"):
+        _stub(n, snapshot_download=None)
+    import generate_chunk_speaker_embedding_from_modelscope_for_diarization as G
+    torch.manual_seed(0)
+    m = C.CAMPPlus(feat_dim=80, embedding_size=192)
+    m.eval()
+    m.load_state_dict(to_torch(campplus_state_dict(wseed, 192)), strict=True)
+    batches = []
+
+    def extract_embeddings(args, batch):     # :215-268 minus the download
+        batches.append(len(batch))
+        with torch.no_grad():
+            return m(torch.stack(batch)).detach()
+
+    G.extract_embeddings = extract_embeddings
+    args = types.SimpleNamespace(length_embedding=6, step_embedding=1, batch_size=bs)
+    fe = G.FBank(80, sample_rate=16000, mean_nor=True)
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for i, s in enumerate(secs):
+            wav = embed_wav(s, wseed_wav + i)
+            path = os.path.join(td, f"spk{i}.wav")
+            with wave_mod.open(path, "wb") as w:
+                w.setnchannels(1)
+                w.setsampwidth(2)
+                w.setframerate(16000)
+                w.writeframes(np.round(wav * 32768).astype(np.int16).tobytes())
+            out[f"emb{i}"] = G.extract_embed(args, path, fe).numpy().astype(np.float32)
+    out["batches"] = np.array(batches, np.int64)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, {k: v.shape for k, v in out.items()}, batches)
+
+
 # ----------------------------------------------------------------------------- EEND-EDA
 EDA_CASES = {
     # name: (model_type, n_layers, chunk lengths, infer_num_speakers, input seed, weight seed)
@@ -310,10 +419,14 @@ if __name__ == "__main__":
     import torch
     torch.set_num_threads(8)
     names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES)
-                             + list(FSEEND_CASES) + list(EEND_CASES))
+                             + list(FSEEND_CASES) + list(EEND_CASES) + list(CAMPP_CASES) + list(CAMPP_EXTRACT))
     for n in names:
         if n in TSVAD_CASES:
             make_tsvad(n)
+        elif n in CAMPP_CASES:
+            make_campp(n)
+        elif n in CAMPP_EXTRACT:
+            make_campp_extract(n)
         elif n in EDA_CASES:
             make_eda(n)
         elif n == "eda_tfm_batch":
