@@ -40,6 +40,10 @@ WORKLOADS = {
     "c5": dict(kind="fseend", n_spk=3, minutes=10.0,
                desc="C5: 8 kHz recording, FS-EEND (4-layer causal encoder, shared 2x fusion decoder, "
                     "logmel23, 100 ms frames), whole recording per test() call; replicas only"),
+    "emb": dict(kind="embed", n_spk=4, minutes=10.0,
+                desc="Target-speaker embeddings: CAM++ (CAMPPLUS_COMMON, 192-d) over 4 speakers' enrollment "
+                     "audio (2.5 min each, 16 kHz), extract_embed 6 s chunks every 1 s, batch 96 "
+                     "(generate_chunk_speaker_embedding_from_modelscope_for_diarization.py); replicas only"),
     "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
                 desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
                      "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
@@ -84,12 +88,39 @@ def cpu_baseline(cfg, sd_np, meeting, ts, target_s):
     n = int(max(probe, min(256, target_s / max(per_win, 1e-6))))
     n = max(probe, (n // probe) * probe)
     t0 = time.perf_counter()
-    meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=min(64, n), max_windows=n)
+    post = meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=min(64, n), max_windows=n)
     dt = time.perf_counter() - t0
     frames = n * 100 * 1   # each window advances the meeting by segment_shift (1 s) = 100 frames
     return dict(value=frames / dt, unit="frames/s", cores=threads, kind="port",
                 sample=f"first {n} windows ({n} s of meeting, fp32, batch {min(64, n)}) of the same meeting "
-                       f"through oracle/pipeline_ref.py on {threads} host threads: {dt:.1f} s")
+                       f"through oracle/pipeline_ref.py on {threads} host threads: {dt:.1f} s"), post, n
+
+
+def der_parity(meeting, gpu_post, cpu_post, span_s, n_real=4, label_rate=25):
+    """The '+ DER' half of the metric: md-eval DER (collar 0.25, ts_vad2/infer.py:136-151) of the
+    GPU path and of the CPU reference path over the same span (the first span_s seconds, which
+    every window of the CPU sample covers exactly as in the full plan), against the synthetic
+    meeting's reference RTTM, at the recipe's thresholds."""
+    from oracle.postprocess_ref import rttm_lines
+    from speaker_diarization_amd import der as der_mod
+    from speaker_diarization_amd.ts_vad.postprocess import THRESHOLDS, posteriors_to_rttm_gpu
+    T = int(span_s * label_rate)
+    keys = [f"{meeting.name}-{i + 1}" for i in range(n_real)]
+    gpu_rttm = posteriors_to_rttm_gpu(keys, gpu_post[:n_real, :T])
+    cpu_rttm = rttm_lines({k: cpu_post[i, :T] for i, k in enumerate(keys)})
+    ref = [f"SPEAKER {meeting.name} 1 {s:.3f} {min(e, span_s) - s:.3f} <NA> <NA> {spk + 1} <NA> <NA>\n"
+           for spk, s, e in sorted(meeting.segments, key=lambda x: (x[1], x[0])) if s < span_s]
+    ref = der_mod.read_rttm(ref)
+    table = {}
+    for thr in THRESHOLDS:
+        g = der_mod.md_eval(ref, der_mod.read_rttm(gpu_rttm[thr]), collar=0.25).der
+        c = der_mod.md_eval(ref, der_mod.read_rttm(cpu_rttm[thr]), collar=0.25).der
+        table[thr] = (round(g, 2), round(c, 2))
+    diffs = [abs(g - c) for g, c in table.values()]
+    return {"span_s": span_s, "collar": 0.25, "threshold": 0.5, "gpu": table[0.5][0], "cpu_reference": table[0.5][1],
+            "max_abs_diff_over_thresholds": round(max(diffs), 3),
+            "per_threshold_gpu_cpu": {str(k): v for k, v in table.items()},
+            "note": "seeded random weights: absolute DER is meaningless, the GPU-vs-reference difference is the check"}
 
 
 def main():
@@ -187,9 +218,10 @@ def main():
             except Exception:
                 pass
 
-    cpu = None
+    cpu, der = None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, sd_np, meeting, ts_np, a.cpu_seconds)
+        cpu, cpu_post, n_cpu = cpu_baseline(cfg, sd_np, meeting, ts_np, a.cpu_seconds)
+        der = der_parity(meeting, post, cpu_post, float(n_cpu))
 
     if rank == 0:
         line = {
@@ -213,6 +245,7 @@ def main():
                        "parallelism": f"window-shard x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "der": der,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
@@ -268,6 +301,18 @@ def main_eend(a, wl):
                 # the device forward of every chunk has completed either way
                 return None
         frames = meeting.wav.size // 160
+    elif kind == "embed":
+        from speaker_diarization_amd.ts_vad.embedding import CAMPPlus, extract_embed
+        from speaker_diarization_amd.weights import campplus_state_dict, to_torch
+        per = minutes * 60.0 / wl["n_spk"]
+        wavs = [torch.from_numpy(make_meeting(per, n_spk=1, seed=900 + 10 * rank + i).wav.astype(np.float32)).to(dev)
+                for i in range(wl["n_spk"])]
+        m = CAMPPlus(feat_dim=80, embedding_size=192, device=dev, precision=prec, max_batch=96)
+        m.load_state_dict(to_torch(campplus_state_dict(777, 192)))
+
+        def step():
+            return [extract_embed(w, m, batch_size=96) for w in wavs]
+        frames = sum(w.numel() for w in wavs) // 160 * world
     else:
         from speaker_diarization_amd.feature import eend_features
         from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
@@ -448,7 +493,7 @@ if __name__ == "__main__":
     _a = parse()
     if WORKLOADS[_a.workload].get("kind") == "fseend_stream":
         main_stream(_a, WORKLOADS[_a.workload])
-    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend"):
+    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend", "embed"):
         main_eend(_a, WORKLOADS[_a.workload])
     else:
         main()

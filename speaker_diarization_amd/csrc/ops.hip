@@ -166,6 +166,95 @@ __global__ __launch_bounds__(256) void cam_context_kernel(
   }
 }
 
+
+// Segment-parallel variant: one workgroup per (segment, batch item), so a batch of B
+// items launches B * nseg workgroups instead of B (the per-item kernel above left most
+// CUs idle at the embedding extractor's B = 96 and ran latency-bound).  Each workgroup
+// streams all T rows once with 8/16-B loads (4 channels per lane, 256/(C/4) rows in
+// flight), accumulating the whole-sequence sum and its own segment's sum in the same
+// pass, then evaluates its segment's context MLP straight from the (L2-resident)
+// weights with shuffle-reduced dot products.
+template <bool XBF, int C, int C1, int C2>
+__global__ __launch_bounds__(256) void cam_context_seg_kernel(
+    const void* __restrict__ xv, int T, int ldx, int seg_len,
+    const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ gate) {
+  constexpr int L = C / 4;          // lanes per row
+  constexpr int P = 256 / L;        // rows in flight
+  constexpr int G1 = 256 / C1;      // threads per first-layer output
+  constexpr int G2 = 256 / C2;
+  static_assert(C % 4 == 0 && 256 % L == 0 && 256 % C1 == 0 && 256 % C2 == 0, "cam_context_seg shape");
+  static_assert(C % G1 == 0 && C1 % G2 == 0 && G1 <= 64 && G2 <= 64, "cam_context_seg split");
+  __shared__ float4 red_t[P][L];
+  __shared__ float4 red_s[P][L];
+  __shared__ float ctx[C];
+  __shared__ float h1[C1];
+  const int s = blockIdx.x, b = blockIdx.y, nseg = gridDim.x;
+  const int tid = threadIdx.x;
+  const int part = tid / L, l = tid % L;
+  const int t0 = s * seg_len, t1 = min(T, t0 + seg_len);
+  float4 at = make_float4(0.f, 0.f, 0.f, 0.f), as = at;
+  auto load = [&](int t) -> float4 {
+    const int64_t o = ((int64_t)b * T + t) * ldx + 4 * l;
+    if constexpr (XBF) {
+      const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(xv) + o);
+      return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                         __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(xv) + o);
+    }
+  };
+  auto acc = [&](int t, const float4& v) {
+    at.x += v.x; at.y += v.y; at.z += v.z; at.w += v.w;
+    if (t >= t0 && t < t1) { as.x += v.x; as.y += v.y; as.z += v.z; as.w += v.w; }
+  };
+  int t = part;
+  for (; t + 3 * P < T; t += 4 * P) {    // four rows in flight per lane
+    const float4 v0 = load(t), v1 = load(t + P), v2 = load(t + 2 * P), v3 = load(t + 3 * P);
+    acc(t, v0); acc(t + P, v1); acc(t + 2 * P, v2); acc(t + 3 * P, v3);
+  }
+  for (; t < T; t += P) acc(t, load(t));
+  red_t[part][l] = at;
+  red_s[part][l] = as;
+  __syncthreads();
+  if (tid < C) {
+    const int ll = tid / 4, k = tid % 4;
+    float tt = 0.f, ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const float* a = reinterpret_cast<const float*>(&red_t[q][ll]);
+      const float* z = reinterpret_cast<const float*>(&red_s[q][ll]);
+      tt += a[k];
+      ss += z[k];
+    }
+    ctx[tid] = tt / (float)T + ss / (float)(t1 - t0);
+  }
+  __syncthreads();
+  {
+    const int j = tid / G1, q = tid % G1;
+    constexpr int KC = C / G1;
+    const float* wr = w1 + (int64_t)j * C + q * KC;
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) a = fmaf(wr[k], ctx[q * KC + k], a);
+#pragma unroll
+    for (int o = G1 / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (q == 0) h1[j] = fmaxf(a + b1[j], 0.f);
+  }
+  __syncthreads();
+  {
+    const int j = tid / G2, q = tid % G2;
+    constexpr int KC = C1 / G2;
+    const float* wr = w2 + (int64_t)j * C1 + q * KC;
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) a = fmaf(wr[k], h1[q * KC + k], a);
+#pragma unroll
+    for (int o = G2 / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (q == 0) gate[((int64_t)b * nseg + s) * C2 + j] = 1.f / (1.f + expf(-(a + b2[j])));
+  }
+}
+
 void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int seg_len, const float* w1,
                  const float* b1, int C1, const float* w2, const float* b2, int C2, float* gate,
                  hipStream_t st) {
@@ -176,6 +265,18 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
   const size_t smem = sizeof(float) * ((256 / C) * nseg * C + nseg * C + nseg * C1 + C1 * (C + 1) +
                                        C2 * (C1 + 1));
   ProfScope prof("cam_context", 2.0 * B * nseg * (C * C1 + C1 * C2), (x_bf16 ? 2.0 : 4.0) * B * T * C, st);
+  const uintptr_t align = x_bf16 ? 8 : 16;
+  if (C == 128 && C1 == 64 && C2 == 32 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % align == 0) {
+    // CAM++ dense layers (bn_channels 128, reduction 2, growth 32)
+    if (x_bf16)
+      hipLaunchKernelGGL((cam_context_seg_kernel<true, 128, 64, 32>), dim3(nseg, B), dim3(256), 0, st, x, T, ldx,
+                         seg_len, w1, b1, w2, b2, gate);
+    else
+      hipLaunchKernelGGL((cam_context_seg_kernel<false, 128, 64, 32>), dim3(nseg, B), dim3(256), 0, st, x, T, ldx,
+                         seg_len, w1, b1, w2, b2, gate);
+    SD_LAUNCH_CHECK();
+    return;
+  }
   if (x_bf16)
     hipLaunchKernelGGL(cam_context_kernel<true>, dim3(B), dim3(256), smem, st, x, T, C, ldx, seg_len, w1,
                        b1, C1, w2, b2, C2, gate);
