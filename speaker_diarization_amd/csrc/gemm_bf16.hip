@@ -298,6 +298,14 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st) {
     conv_fcm3x3(p, st);
     return;
   }
+  if (gemm_areg_supported(p)) {     // A read once, weights streamed (gemm_areg.hip)
+    conv_gemm_areg(p, st);
+    return;
+  }
+  if (p.K > 384 && p.N >= 256 && gemm_ring_supported(p)) {   // stream would split N into 64-col panels
+    conv_gemm_ring(p, st);
+    return;
+  }
   if (gemm_stream_supported(p)) {   // weight-resident streaming path (gemm_stream.hip)
     conv_gemm_stream(p, st);
     return;

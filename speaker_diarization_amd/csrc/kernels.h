@@ -66,6 +66,8 @@ void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
 bool fcm_conv_supported(const ConvGemmArgs& p);               // bf16 3x3 32->32, pad 1, freq stride 1|2
 void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
+bool gemm_areg_supported(const ConvGemmArgs& p);             // bf16 A linear, K in {192,256,384}, N % 64 == 0, N >= 768
+void conv_gemm_areg(const ConvGemmArgs& p, hipStream_t st);
 bool gemm_skinny_supported(const ConvGemmArgs& p);            // <= 16 rows, linear or stride-1 1-D conv
 void conv_gemm_skinny(const ConvGemmArgs& p, bool w_bf16, hipStream_t st);
 

@@ -91,3 +91,22 @@ def test_pipeline_vs_oracle(gpu, variant, precision):
     err = np.abs(post[:3] - ref[:3]).max()
     print(f"pipeline v{variant} {precision}: max|post diff| = {err:.3e}")
     assert err < (1e-3 if precision == "fp32" else 2e-2)
+
+
+def test_tsvad_v1_large_batch_uses_wide_gemm_paths(gpu):
+    """B = 40 windows x 4 speakers x 150 frames = 24000 conformer rows: the size at which the
+    production GEMM paths take over (gemm_areg for the QKV / GLU-pw1 projections, the ring GEMM
+    for the K = 512 FFN output, gemm_stream for the rest).  bf16 logits vs the fp32 CPU oracle."""
+    from oracle.tsvad_ref import tsvad_forward
+    cfg = _cfg(1, 6)
+    sd = to_torch(tsvad_state_dict(cfg, seed=31))
+    B = 40
+    x, ts = tsvad_inputs(B, 598, 150, seed=32)
+    m = TSVADModel(cfg, device=gpu, precision="bf16", max_batch=B)
+    m.load_state_dict(sd)
+    out = m.forward(torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu), 150).cpu().numpy()
+    with torch.no_grad():
+        ref = tsvad_forward(sd, cfg, torch.from_numpy(x), torch.from_numpy(ts), 150).numpy()
+    err = np.abs(out - ref).max()
+    print(f"B={B} bf16: max|logit diff| = {err:.3e}")
+    assert err < BF16_ATOL
