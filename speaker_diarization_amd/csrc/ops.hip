@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void cam_context_kernel(
 // weights with shuffle-reduced dot products.
 template <bool XBF, int C, int C1, int C2>
 __global__ __launch_bounds__(256) void cam_context_seg_kernel(
-    const void* __restrict__ xv, int T, int ldx, int seg_len,
+    const void* __restrict__ xv, int T, int ldx, int seg_len, int nseg_arg,
     const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ gate) {
   constexpr int L = C / 4;          // lanes per row
@@ -189,7 +189,11 @@ __global__ __launch_bounds__(256) void cam_context_seg_kernel(
   __shared__ float4 red_s[P][L];
   __shared__ float ctx[C];
   __shared__ float h1[C1];
-  const int s = blockIdx.x, b = blockIdx.y, nseg = gridDim.x;
+  // 1-D grid, remapped so the nseg workgroups of one item are consecutive logical ids on one
+  // XCD: the item's rows are fetched into that XCD's L2 once instead of once per segment.
+  const int nseg = nseg_arg;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = lid / nseg, s = lid - b * nseg;
   const int tid = threadIdx.x;
   const int part = tid / L, l = tid % L;
   const int t0 = s * seg_len, t1 = min(T, t0 + seg_len);
@@ -269,11 +273,11 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
   if (C == 128 && C1 == 64 && C2 == 32 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % align == 0) {
     // CAM++ dense layers (bn_channels 128, reduction 2, growth 32)
     if (x_bf16)
-      hipLaunchKernelGGL((cam_context_seg_kernel<true, 128, 64, 32>), dim3(nseg, B), dim3(256), 0, st, x, T, ldx,
-                         seg_len, w1, b1, w2, b2, gate);
+      hipLaunchKernelGGL((cam_context_seg_kernel<true, 128, 64, 32>), dim3(nseg * B), dim3(256), 0, st, x, T, ldx,
+                         seg_len, nseg, w1, b1, w2, b2, gate);
     else
-      hipLaunchKernelGGL((cam_context_seg_kernel<false, 128, 64, 32>), dim3(nseg, B), dim3(256), 0, st, x, T, ldx,
-                         seg_len, w1, b1, w2, b2, gate);
+      hipLaunchKernelGGL((cam_context_seg_kernel<false, 128, 64, 32>), dim3(nseg * B), dim3(256), 0, st, x, T, ldx,
+                         seg_len, nseg, w1, b1, w2, b2, gate);
     SD_LAUNCH_CHECK();
     return;
   }
