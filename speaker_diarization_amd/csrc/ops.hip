@@ -597,8 +597,15 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
                                                          act_t<BF>* __restrict__ y,
                                                          float* __restrict__ partial, int fused_silu,
                                                          int glu_in) {
-  __shared__ float g[(kDwTT + kDwMaxK - 1) * kDwCB];
+  // bf16 mode stages bf16 (the activations already are), so a whole 150-frame conformer
+  // sequence (+ halo) fits one stage in 24 KiB: every global load of the block is in flight
+  // at once instead of one latency per 64-frame tile.
+  constexpr int TT = BF ? 160 : kDwTT;
+  __shared__ act_t<BF> g[(TT + kDwMaxK - 1) * kDwCB];
   __shared__ float red[2][256];
+  // bf16 mode: each wave's run of kDwR output rows is transposed through LDS so the stores
+  // leave as 16-B lanes (8 rows x 128 B per wave-instruction) instead of 2-B lanes.
+  __shared__ uint16_t otile[BF ? 4 : 1][kDwR * kDwCB];
   const int pad = (k - 1) / 2;
   const int s = blockIdx.y;
   const int c0 = blockIdx.x * kDwCB;
@@ -614,29 +621,15 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
   float lsum = 0.f, lsq = 0.f;
   constexpr int VEC = BF ? 8 : 4;             // elements per 16-B load
   constexpr int CPR = kDwCB / VEC;            // vector chunks per row
-  for (int t0 = 0; t0 < T; t0 += kDwTT) {
-    const int span = min(kDwTT, T - t0) + k - 1;
+  for (int t0 = 0; t0 < T; t0 += TT) {
+    const int span = min(TT, T - t0) + k - 1;
     __syncthreads();
     for (int i = threadIdx.x; i < span * CPR; i += blockDim.x) {
       const int tt = i / CPR, ch = (i % CPR) * VEC;
       const int t = t0 - pad + tt;
-      float v[VEC];
-#pragma unroll
-      for (int u = 0; u < VEC; ++u) v[u] = 0.f;
+      uint4 out = {0u, 0u, 0u, 0u};            // VEC elements of act_t<BF>
       if (t >= 0 && t < T && c0 + ch < C && !glu_in) {
-        const act_t<BF>* ra = xs + (int64_t)t * C + c0 + ch;   // already gated (GLU epilogue of pw1)
-        if constexpr (BF) {
-          const uint4 a4 = *reinterpret_cast<const uint4*>(ra);
-          const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            v[2 * u] = __uint_as_float(aw[u] << 16);
-            v[2 * u + 1] = __uint_as_float(aw[u] & 0xffff0000u);
-          }
-        } else {
-          const float4 a4 = *reinterpret_cast<const float4*>(ra);
-          v[0] = a4.x; v[1] = a4.y; v[2] = a4.z; v[3] = a4.w;
-        }
+        out = *reinterpret_cast<const uint4*>(xs + (int64_t)t * C + c0 + ch);   // already gated (pw1 GLU epilogue)
       } else if (t >= 0 && t < T && c0 + ch < C) {
         // pw1 rows interleaved in 32-column groups [16 values | 16 gates] (glu_interleave_row)
         const int cc = c0 + ch;
@@ -645,32 +638,30 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
           const uint4 a4 = *reinterpret_cast<const uint4*>(ra);
           const uint4 g4 = *reinterpret_cast<const uint4*>(ra + 16);
           const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w}, gw[4] = {g4.x, g4.y, g4.z, g4.w};
+          uint32_t o[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float a0 = __uint_as_float(aw[u] << 16), a1 = __uint_as_float(aw[u] & 0xffff0000u);
             const float g0 = __uint_as_float(gw[u] << 16), g1 = __uint_as_float(gw[u] & 0xffff0000u);
-            v[2 * u] = a0 / (1.f + __expf(-g0));
-            v[2 * u + 1] = a1 / (1.f + __expf(-g1));
+            o[u] = pack_bf16x2(a0 / (1.f + __expf(-g0)), a1 / (1.f + __expf(-g1)));
           }
+          out = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
           const float4 a4 = *reinterpret_cast<const float4*>(ra);
           const float4 g4 = *reinterpret_cast<const float4*>(ra + 16);
-          v[0] = a4.x / (1.f + __expf(-g4.x));
-          v[1] = a4.y / (1.f + __expf(-g4.y));
-          v[2] = a4.z / (1.f + __expf(-g4.z));
-          v[3] = a4.w / (1.f + __expf(-g4.w));
+          out = make_uint4(__float_as_uint(a4.x / (1.f + __expf(-g4.x))), __float_as_uint(a4.y / (1.f + __expf(-g4.y))),
+                           __float_as_uint(a4.z / (1.f + __expf(-g4.z))), __float_as_uint(a4.w / (1.f + __expf(-g4.w))));
         }
       }
-      float* dst = g + tt * kDwCB + ch;
-#pragma unroll
-      for (int u = 0; u < VEC; u += 4) *reinterpret_cast<float4*>(dst + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
+      *reinterpret_cast<uint4*>(g + tt * kDwCB + ch) = out;
     }
     __syncthreads();
-    const int nout = min(kDwTT, T - t0);
+    const int nout = min(TT, T - t0);
     for (int r0 = wv * kDwR; r0 < nout; r0 += 4 * kDwR) {
       float win[kDwR + kDwMaxK - 1];
 #pragma unroll
-      for (int i = 0; i < kDwR + kDwMaxK - 1; ++i) win[i] = (i < kDwR + k - 1) ? g[(r0 + i) * kDwCB + lane] : 0.f;
+      for (int i = 0; i < kDwR + kDwMaxK - 1; ++i)
+        win[i] = (i < kDwR + k - 1) ? ld_act(g, (r0 + i) * kDwCB + lane) : 0.f;
 #pragma unroll
       for (int r = 0; r < kDwR; ++r) {
         float acc = bv;
@@ -678,11 +669,21 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
         for (int j = 0; j < kDwMaxK; ++j) acc = fmaf(wr[j], win[r + j], acc);
         if (fused_silu) acc = acc / (1.f + __expf(-acc));
         const int t = t0 + r0 + r;
-        if (r0 + r < nout && c < C) {
+        if constexpr (BF) {
+          otile[wv][r * kDwCB + lane] = f2bf_bits(acc);
+        } else if (r0 + r < nout && c < C) {
           st_act(ys, (int64_t)t * C + c, acc);
+        }
+        if (r0 + r < nout && c < C) {
           lsum += acc;
           lsq += acc * acc;
         }
+      }
+      if constexpr (BF) {
+        // lane l: row l / 8 of the run, channels 8 * (l % 8) .. +7 (same-wave LDS round trip)
+        const int rr = lane >> 3, cc = (lane & 7) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(&otile[wv][rr * kDwCB + cc]);
+        if (r0 + rr < nout && c0 + cc < C) *reinterpret_cast<uint4*>(ys + (int64_t)(t0 + r0 + rr) * C + c0 + cc) = v;
       }
     }
   }
@@ -720,6 +721,11 @@ void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
   SD_LAUNCH_CHECK();
 }
 
+// GroupNorm(1 group) statistics from the dwconv partials, then y = silu(GN(y)) in place.
+// Each thread owns 8 consecutive channels of a row (one 16-B bf16 / 2 x 16-B fp32 access);
+// a sequence's T x C elements are split over kGnBlocks workgroups.
+constexpr int kGnBlocks = 4;
+
 template <bool BF>
 __global__ __launch_bounds__(256) void groupnorm_silu_kernel(act_t<BF>* __restrict__ y, int T, int C,
                                                              const float* __restrict__ partial, int nblk,
@@ -738,21 +744,52 @@ __global__ __launch_bounds__(256) void groupnorm_silu_kernel(act_t<BF>* __restri
   const float fm = (float)mean;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   act_t<BF>* ys = y + (int64_t)s * T * C;
-  const int64_t total = (int64_t)T * C;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int c = i % C;
-    float v = (ld_act(ys, i) - fm) * rstd * g[c] + b[c];
-    st_act(ys, i, v / (1.f + expf(-v)));
+  const int cv = C / 8;                         // 8-channel vectors per row
+  const int nvec = T * cv;
+  const int per = (nvec + gridDim.x - 1) / gridDim.x;
+  const int v0 = blockIdx.x * per, v1 = min(nvec, v0 + per);
+  for (int v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+    const int c = (v % cv) * 8;
+    act_t<BF>* p = ys + (int64_t)v * 8;
+    float x[8];
+    if constexpr (BF) {
+      const uint4 u = *reinterpret_cast<const uint4*>(p);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(w[i] << 16);
+        x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(p), bq = *reinterpret_cast<const float4*>(p + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = bq.x; x[5] = bq.y; x[6] = bq.z; x[7] = bq.w;
+    }
+    const float4 g0 = *reinterpret_cast<const float4*>(g + c), g1 = *reinterpret_cast<const float4*>(g + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(b + c), b1 = *reinterpret_cast<const float4*>(b + c + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float t = (x[i] - fm) * rstd * gg[i] + bb[i];
+      x[i] = t / (1.f + __expf(-t));
+    }
+    if constexpr (BF) {
+      const uint4 u = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                       pack_bf16x2(x[6], x[7])};
+      *reinterpret_cast<uint4*>(p) = u;
+    } else {
+      *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
   }
 }
 
 void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
                     const float* b, float eps, bool io_bf16, hipStream_t st) {
+  SD_CHECK(C % 8 == 0, kErrInvalid, "groupnorm_silu: channels must be a multiple of 8");
   int nblk = cdiv(C, kDwCB);
-  int per = cdiv(T * C, 256);
-  dim3 grid(min(per, 16), S);
-  ProfScope prof("groupnorm_silu", 0.0, 8.0 * S * T * C, st);
+  dim3 grid(kGnBlocks, S);
+  ProfScope prof("groupnorm_silu", 0.0, (io_bf16 ? 4.0 : 8.0) * S * T * C, st);
   if (io_bf16)
     hipLaunchKernelGGL(groupnorm_silu_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<uint16_t*>(y), T,
                        C, partial, nblk, g, b, eps);
