@@ -64,6 +64,7 @@ ConvL load_conv_bn(ParamStore& ps, DeviceArena& arena, bool bf16, const std::str
 // ------------------------------------------------------------------------------ CamTrunk
 void CamTrunk::load(ParamStore& ps, DeviceArena& arena, const std::string& pre, bool bf16) {
   bf16_ = bf16;
+  no_fused_ = getenv("SDIAR_NO_CAM_FUSED") != nullptr;
   auto conv_bn = [&](const std::string& w, const std::string& bn, const std::string& bias = "") {
     return load_conv_bn(ps, arena, bf16, w, bn, bias);
   };
@@ -211,10 +212,23 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
       ConvGemmArgs p = cam_conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp_, bf}, 128);
       p.act = kActRelu;
       conv_gemm(p, bf, st);
-      cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
-      ConvGemmArgs q = cam_conv1d(Tens{tmp_, bf}, B, T2, 128, L.local, 1, L.dil, L.dil, act_at(D, cin), ld);
-      q.gate = gate_; q.gate_seg = 100; q.gate_nseg = (T2 + 99) / 100;
-      conv_gemm(q, bf, st);
+      if (!no_fused_ && cam_local_fused_supported(128, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil, 100, ld, bf)) {
+        // Small batches (the embedding extractor's 96 chunks): one launch per layer that also
+        // computes the gate.  Large batches: the context kernel, then the conv kernel reading
+        // only each segment's window rows (fewer bytes per workgroup, higher occupancy).
+        if (B * ((T2 + 99) / 100) < 1024) {
+          cam_local_fused(tmp_, B, T2, L.dil, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
+                          act_at(D, cin).p, ld, st);
+        } else {
+          cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
+          cam_local_conv(tmp_, B, T2, L.dil, L.local.w.w, L.local.beta, gate_, act_at(D, cin).p, ld, st);
+        }
+      } else {
+        cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
+        ConvGemmArgs q = cam_conv1d(Tens{tmp_, bf}, B, T2, 128, L.local, 1, L.dil, L.dil, act_at(D, cin), ld);
+        q.gate = gate_; q.gate_seg = 100; q.gate_nseg = (T2 + 99) / 100;
+        conv_gemm(q, bf, st);
+      }
       cin += L.local.w.N;
     }
     SD_CHECK(cin == ld, kErrShape, "dense block width");

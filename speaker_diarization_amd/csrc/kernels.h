@@ -97,6 +97,14 @@ void fcm_conv1(const float* fbank, int B, int T, int F, const float* w /*32x9*/,
 void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int seg_len,
                  const float* w1, const float* b1, int C1, const float* w2, const float* b2,
                  int C2, float* gate, hipStream_t st);
+// CAM++ dense-layer tail fused (cam_fused.hip): context gate + linear_local k3 conv + gating
+// for one bf16 bottleneck map x (B, T, 128) -> out (B, T, 32) at row stride ldo (bf16).
+bool cam_local_fused_supported(int C, int C1, int C2, int N, int taps, int dil, int seg_len, int ldo, bool bf16);
+void cam_local_fused(const void* x, int B, int T, int dil, const void* wt, const float* bias, const float* w1,
+                     const float* b1, const float* w2, const float* b2, void* out, int ldo, hipStream_t st);
+// The conv + gating half alone, gate (B, nseg, 32) from cam_context().
+void cam_local_conv(const void* x, int B, int T, int dil, const void* wt, const float* bias, const float* gate,
+                    void* out, int ldo, hipStream_t st);
 // CAM++ out_nonlinear + StatsPool (cam_pplus_wespeaker.py:28-39, 372-379):
 // v = relu(x * s + h) over x (B, T, C) channel-last (C % 64 == 0);
 // stats (B, 2C) = [mean_t v | unbiased std_t v] (nullable); tout (B, T, C) = v (nullable).
