@@ -77,6 +77,39 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_s
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 int sd_tsvad_destroy(sd_tsvad* h);
 
+/* ------------------------------------------------------------------ chunk-streaming TS-VAD
+ * Replaces TSVADModel of egs/alimeeting/ts_vad2_streaming/model.py:95-1117 in its streaming
+ * decode: forward_chunk_by_chunk(_temp1)(xs, target_speech, labels, decoding_chunk_size,
+ * num_decoding_left_chunks) (model.py:368-461, 594-655; called through infer_debug :951-975 with
+ * simulate_streaming, B = 1).  The KV caches are expressed as block-causal attention masks, so
+ * one call decodes a whole window with the reference's per-chunk results.  State-dict keys are
+ * the streaming model's (embed.speech_encoder.*, single_backend.{i}.self_attn.linear_q.*, ...). */
+typedef struct sd_tsvad_stream sd_tsvad_stream;
+
+typedef struct {
+  int max_num_speaker;            /* 4 */
+  int max_labels;                 /* workspace: label frames (25 Hz) per window */
+  int precision;                  /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate */
+  int num_transformer_layer;      /* TSVADConfig defaults (model.py:38-79): 2, 4, 384, 1536, 192 */
+  int num_attention_head;
+  int transformer_embed_dim;
+  int transformer_ffn_embed_dim;
+  int speaker_embed_dim;
+} sd_tsvad_stream_config;
+
+int sd_tsvad_stream_create(const sd_tsvad_stream_config* cfg, sd_tsvad_stream** out);
+int sd_tsvad_stream_set_param(sd_tsvad_stream* h, const char* name, const float* host_data, const int64_t* shape,
+                              int ndim);
+int sd_tsvad_stream_finalize(sd_tsvad_stream* h);
+/* feats: device (4 * T_label, 80) fbank, already padded / trimmed to 4 x labels (model.py:614-618);
+ * ts: device (max_num_speaker, speaker_embed_dim); chunk: decoding_chunk_size (>= 2 label frames,
+ * and the last partial chunk >= 2); left_chunks: num_decoding_left_chunks (< 0: all history);
+ * logits: device (max_num_speaker, T_label), pre-sigmoid. */
+int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int T_label, int chunk,
+                            int left_chunks, float* logits, void* stream);
+int64_t sd_tsvad_stream_device_bytes(const sd_tsvad_stream* h);
+int sd_tsvad_stream_destroy(sd_tsvad_stream* h);
+
 /* ------------------------------------------------------------------ CAM++ embeddings
  * Replaces CAMPPlus (egs/alimeeting/ts_vad2/cam_pplus_wespeaker.py:311-399) as the target-speaker
  * embedding extractor of generate_chunk_speaker_embedding_from_modelscope_for_diarization.py:
@@ -282,6 +315,11 @@ int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, i
 /* Attention core on packed qkv (S*T, 3D) -> out (S*T, D). */
 int sd_op_attention(const float* qkv, int S, int T, int D, int nh, int causal, int causal_delay,
                     const int* key_len, float* out, int precision, void* stream);
+/* Chunk-streaming attention (ts_vad2_streaming forward_chunk_by_chunk's KV caches as one
+ * block-causal mask): query i sees key j iff j / chunk <= i / chunk and, when left >= 0,
+ * j / chunk >= i / chunk - left.  precision as sd_op_attention. */
+int sd_op_attention_chunk(const float* qkv, int S, int T, int D, int nh, int chunk, int left, float* out,
+                          int precision, void* stream);
 int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
                     float* y, void* stream);
 /* Residual add + LayerNorm of the encoder blocks: s = x + t (t fp32, or bf16 bits when

@@ -85,6 +85,19 @@ class CamppConfig(ctypes.Structure):
     ]
 
 
+class TsvadStreamConfig(ctypes.Structure):
+    _fields_ = [
+        ("max_num_speaker", c_int),
+        ("max_labels", c_int),
+        ("precision", c_int),
+        ("num_transformer_layer", c_int),
+        ("num_attention_head", c_int),
+        ("transformer_embed_dim", c_int),
+        ("transformer_ffn_embed_dim", c_int),
+        ("speaker_embed_dim", c_int),
+    ]
+
+
 _SIGS = {
     "sd_last_error": (c_char_p, []),
     "sd_version": (c_int, []),
@@ -98,6 +111,12 @@ _SIGS = {
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
+    "sd_tsvad_stream_create": (c_int, [POINTER(TsvadStreamConfig), POINTER(c_void_p)]),
+    "sd_tsvad_stream_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_tsvad_stream_finalize": (c_int, [c_void_p]),
+    "sd_tsvad_stream_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sd_tsvad_stream_device_bytes": (c_int64, [c_void_p]),
+    "sd_tsvad_stream_destroy": (c_int, [c_void_p]),
     "sd_campp_create": (c_int, [POINTER(CamppConfig), POINTER(c_void_p)]),
     "sd_campp_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_campp_finalize": (c_int, [c_void_p]),
@@ -146,6 +165,8 @@ _SIGS = {
                              c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                 c_void_p]),
+    "sd_op_attention_chunk": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                      c_void_p]),
     "sd_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "sd_op_lstm": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p]),

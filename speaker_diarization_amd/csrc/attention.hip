@@ -19,6 +19,15 @@ namespace sd {
 namespace {
 
 constexpr int kQB = 64;   // queries per block
+
+// Chunk-streaming visibility (AttnArgs::chunk / left) as the key window [lo, hi) of query q:
+// keys of chunks max(0, c - left) .. c, c = q / chunk.  One division per query.
+struct KeyWindow { int lo, hi; };
+__device__ __forceinline__ KeyWindow chunk_window(const AttnArgs& a, int q) {
+  if (!a.chunk) return {0, 0x7fffffff};
+  const int qc = q / a.chunk;
+  return {a.left < 0 ? 0 : max(0, qc - a.left) * a.chunk, (qc + 1) * a.chunk};
+}
 constexpr int kKT = 32;   // keys per tile
 
 constexpr int f32_stride(int hd) { return hd + (((4 - hd) % 32) + 32) % 32; }
@@ -86,9 +95,13 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
+  const KeyWindow kw = chunk_window(a, myq);
   int k_end = klen;
   if (a.causal) k_end = min(k_end, blockIdx.x * kQB + kQB + a.causal_delay);
-  for (int k0 = 0; k0 < k_end; k0 += kKT) {
+  if (a.chunk) k_end = min(k_end, ((blockIdx.x * kQB + kQB - 1) / a.chunk + 1) * a.chunk);
+  // left >= 0: tiles wholly before the block's first query window hold no visible key
+  const int k_begin = (a.chunk && a.left >= 0) ? chunk_window(a, blockIdx.x * kQB).lo / kKT * kKT : 0;
+  for (int k0 = k_begin; k0 < k_end; k0 += kKT) {
     __syncthreads();
     // Stage K and V for keys [k0, k0+32).
     constexpr int F4 = HD / 4;
@@ -163,7 +176,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int key = k0 + st * 16 + g * 4 + r;
-        bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
+        bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay) && key >= kw.lo && key < kw.hi;
         float v = ok ? sc[st][r] : -INFINITY;
         sc[st][r] = v;
         tmax = fmaxf(tmax, v);
@@ -346,9 +359,12 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
 #pragma unroll
       for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
       float m_run = -INFINITY, l_run = 0.f;   // statistics of query myq
+      const KeyWindow kw = chunk_window(a, myq);
       int k_end = klen;
       if (a.causal) k_end = min(k_end, q0 + 16 + a.causal_delay);
-      for (int k0 = 0; k0 < k_end; k0 += 32) {
+      if (a.chunk) k_end = min(k_end, ((q0 + 15) / a.chunk + 1) * a.chunk);
+      const int k_begin = (a.chunk && a.left >= 0) ? chunk_window(a, q0).lo / 32 * 32 : 0;
+      for (int k0 = k_begin; k0 < k_end; k0 += 32) {
         floatx4 sc[2];
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -366,7 +382,7 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = k0 + st * 16 + g * 4 + r;
-            const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
+            const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay) && key >= kw.lo && key < kw.hi;
             const float v = ok ? sc[st][r] : -INFINITY;
             sc[st][r] = v;
             tmax = fmaxf(tmax, v);

@@ -15,6 +15,7 @@
 #include "fseend_stream.h"
 #include "tsvad.h"
 #include "campp.h"
+#include "tsvad_stream.h"
 
 namespace sd {
 static thread_local std::string g_err;
@@ -32,6 +33,10 @@ struct sd_eda {
 
 struct sd_campp {
   std::unique_ptr<sd::CamppModel> model;
+};
+
+struct sd_tsvad_stream {
+  std::unique_ptr<sd::TsvadStreamModel> model;
 };
 
 struct sd_fseend {
@@ -355,6 +360,61 @@ int sd_fbank_kaldi_ex(const float* wav, int64_t n_samples, float in_scale, int n
   });
 }
 
+int sd_tsvad_stream_create(const sd_tsvad_stream_config* c, sd_tsvad_stream** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->max_labels > 0 && c->max_num_speaker > 0, sd::kErrInvalid, "bad workspace sizes");
+    SD_CHECK(c->num_attention_head > 0 && c->transformer_embed_dim % c->num_attention_head == 0, sd::kErrInvalid,
+             "transformer_embed_dim must be divisible by num_attention_head");
+    sd::TsvadStreamConfig t;
+    t.max_num_speaker = c->max_num_speaker;
+    t.max_labels = c->max_labels;
+    t.bf16 = c->precision == 1;
+    t.num_transformer_layer = c->num_transformer_layer;
+    t.num_attention_head = c->num_attention_head;
+    t.embed_dim = c->transformer_embed_dim;
+    t.ffn_dim = c->transformer_ffn_embed_dim;
+    t.speaker_embed_dim = c->speaker_embed_dim;
+    auto* h = new sd_tsvad_stream;
+    h->model.reset(new sd::TsvadStreamModel(t));
+    *out = h;
+  });
+}
+
+int sd_tsvad_stream_set_param(sd_tsvad_stream* h, const char* name, const float* data, const int64_t* shape,
+                              int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_tsvad_stream_finalize(sd_tsvad_stream* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int T_label, int chunk,
+                            int left_chunks, float* logits, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && feats && ts && logits, sd::kErrInvalid, "null argument");
+    SD_CHECK(chunk > 0, sd::kErrShape, "decoding_chunk_size must be > 0");
+    h->model->forward(feats, ts, T_label, chunk, left_chunks, logits, S(stream));
+  });
+}
+
+int64_t sd_tsvad_stream_device_bytes(const sd_tsvad_stream* h) {
+  return h ? (int64_t)h->model->device_bytes() : 0;
+}
+
+int sd_tsvad_stream_destroy(sd_tsvad_stream* h) {
+  return guard([&] { delete h; });
+}
+
 int sd_campp_create(const sd_campp_config* c, sd_campp** out) {
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
@@ -525,23 +585,37 @@ int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, i
   });
 }
 
+namespace {
+void op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, int causal_delay, const int* key_len,
+                  int chunk, int left, float* out, int precision, hipStream_t st) {
+  SD_CHECK(precision >= 0 && precision <= 2, sd::kErrInvalid, "precision must be 0, 1 or 2");
+  sd::AttnArgs a;
+  a.qkv = qkv; a.S = S_; a.T = T; a.D = D; a.nh = nh; a.ld_qkv = 3 * D;
+  a.out = out; a.ldo = D; a.scale = 1.f / std::sqrt((float)(D / nh));
+  a.causal = causal; a.causal_delay = causal_delay; a.key_len = key_len;
+  a.chunk = chunk; a.left = left;
+  if (precision == 2) {   // bf16 storage: qkv and out in bf16 (the encoders' layout)
+    Scratch qb((size_t)S_ * T * 3 * D * 2, st), ob((size_t)S_ * T * D * 2, st);
+    sd::f32_to_bf16(qkv, (int64_t)S_ * T * 3 * D, qb.p, st);
+    a.qkv = qb.p; a.out = ob.p; a.io_bf16 = true;
+    sd::attention(a, true, st);
+    sd::bf16_to_f32(ob.p, (int64_t)S_ * T * D, out, st);
+    return;
+  }
+  sd::attention(a, precision == 1, st);
+}
+}  // namespace
+
 int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, int causal_delay,
                     const int* key_len, float* out, int precision, void* stream) {
+  return guard([&] { op_attention(qkv, S_, T, D, nh, causal, causal_delay, key_len, 0, -1, out, precision, S(stream)); });
+}
+
+int sd_op_attention_chunk(const float* qkv, int S_, int T, int D, int nh, int chunk, int left, float* out,
+                          int precision, void* stream) {
   return guard([&] {
-    sd::AttnArgs a;
-    a.qkv = qkv; a.S = S_; a.T = T; a.D = D; a.nh = nh; a.ld_qkv = 3 * D;
-    a.out = out; a.ldo = D; a.scale = 1.f / std::sqrt((float)(D / nh));
-    a.causal = causal; a.causal_delay = causal_delay; a.key_len = key_len;
-    if (precision == 2) {   // bf16 storage: qkv and out in bf16 (the encoders' layout)
-      hipStream_t st = S(stream);
-      Scratch qb((size_t)S_ * T * 3 * D * 2, st), ob((size_t)S_ * T * D * 2, st);
-      sd::f32_to_bf16(qkv, (int64_t)S_ * T * 3 * D, qb.p, st);
-      a.qkv = qb.p; a.out = ob.p; a.io_bf16 = true;
-      sd::attention(a, true, st);
-      sd::bf16_to_f32(ob.p, (int64_t)S_ * T * D, out, st);
-      return;
-    }
-    sd::attention(a, precision == 1, S(stream));
+    SD_CHECK(chunk > 0, sd::kErrInvalid, "decoding chunk must be > 0");
+    op_attention(qkv, S_, T, D, nh, 0, 0, nullptr, chunk, left, out, precision, S(stream));
   });
 }
 

@@ -139,6 +139,10 @@ struct AttnArgs {
   // Token t of sequence s lives at row (s / seq_inner) * seq_outer + (s % seq_inner) * seq_inner_stride
   // + t * tok_stride of qkv / out.  Defaults (seq_outer 0 -> T) give contiguous sequences; the FS-EEND
   // decoder runs its time attention over the slots of a (T, C) token grid with tok_stride C.
+  // Chunk-streaming mask (ts_vad2_streaming forward_chunk_by_chunk with KV caches, expressed as
+  // one forward): query i sees key j iff chunk(j) <= chunk(i) and, when left >= 0,
+  // chunk(j) >= chunk(i) - left, with chunk(x) = x / chunk.  chunk 0: off.
+  int chunk = 0, left = -1;
   int seq_inner = 1;
   int64_t seq_outer = 0;
   int seq_inner_stride = 0;
@@ -153,6 +157,11 @@ void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
                          int T, int E, const float* pe, float* out, hipStream_t st);
 
+// Chunk-streaming speaker input (ts_vad2_streaming/model.py:767-777): row (spk, t) =
+// [ts[spk] | mix[t]] * scale + pe[pos(t)], pos(t) = start(t / C) + t % C with start(c) = 0
+// (left < 0: the whole history is cached) or max(0, c - left) * C.  out (NS * T, 2E).
+void build_stream_input(const float* ts, const float* mix, int T, int NS, int E, float scale, const float* pe,
+                        int C, int left, float* out, hipStream_t st);
 // x[r, :] += pe[r % T, :]  (rows of length D at stride ld)
 void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st);
 

@@ -253,6 +253,8 @@ def synthetic_state_dict(layout: list, seed: int = 777, extras: Dict[str, np.nda
     for name, shape, kind in layout:
         if kind == "pe":
             sd[name] = sinusoid_pe(shape[0], shape[2])
+        elif kind == "pe1":   # (1, max_len, d) buffer of the wenet-style PositionalEncoding
+            sd[name] = np.ascontiguousarray(sinusoid_pe(shape[1], shape[2]).transpose(1, 0, 2))
         else:
             sd[name] = _init(rng, shape, kind)
     if extras:
@@ -262,6 +264,57 @@ def synthetic_state_dict(layout: list, seed: int = 777, extras: Dict[str, np.nda
 
 def tsvad_state_dict(cfg: TSVADConfig, seed: int = 777):
     return synthetic_state_dict(tsvad_layout(cfg), seed)
+
+
+@dataclass
+class TSVADStreamingConfig:
+    """egs/alimeeting/ts_vad2_streaming/model.py:38-79 (TSVADConfig) fields the chunk-streaming
+    inference path reads (CAM++ Subsampling4 + wenet pre-LN transformers)."""
+    num_attention_head: int = 4
+    num_transformer_layer: int = 2
+    transformer_embed_dim: int = 384
+    transformer_ffn_embed_dim: int = 1536
+    speaker_embed_dim: int = 192
+    max_num_speaker: int = 4
+    pe_max_len: int = 5000           # PositionalEncoding default max_len (model.py:1189-1212)
+
+
+def _wenet_layer(k: list, p: str, e: int, ffn: int):
+    """transformer_chunk_streaming.TransformerEncoderLayer (MultiHeadedAttention with separate
+    linear_q/k/v/out, PositionwiseFeedForward w_1/w_2, norm1/norm2)."""
+    for n in ("linear_q", "linear_k", "linear_v", "linear_out"):
+        k.append((f"{p}self_attn.{n}.weight", (e, e), "linear"))
+        k.append((f"{p}self_attn.{n}.bias", (e,), "small"))
+    k.append((p + "feed_forward.w_1.weight", (ffn, e), "linear"))
+    k.append((p + "feed_forward.w_1.bias", (ffn,), "small"))
+    k.append((p + "feed_forward.w_2.weight", (e, ffn), "linear"))
+    k.append((p + "feed_forward.w_2.bias", (e,), "small"))
+    _ln(k, p + "norm1", e)
+    _ln(k, p + "norm2", e)
+
+
+def tsvad_streaming_layout(cfg: TSVADStreamingConfig) -> list:
+    """Key layout of ts_vad2_streaming/model.py TSVADModel (:96-171)."""
+    e, se, ns = cfg.transformer_embed_dim, cfg.speaker_embed_dim, cfg.max_num_speaker
+    k = campplus_layout("embed.speech_encoder.")
+    k.append(("embed.speech_down_or_up.0.weight", (se, 512, 5), "conv1d"))
+    k.append(("embed.speech_down_or_up.0.bias", (se,), "small"))
+    _bn(k, "embed.speech_down_or_up.1.bn", se)
+    for i in range(cfg.num_transformer_layer):
+        _wenet_layer(k, f"single_backend.{i}.", e, cfg.transformer_ffn_embed_dim)
+    k.append(("backend_down.0.weight", (e, e * ns, 5), "conv1d"))
+    k.append(("backend_down.0.bias", (e,), "small"))
+    _bn(k, "backend_down.1.bn", e)
+    k.append(("pos_encoder.pe", (1, cfg.pe_max_len, e), "pe1"))
+    for i in range(cfg.num_transformer_layer):
+        _wenet_layer(k, f"multi_backend.{i}.", e, cfg.transformer_ffn_embed_dim)
+    k.append(("fc.weight", (ns, e), "linear"))
+    k.append(("fc.bias", (ns,), "small"))
+    return k
+
+
+def tsvad_streaming_state_dict(cfg: TSVADStreamingConfig, seed: int = 777):
+    return synthetic_state_dict(tsvad_streaming_layout(cfg), seed)
 
 
 def campplus_state_dict(seed: int = 777, embedding_size: int = 192):

@@ -207,6 +207,53 @@ def make_campp_extract(name):
     print(name, {k: v.shape for k, v in out.items()}, batches)
 
 
+# ----------------------------------------------------------------------------- streaming TS-VAD
+TSVAD_STREAM_CASES = {
+    # name: (T_label, decoding_chunk_size, num_decoding_left_chunks, T_fbank, input seed, weight seed)
+    "tsvad_stream_c25": (100, 25, -1, 400, 61, 811),
+    "tsvad_stream_c10_l2": (60, 10, 2, 240, 62, 812),
+    "tsvad_stream_tail": (70, 25, -1, 277, 63, 813),     # short last chunk; xs padded to 4 * T_label
+}
+
+
+def tsvad_stream_inputs(T_fb, seed):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal((1, T_fb, 80)).astype(np.float32),
+            rng.standard_normal((1, 4, 192)).astype(np.float32))
+
+
+def make_tsvad_stream(name):
+    """ts_vad2_streaming/model.py TSVADModel.forward_chunk_by_chunk_temp1 (the path infer_debug
+    takes with simulate_streaming, model.py:951-975), B = 1."""
+    import torch
+    from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
+    T_lab, dcs, left, T_fb, iseed, wseed = TSVAD_STREAM_CASES[name]
+    install_stubs()
+    d = os.path.join(REF, "egs/alimeeting/ts_vad2_streaming")
+    sys.path.insert(0, d)
+    for mod in ("model", "cam_pplus_wespeaker", "datasets", "ts_vad_dataset", "mask", "transformer_chunk_streaming"):
+        sys.modules.pop(mod, None)
+    import model as M
+    M.Subsampling4.load_speaker_encoder = lambda self, *a, **k: None
+    torch.manual_seed(0)
+    m = M.TSVADModel()
+    m.eval()
+    cfg = TSVADStreamingConfig()
+    m.load_state_dict(to_torch(tsvad_streaming_state_dict(cfg, seed=wseed)), strict=True)
+    xs, ts = tsvad_stream_inputs(T_fb, iseed)
+    labels = torch.zeros(1, 4, T_lab)
+    import contextlib, io
+    with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+        ys = m.forward_chunk_by_chunk_temp1(torch.from_numpy(xs), torch.from_numpy(ts), labels,
+                                            decoding_chunk_size=dcs, num_decoding_left_chunks=left)
+    out = dict(logits=ys.numpy().astype(np.float32))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, out["logits"].shape)
+    sys.path.remove(d)
+    for mod in ("model", "cam_pplus_wespeaker", "datasets", "ts_vad_dataset", "mask", "transformer_chunk_streaming"):
+        sys.modules.pop(mod, None)
+
+
 # ----------------------------------------------------------------------------- EEND-EDA
 EDA_CASES = {
     # name: (model_type, n_layers, chunk lengths, infer_num_speakers, input seed, weight seed)
@@ -419,12 +466,14 @@ if __name__ == "__main__":
     import torch
     torch.set_num_threads(8)
     names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES)
-                             + list(FSEEND_CASES) + list(EEND_CASES) + list(CAMPP_CASES) + list(CAMPP_EXTRACT))
+                             + list(FSEEND_CASES) + list(EEND_CASES) + list(CAMPP_CASES) + list(CAMPP_EXTRACT) + list(TSVAD_STREAM_CASES))
     for n in names:
         if n in TSVAD_CASES:
             make_tsvad(n)
         elif n in CAMPP_CASES:
             make_campp(n)
+        elif n in TSVAD_STREAM_CASES:
+            make_tsvad_stream(n)
         elif n in CAMPP_EXTRACT:
             make_campp_extract(n)
         elif n in EDA_CASES:

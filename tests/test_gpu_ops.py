@@ -166,6 +166,37 @@ def test_attention_key_len(gpu, precision):
         assert _rel_err(out.cpu(), ref) < 2e-2
 
 
+def _chunk_mask(T, chunk, left):
+    """Key visibility of forward_chunk_by_chunk's KV caches (ts_vad2_streaming/model.py:594-655,
+    transformer_chunk_streaming.py:305-373): chunks max(0, c - left) .. c."""
+    c = torch.arange(T) // chunk
+    vis = c[None, :] <= c[:, None]
+    if left >= 0:
+        vis &= c[None, :] >= c[:, None] - left
+    return ~vis
+
+
+@pytest.mark.parametrize("precision", [0, 1, 2])
+@pytest.mark.parametrize("S,T,D,nh,chunk,left", [(4, 100, 384, 4, 25, -1), (4, 100, 384, 4, 25, 1),
+                                                  (1, 64, 96, 1, 1000, -1), (2, 300, 384, 4, 16, 0),
+                                                  (3, 250, 384, 4, 50, 2), (1, 77, 256, 4, 10, 3)])
+def test_attention_chunk(gpu, precision, S, T, D, nh, chunk, left):
+    g = torch.Generator().manual_seed(T + chunk)
+    qkv = torch.randn(S * T, 3 * D, generator=g)
+    hd = D // nh
+    q, k, v = qkv.view(S, T, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2) / math.sqrt(hd)).masked_fill(_chunk_mask(T, chunk, left), float("-inf"))
+    ref = (torch.softmax(sc, -1) @ v).permute(0, 2, 1, 3).reshape(S * T, D)
+    out = torch.empty(S * T, D, device=gpu)
+    _lib.call("sd_op_attention_chunk", _d(qkv, gpu), S, T, D, nh, chunk, left, out.data_ptr(), precision,
+              _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    if precision == 0:
+        torch.testing.assert_close(out.cpu(), ref, **FP32_TOL)
+    else:
+        assert _rel_err(out.cpu(), ref) < 2e-2
+
+
 def test_attention_large_logits(gpu):
     """Online-softmax rescale path: a key tile far later in the sequence dominates."""
     S, T, D, nh = 1, 200, 256, 4

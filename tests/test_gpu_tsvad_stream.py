@@ -1,0 +1,59 @@
+"""Chunk-streaming TS-VAD on the GPU (libsdiar sd_tsvad_stream_*) vs the reference goldens and
+the CPU oracle.  Tolerances: fp32 1e-3 absolute (north_star); bf16 1 % of the logit range
+(bf16 operands carry 8 mantissa bits, and this model's logits reach |8|, four times the offline
+TS-VAD's, whose bf16 bound is 2e-2 absolute)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from make_golden import TSVAD_STREAM_CASES, tsvad_stream_inputs
+from speaker_diarization_amd.ts_vad.streaming import TSVADStreamingModel
+from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(TSVAD_STREAM_CASES))
+def test_stream_matches_reference(gpu, name, precision):
+    T_lab, dcs, left, T_fb, iseed, wseed = TSVAD_STREAM_CASES[name]
+    m = TSVADStreamingModel(TSVADStreamingConfig(), device=gpu, precision=precision, max_labels=128)
+    m.load_state_dict(to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=wseed)))
+    xs, ts = tsvad_stream_inputs(T_fb, iseed)
+    y = m.forward_chunk_by_chunk_temp1(torch.from_numpy(xs), torch.from_numpy(ts), torch.zeros(1, 4, T_lab),
+                                       decoding_chunk_size=dcs, num_decoding_left_chunks=left).cpu().numpy()
+    g = np.load(os.path.join(GOLD, name + ".npz"))["logits"]
+    err = np.abs(y - g).max()
+    print(f"{name} {precision}: max|logit diff| = {err:.3e} (max|logit| {np.abs(g).max():.2f})")
+    assert err < (1e-3 if precision == "fp32" else 1e-2 * max(1.0, float(np.abs(g).max())))
+
+
+def test_stream_long_window_vs_oracle(gpu):
+    """A 16 s window (400 label frames, 16 chunks of 25) through the long-sequence attention
+    kernel (T > 256) vs the oracle's literal chunk loop, with a 4-chunk left context."""
+    from oracle.tsvad_stream_ref import forward_chunk_by_chunk
+    sd = tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=71)
+    xs, ts = tsvad_stream_inputs(1600, 72)
+    m = TSVADStreamingModel(device=gpu, precision="fp32", max_labels=400).load_state_dict(to_torch(sd))
+    for left in (-1, 4):
+        y = m.forward_chunk_by_chunk(torch.from_numpy(xs), torch.from_numpy(ts), 400, 25, left).cpu().numpy()
+        with torch.no_grad():
+            ref = forward_chunk_by_chunk(to_torch(sd), torch.from_numpy(xs), torch.from_numpy(ts), 400, 25, left).numpy()
+        assert np.abs(y - ref).max() < 1e-3, left
+
+
+def test_stream_errors(gpu):
+    sd = to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=3))
+    m = TSVADStreamingModel(device=gpu, precision="fp32", max_labels=64).load_state_dict(sd)
+    xs, ts = tsvad_stream_inputs(200, 4)
+    with pytest.raises(ValueError):
+        m.forward_chunk_by_chunk(torch.from_numpy(xs), torch.from_numpy(ts), 100, 25)   # > max_labels
+    with pytest.raises(ValueError):
+        m.forward_chunk_by_chunk(torch.from_numpy(xs), torch.from_numpy(ts), 50, 1)     # 4-frame chunks
+    bad = dict(sd)
+    bad.pop("fc.bias")
+    with pytest.raises(RuntimeError, match="fc.bias"):
+        TSVADStreamingModel(device=gpu, max_labels=64).load_state_dict(bad)

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/e7
+O=gpurun_out/${RUN:-e7}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_tsvad.py tests/test_gpu_campp.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }
 timeout -k 10 200 python -u bench.py --no-cpu-baseline > $O/c2.json 2> $O/c2.err || exit 2
