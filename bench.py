@@ -44,6 +44,10 @@ WORKLOADS = {
                 desc="Target-speaker embeddings: CAM++ (CAMPPLUS_COMMON, 192-d) over 4 speakers' enrollment "
                      "audio (2.5 min each, 16 kHz), extract_embed 6 s chunks every 1 s, batch 96 "
                      "(generate_chunk_speaker_embedding_from_modelscope_for_diarization.py); replicas only"),
+    "tss": dict(kind="tsvad_stream", n_spk=4, minutes=10.0, chunk=25, left=-1,
+                desc="Chunk-streaming TS-VAD (ts_vad2_streaming, run_ts_vad2_streaming.sh decode: rs_len 10 s, "
+                     "segment_shift 1 s, decoding_chunk_size 25 (1 s), num_decoding_left_chunks -1, "
+                     "simulate_streaming), 4 speakers, 64 windows per call; replicas only"),
     "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
                 desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
                      "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
@@ -321,6 +325,22 @@ def main_eend(a, wl):
         def step():
             return [extract_embed(w, m, batch_size=96) for w in wavs]
         frames = sum(w.numel() for w in wavs) // 160 * world
+    elif kind == "tsvad_stream":
+        from speaker_diarization_amd.synth import speaker_embeddings
+        from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+        from speaker_diarization_amd.ts_vad.streaming import StreamingWindowDecoder, TSVADStreamingModel
+        from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
+        meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank)
+        m = TSVADStreamingModel(device=dev, precision=prec, max_labels=250, max_windows=64)
+        m.load_state_dict(to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=777)))
+        pipe = TSVADPipeline(StreamingWindowDecoder(m, wl["chunk"], wl["left"]), segment_shift=1, batch_size=64)
+        wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+        ts = torch.from_numpy(speaker_embeddings(4, seed=777)).to(dev)
+        plan = pipe.plan(wav.numel() // 640)
+
+        def step():   # replicas: every rank decodes its own meeting
+            return pipe.average(pipe.window_logits(wav, ts, plan), plan)
+        frames = meeting.wav.size // 160 * world
     else:
         from speaker_diarization_amd.feature import eend_features
         from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
@@ -496,7 +516,7 @@ if __name__ == "__main__":
     _a = parse()
     if WORKLOADS[_a.workload].get("kind") == "fseend_stream":
         main_stream(_a, WORKLOADS[_a.workload])
-    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend", "embed"):
+    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend", "embed", "tsvad_stream"):
         main_eend(_a, WORKLOADS[_a.workload])
     else:
         main()

@@ -95,17 +95,20 @@ typedef struct {
   int transformer_embed_dim;
   int transformer_ffn_embed_dim;
   int speaker_embed_dim;
+  int max_windows;                /* workspace: windows per forward call (>= 1) */
 } sd_tsvad_stream_config;
 
 int sd_tsvad_stream_create(const sd_tsvad_stream_config* cfg, sd_tsvad_stream** out);
 int sd_tsvad_stream_set_param(sd_tsvad_stream* h, const char* name, const float* host_data, const int64_t* shape,
                               int ndim);
 int sd_tsvad_stream_finalize(sd_tsvad_stream* h);
-/* feats: device (4 * T_label, 80) fbank, already padded / trimmed to 4 x labels (model.py:614-618);
- * ts: device (max_num_speaker, speaker_embed_dim); chunk: decoding_chunk_size (>= 2 label frames,
- * and the last partial chunk >= 2); left_chunks: num_decoding_left_chunks (< 0: all history);
- * logits: device (max_num_speaker, T_label), pre-sigmoid. */
-int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int T_label, int chunk,
+/* B independent windows, each decoded as the reference's chunk loop decodes one (infer_debug,
+ * batch 1, model.py:951-975).  feats: device (B, 4 * T_label, 80) fbank, already padded / trimmed
+ * to 4 x labels (model.py:614-618); ts: device (B, max_num_speaker, speaker_embed_dim); chunk:
+ * decoding_chunk_size (>= 2 label frames, and the last partial chunk >= 2); left_chunks:
+ * num_decoding_left_chunks (< 0: all history); logits: device (B, max_num_speaker, T_label),
+ * pre-sigmoid. */
+int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int B, int T_label, int chunk,
                             int left_chunks, float* logits, void* stream);
 int64_t sd_tsvad_stream_device_bytes(const sd_tsvad_stream* h);
 int sd_tsvad_stream_destroy(sd_tsvad_stream* h);

@@ -95,6 +95,7 @@ class TsvadStreamConfig(ctypes.Structure):
         ("transformer_embed_dim", c_int),
         ("transformer_ffn_embed_dim", c_int),
         ("speaker_embed_dim", c_int),
+        ("max_windows", c_int),
     ]
 
 
@@ -114,7 +115,8 @@ _SIGS = {
     "sd_tsvad_stream_create": (c_int, [POINTER(TsvadStreamConfig), POINTER(c_void_p)]),
     "sd_tsvad_stream_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_tsvad_stream_finalize": (c_int, [c_void_p]),
-    "sd_tsvad_stream_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sd_tsvad_stream_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                        c_void_p]),
     "sd_tsvad_stream_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_stream_destroy": (c_int, [c_void_p]),
     "sd_campp_create": (c_int, [POINTER(CamppConfig), POINTER(c_void_p)]),

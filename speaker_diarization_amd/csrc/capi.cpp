@@ -364,12 +364,14 @@ int sd_tsvad_stream_create(const sd_tsvad_stream_config* c, sd_tsvad_stream** ou
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
     SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
-    SD_CHECK(c->max_labels > 0 && c->max_num_speaker > 0, sd::kErrInvalid, "bad workspace sizes");
+    SD_CHECK(c->max_labels > 0 && c->max_num_speaker > 0 && c->max_windows > 0, sd::kErrInvalid,
+             "bad workspace sizes");
     SD_CHECK(c->num_attention_head > 0 && c->transformer_embed_dim % c->num_attention_head == 0, sd::kErrInvalid,
              "transformer_embed_dim must be divisible by num_attention_head");
     sd::TsvadStreamConfig t;
     t.max_num_speaker = c->max_num_speaker;
     t.max_labels = c->max_labels;
+    t.max_windows = c->max_windows;
     t.bf16 = c->precision == 1;
     t.num_transformer_layer = c->num_transformer_layer;
     t.num_attention_head = c->num_attention_head;
@@ -398,12 +400,12 @@ int sd_tsvad_stream_finalize(sd_tsvad_stream* h) {
   });
 }
 
-int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int T_label, int chunk,
+int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int B, int T_label, int chunk,
                             int left_chunks, float* logits, void* stream) {
   return guard([&] {
     SD_CHECK(h && feats && ts && logits, sd::kErrInvalid, "null argument");
     SD_CHECK(chunk > 0, sd::kErrShape, "decoding_chunk_size must be > 0");
-    h->model->forward(feats, ts, T_label, chunk, left_chunks, logits, S(stream));
+    h->model->forward(feats, ts, B, T_label, chunk, left_chunks, logits, S(stream));
   });
 }
 

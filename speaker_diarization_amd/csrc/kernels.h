@@ -157,11 +157,11 @@ void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
                          int T, int E, const float* pe, float* out, hipStream_t st);
 
-// Chunk-streaming speaker input (ts_vad2_streaming/model.py:767-777): row (spk, t) =
-// [ts[spk] | mix[t]] * scale + pe[pos(t)], pos(t) = start(t / C) + t % C with start(c) = 0
-// (left < 0: the whole history is cached) or max(0, c - left) * C.  out (NS * T, 2E).
-void build_stream_input(const float* ts, const float* mix, int T, int NS, int E, float scale, const float* pe,
-                        int C, int left, float* out, hipStream_t st);
+// Chunk-streaming speaker input (ts_vad2_streaming/model.py:767-777): row (b, spk, t) =
+// [ts[b, spk] | mix[b, t]] * scale + pe[pos(t)], pos(t) = start(t / C) + t % C with start(c) = 0
+// (left < 0: the whole history is cached) or max(0, c - left) * C.  out (B * NS * T, 2E).
+void build_stream_input(const float* ts, const float* mix, int B, int T, int NS, int E, float scale,
+                        const float* pe, int C, int left, float* out, hipStream_t st);
 // x[r, :] += pe[r % T, :]  (rows of length D at stride ld)
 void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st);
 

@@ -515,24 +515,24 @@ void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix,
 }
 
 __global__ void build_stream_input_kernel(const float* __restrict__ ts, const float* __restrict__ mix, int T,
-                                          int E, float scale, const float* __restrict__ pe, int C, int left,
-                                          float* __restrict__ out) {
-  const int row = blockIdx.x;   // (spk, t)
-  const int t = row % T, spk = row / T;
+                                          int NS, int E, float scale, const float* __restrict__ pe, int C,
+                                          int left, float* __restrict__ out) {
+  const int row = blockIdx.x;   // (window, spk, t)
+  const int t = row % T, spk = row / T, w = spk / NS;
   const int ch = t / C;
   const int pos = (left < 0 ? 0 : max(0, ch - left) * C) + t % C;
   float* o = out + (int64_t)row * 2 * E;
   const float* pr = pe + (int64_t)pos * 2 * E;
   for (int c = threadIdx.x; c < 2 * E; c += blockDim.x) {
-    const float v = c < E ? ts[(int64_t)spk * E + c] : mix[(int64_t)t * E + c - E];
+    const float v = c < E ? ts[(int64_t)spk * E + c] : mix[((int64_t)w * T + t) * E + c - E];
     o[c] = v * scale + pr[c];
   }
 }
 
-void build_stream_input(const float* ts, const float* mix, int T, int NS, int E, float scale, const float* pe,
-                        int C, int left, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(build_stream_input_kernel, dim3(NS * T), dim3(128), 0, st, ts, mix, T, E, scale, pe, C, left,
-                     out);
+void build_stream_input(const float* ts, const float* mix, int B, int T, int NS, int E, float scale,
+                        const float* pe, int C, int left, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(build_stream_input_kernel, dim3(B * NS * T), dim3(128), 0, st, ts, mix, T, NS, E, scale, pe, C,
+                     left, out);
   SD_LAUNCH_CHECK();
 }
 

@@ -9,6 +9,7 @@
 #include "tsvad_stream.h"
 
 #include <cmath>
+#include <functional>
 
 namespace sd {
 
@@ -76,8 +77,8 @@ void TsvadStreamModel::finalize() {
   }
   // CAM++ workspace by total frames: a window's chunks hold 4 * T_lab fbank frames in all, and
   // the trunk's buffers scale with items x frames (see CamTrunk::alloc).
-  cam_.alloc(arena_, cfg_.max_labels, 6);
-  const int64_t Tm = cfg_.max_labels, NS = cfg_.max_num_speaker, E = cfg_.embed_dim;
+  const int64_t Tm = (int64_t)cfg_.max_windows * cfg_.max_labels, NS = cfg_.max_num_speaker, E = cfg_.embed_dim;
+  cam_.alloc(arena_, (int)Tm, 6);
   const int64_t rows = NS * Tm;
   mix_ = ws(Tm * cfg_.speaker_embed_dim);
   X_ = ws(rows * E);
@@ -118,9 +119,10 @@ void TsvadStreamModel::run_layers(const std::vector<WenetLayerL>& Ls, float* X, 
   }
 }
 
-void TsvadStreamModel::forward(const float* feats, const float* ts, int T_lab, int chunk, int left, float* logits,
-                               hipStream_t st) {
+void TsvadStreamModel::forward(const float* feats, const float* ts, int B, int T_lab, int chunk, int left,
+                               float* logits, hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
+  SD_CHECK(B >= 1 && B <= cfg_.max_windows, kErrInvalid, "windows per call exceed max_windows");
   SD_CHECK(T_lab >= 1 && T_lab <= cfg_.max_labels, kErrInvalid, "label frames exceed max_labels");
   SD_CHECK(chunk >= 2, kErrInvalid, "decoding_chunk_size must be >= 2 (8 fbank frames per chunk)");
   const bool bf = cfg_.bf16;
@@ -128,36 +130,46 @@ void TsvadStreamModel::forward(const float* feats, const float* ts, int T_lab, i
   // positional-encoding rows used: start(c) + C <= T_lab + C
   SD_CHECK(T_lab + chunk <= pe_len_, kErrShape, "window longer than pos_encoder max_len");
   const int n_full = T_lab / chunk, tail = T_lab % chunk;
-  // ---- embed: CAM++ (get_time_out) + speech_down_or_up per chunk (chunks are contiguous rows)
-  auto embed = [&](const float* f, int B, int C) {
-    const Tens x4 = cam_.forward(f, B, 4 * C, st);
-    ConvGemmArgs p = cam_conv1d(x4, B, CamTrunk::out_frames(4 * C), CamTrunk::kChannels, down_, 2, 2, 1,
-                                Tens{mix_ + (int64_t)(f - feats) / (4 * 80) * SE, false}, SE);
+  SD_CHECK(tail == 0 || tail >= 2, kErrInvalid, "last chunk must hold >= 2 label frames (8 fbank frames)");
+  // Chunk runs: windows are contiguous, so without a tail every window's chunks form one run of
+  // B * n_full equal chunks; with a tail, each window's full chunks and its tail are separate runs.
+  // ---- embed: CAM++ (get_time_out) + speech_down_or_up per chunk (chunk c of the window holds
+  // fbank rows 4Cc .. 4C(c+1) and label rows Cc .. C(c+1))
+  auto embed = [&](int64_t lab0, int nb, int C) {
+    const Tens x4 = cam_.forward(feats + lab0 * 4 * 80, nb, 4 * C, st);
+    ConvGemmArgs p = cam_conv1d(x4, nb, CamTrunk::out_frames(4 * C), CamTrunk::kChannels, down_, 2, 2, 1,
+                                Tens{mix_ + lab0 * SE, false}, SE);
     p.act = kActRelu;
     SD_CHECK(p.Wo == C, kErrShape, "label and ref_speech(mix speech) diff");
     conv_gemm(p, bf, st);
   };
-  if (n_full) embed(feats, n_full, chunk);
-  if (tail) {
-    SD_CHECK(tail >= 2, kErrInvalid, "last chunk must hold >= 2 label frames (8 fbank frames)");
-    embed(feats + (int64_t)n_full * 4 * chunk * 80, 1, tail);
-  }
-  // ---- per-speaker encoder over S = NS sequences of T_lab tokens
-  build_stream_input(ts, mix_, T_lab, NS, SE, std::sqrt((float)E), pe_, chunk, left, X_, st);
-  run_layers(single_, X_, NS, T_lab, chunk, left, st);
-  speakers_to_channels(X_, 1, NS, T_lab, E, X2_, bf, st);
   // ---- backend_down over each chunk alone (zero padding at the chunk edges)
-  auto down = [&](int r0, int B, int C) {
-    ConvGemmArgs p = cam_conv1d(act_at(Tens{X2_, bf}, (int64_t)r0 * NS * E), B, C, NS * E, backend_down_, 1, 2, 1,
-                                Tens{X_ + (int64_t)r0 * E, false}, E);
+  auto down = [&](int64_t lab0, int nb, int C) {
+    ConvGemmArgs p = cam_conv1d(act_at(Tens{X2_, bf}, lab0 * NS * E), nb, C, NS * E, backend_down_, 1, 2, 1,
+                                Tens{X_ + lab0 * E, false}, E);
     p.act = kActRelu;
     conv_gemm(p, bf, st);
   };
-  if (n_full) down(0, n_full, chunk);
-  if (tail) down(n_full * chunk, 1, tail);
+  auto per_chunk_runs = [&](const std::function<void(int64_t, int, int)>& f) {
+    if (!tail) {
+      f(0, B * n_full, chunk);
+      return;
+    }
+    for (int b = 0; b < B; ++b) {
+      const int64_t w0 = (int64_t)b * T_lab;
+      if (n_full) f(w0, n_full, chunk);
+      f(w0 + (int64_t)n_full * chunk, 1, tail);
+    }
+  };
+  per_chunk_runs(embed);
+  // ---- per-speaker encoder over S = B * NS sequences of T_lab tokens
+  build_stream_input(ts, mix_, B, T_lab, NS, SE, std::sqrt((float)E), pe_, chunk, left, X_, st);
+  run_layers(single_, X_, B * NS, T_lab, chunk, left, st);
+  speakers_to_channels(X_, B, NS, T_lab, E, X2_, bf, st);
+  per_chunk_runs(down);
   // ---- multi-speaker encoder (no positional encoding: model.py:853-858) + fc
-  run_layers(multi_, X_, 1, T_lab, chunk, left, st);
-  ConvGemmArgs f = cam_conv1d(Tens{X_, false}, 1, T_lab, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
+  run_layers(multi_, X_, B, T_lab, chunk, left, st);
+  ConvGemmArgs f = cam_conv1d(Tens{X_, false}, B, T_lab, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
   f.o_sb = (int64_t)NS * T_lab; f.o_sw = 1; f.o_sn = T_lab;
   conv_gemm(f, bf, st);
 }

@@ -16,7 +16,8 @@ namespace sd {
 
 struct TsvadStreamConfig {
   int max_num_speaker = 4;
-  int max_labels = 200;        // label frames (25 Hz) per forward
+  int max_labels = 200;        // label frames (25 Hz) per window
+  int max_windows = 1;         // windows per forward
   bool bf16 = false;
   int num_transformer_layer = 2;
   int num_attention_head = 4;
@@ -38,10 +39,11 @@ class TsvadStreamModel {
   void finalize();
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
-  // feats (4 * T_lab, 80) fbank of one window (padded to 4 x labels, model.py:614-618);
-  // ts (NS, 192); chunk = decoding_chunk_size (label frames), left = num_decoding_left_chunks;
-  // logits (NS, T_lab) pre-sigmoid.
-  void forward(const float* feats, const float* ts, int T_lab, int chunk, int left, float* logits, hipStream_t st);
+  // B independent windows: feats (B, 4 * T_lab, 80) fbank (padded to 4 x labels,
+  // model.py:614-618); ts (B, NS, 192); chunk = decoding_chunk_size (label frames),
+  // left = num_decoding_left_chunks; logits (B, NS, T_lab) pre-sigmoid.
+  void forward(const float* feats, const float* ts, int B, int T_lab, int chunk, int left, float* logits,
+               hipStream_t st);
 
  private:
   WenetLayerL load_layer(const std::string& prefix);

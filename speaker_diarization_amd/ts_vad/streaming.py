@@ -7,6 +7,8 @@ and its `forward_chunk_by_chunk_temp1` alias (the one `infer_debug` calls with
 simulate_streaming, model.py:951-975), both B = 1 like the reference (`forward_chunk` asserts
 it, :720).  libsdiar decodes the whole window in one call: the KV caches of the reference's
 chunk loop become block-causal attention masks (include/sdiar.h, sd_tsvad_stream_*).
+`forward_windows` decodes a batch of independent windows in one call (what infer.py's window
+loop does one window at a time, infer_debug batch 1).
 """
 from __future__ import annotations
 
@@ -20,7 +22,7 @@ from ..weights import TSVADStreamingConfig, unwrap_checkpoint
 
 class TSVADStreamingModel:
     def __init__(self, cfg: TSVADStreamingConfig = None, device=None, precision: str = "bf16",
-                 max_labels: int = 400):
+                 max_labels: int = 400, max_windows: int = 1):
         import torch
         self.cfg = cfg or TSVADStreamingConfig()
         if precision not in ("bf16", "fp32"):
@@ -28,7 +30,7 @@ class TSVADStreamingModel:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
             raise ValueError("TSVADStreamingModel (MI355X backend) runs on a HIP device only")
-        self.precision, self.max_labels = precision, max_labels
+        self.precision, self.max_labels, self.max_windows = precision, max_labels, max_windows
         self.max_num_speaker = self.cfg.max_num_speaker
         self.subsampling_rate = 4   # Subsampling4 (model.py:1318)
         c = self.cfg
@@ -36,7 +38,7 @@ class TSVADStreamingModel:
             max_num_speaker=c.max_num_speaker, max_labels=max_labels, precision=1 if precision == "bf16" else 0,
             num_transformer_layer=c.num_transformer_layer, num_attention_head=c.num_attention_head,
             transformer_embed_dim=c.transformer_embed_dim, transformer_ffn_embed_dim=c.transformer_ffn_embed_dim,
-            speaker_embed_dim=c.speaker_embed_dim)
+            speaker_embed_dim=c.speaker_embed_dim, max_windows=max_windows)
         h = ctypes.c_void_p()
         _lib.call("sd_tsvad_stream_create", ctypes.byref(conf), ctypes.byref(h))
         self._h = h
@@ -85,8 +87,51 @@ class TSVADStreamingModel:
         assert ts.shape == (self.max_num_speaker, self.cfg.speaker_embed_dim)
         if out is None:
             out = torch.empty(1, self.max_num_speaker, T_lab, device=self.device, dtype=torch.float32)
-        _lib.call("sd_tsvad_stream_forward", self._h, _lib.ptr(x), _lib.ptr(ts), T_lab, int(decoding_chunk_size),
+        _lib.call("sd_tsvad_stream_forward", self._h, _lib.ptr(x), _lib.ptr(ts), 1, T_lab, int(decoding_chunk_size),
+                  int(num_decoding_left_chunks), _lib.ptr(out), _lib.stream_ptr(self.device))
+        return out
+
+    def forward_windows(self, xs, target_speech, T_lab: int, decoding_chunk_size: int,
+                        num_decoding_left_chunks: int = -1, out=None):
+        """B windows at once: xs (B, 4 * T_lab, 80) fbank on the device, target_speech (B, NS, 192)
+        -> logits (B, NS, T_lab); window b equals forward_chunk_by_chunk on window b alone."""
+        import torch
+        B = xs.shape[0]
+        assert decoding_chunk_size > 0
+        assert xs.shape[1:] == (self.subsampling_rate * T_lab, 80), xs.shape
+        assert target_speech.shape == (B, self.max_num_speaker, self.cfg.speaker_embed_dim)
+        assert xs.device == self.device and xs.dtype == torch.float32 and xs.is_contiguous()
+        ts = target_speech.to(self.device, torch.float32).contiguous()
+        if out is None:
+            out = torch.empty(B, self.max_num_speaker, T_lab, device=self.device, dtype=torch.float32)
+        _lib.call("sd_tsvad_stream_forward", self._h, _lib.ptr(xs), _lib.ptr(ts), B, T_lab, int(decoding_chunk_size),
                   int(num_decoding_left_chunks), _lib.ptr(out), _lib.stream_ptr(self.device))
         return out
 
     forward_chunk_by_chunk_temp1 = forward_chunk_by_chunk
+
+
+class StreamingWindowDecoder:
+    """Adapter that lets ts_vad.pipeline.TSVADPipeline (window plan, device fbank + window CMN,
+    overlap average) drive the chunk-streaming model: the streaming recipe's decode
+    (run_ts_vad2_streaming.sh: rs_len 10, segment_shift 1, decoding_chunk_size 25,
+    num_decoding_left_chunks -1; infer.py window loop -> infer_debug -> forward_chunk_by_chunk_temp1).
+    Each batch of windows is padded / trimmed to 4 x labels (model.py:614-618) and decoded in one
+    sd_tsvad_stream_forward call."""
+
+    def __init__(self, model: TSVADStreamingModel, decoding_chunk_size: int = 25, num_decoding_left_chunks: int = -1,
+                 rs_len: int = 10, label_rate: int = 25, sample_rate: int = 16000):
+        from types import SimpleNamespace
+        self.model = model
+        self.cfg = SimpleNamespace(rs_len=rs_len, label_rate=label_rate, sample_rate=sample_rate)
+        self.max_batch = model.max_windows
+        self.max_num_speaker = model.max_num_speaker
+        self.device = model.device
+        self.chunk, self.left = decoding_chunk_size, num_decoding_left_chunks
+
+    def forward(self, ref, ts, T_lab: int):
+        import torch
+        n = self.model.subsampling_rate * T_lab
+        if ref.shape[1] != n:
+            ref = torch.nn.functional.pad(ref, (0, 0, 0, n - ref.shape[1]))
+        return self.model.forward_windows(ref.contiguous(), ts, T_lab, self.chunk, self.left)

@@ -57,3 +57,24 @@ def test_stream_errors(gpu):
     bad.pop("fc.bias")
     with pytest.raises(RuntimeError, match="fc.bias"):
         TSVADStreamingModel(device=gpu, max_labels=64).load_state_dict(bad)
+
+
+@pytest.mark.parametrize("T_lab,dcs,left", [(250, 25, -1), (100, 25, 1), (70, 25, -1), (64, 10, 0)])
+def test_stream_windows_batch(gpu, T_lab, dcs, left):
+    """forward_windows over B windows == forward_chunk_by_chunk on each window alone (with and
+    without a partial last chunk), and window 0 vs the oracle's chunk loop."""
+    from oracle.tsvad_stream_ref import forward_chunk_by_chunk
+    sd = tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=91)
+    B = 3
+    m = TSVADStreamingModel(device=gpu, precision="fp32", max_labels=T_lab, max_windows=B).load_state_dict(to_torch(sd))
+    xs = np.stack([tsvad_stream_inputs(4 * T_lab, 100 + b)[0][0] for b in range(B)])
+    ts = np.stack([tsvad_stream_inputs(4 * T_lab, 100 + b)[1][0] for b in range(B)])
+    y = m.forward_windows(torch.from_numpy(xs).to(gpu), torch.from_numpy(ts), T_lab, dcs, left).cpu().numpy()
+    for b in range(B):
+        yb = m.forward_chunk_by_chunk(torch.from_numpy(xs[b:b + 1]), torch.from_numpy(ts[b:b + 1]), T_lab, dcs,
+                                      left).cpu().numpy()
+        assert np.abs(y[b:b + 1] - yb).max() < 1e-5, b
+    with torch.no_grad():
+        ref = forward_chunk_by_chunk(to_torch(sd), torch.from_numpy(xs[:1]), torch.from_numpy(ts[:1]), T_lab, dcs,
+                                     left).numpy()
+    assert np.abs(y[:1] - ref).max() < 1e-3
