@@ -395,6 +395,9 @@ def main_eend(a, wl):
                 "config": {"workload": wl["desc"], "minutes_per_gpu": minutes,
                            "parallelism": ("chunk-shard x%d + RCCL all-gather" % world if kind == "eda" else
                                            "replicas x%d" % world) if world > 1 else "1 GPU"}}
+        if kind == "tsvad_stream" and world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = tss_cpu_baseline(meeting, plan, wl)
+            line["speedup_vs_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
         if kernels:
             tot = sum(v["ms"] for v in kernels.values())
             line["kernel_ms_share"] = {k: round(v["ms"] / tot, 3) for k, v in
@@ -404,6 +407,33 @@ def main_eend(a, wl):
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def tss_cpu_baseline(meeting, plan, wl, n_win=8):
+    """The reference's streaming decode on the host: oracle/tsvad_stream_ref.py (the literal
+    forward_chunk_by_chunk_temp1 cache loop, one window per call like infer_debug) over the
+    first n_win windows of the same meeting (window fbank + CMN, oracle/fbank_ref.py), fp32,
+    16 torch threads.  Meeting frames/s = windows/s x (meeting frames / windows)."""
+    import torch
+    from oracle.fbank_ref import window_fbank
+    from oracle.tsvad_stream_ref import forward_chunk_by_chunk
+    from speaker_diarization_amd.synth import speaker_embeddings
+    from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
+    torch.set_num_threads(16)
+    sd = to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=777))
+    ts = torch.from_numpy(speaker_embeddings(4, seed=777))[None]
+    spl = plan.samples_per_label
+    wins = [(torch.from_numpy(window_fbank(meeting.wav[int(plan.starts[w]) * spl:int(plan.ends[w]) * spl]))[None],
+             int(plan.lens[w])) for w in range(min(n_win, plan.n_win))]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for f, n in wins:
+            forward_chunk_by_chunk(sd, f, ts, n, wl["chunk"], wl["left"])
+    dt = time.perf_counter() - t0
+    frames_per_win = (meeting.wav.size // 160) / plan.n_win
+    return dict(value=round(len(wins) * frames_per_win / dt, 2), unit="frames/s", cores=16, kind="port",
+                sample="first %d windows (10 s each) of the same meeting through oracle/tsvad_stream_ref.py "
+                       "(literal chunk loop with KV caches, fp32, 16 host threads): %.1f s" % (len(wins), dt))
 
 
 def main_stream(a, wl):
