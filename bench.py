@@ -47,7 +47,8 @@ WORKLOADS = {
     "tss": dict(kind="tsvad_stream", n_spk=4, minutes=10.0, chunk=25, left=-1,
                 desc="Chunk-streaming TS-VAD (ts_vad2_streaming, run_ts_vad2_streaming.sh decode: rs_len 10 s, "
                      "segment_shift 1 s, decoding_chunk_size 25 (1 s), num_decoding_left_chunks -1, "
-                     "simulate_streaming), 4 speakers, 64 windows per call; replicas only"),
+                     "simulate_streaming), 4 speakers, reference batches of 64 windows fused 4 per device call; "
+                     "replicas only"),
     "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
                 desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
                      "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
@@ -331,7 +332,8 @@ def main_eend(a, wl):
         from speaker_diarization_amd.ts_vad.streaming import StreamingWindowDecoder, TSVADStreamingModel
         from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
         meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank)
-        m = TSVADStreamingModel(device=dev, precision=prec, max_labels=250, max_windows=64)
+        n_dev = int(os.environ.get("SDIAR_TSS_WINDOWS", "256"))   # windows per device call (64: 61.8 ms)
+        m = TSVADStreamingModel(device=dev, precision=prec, max_labels=250, max_windows=n_dev)
         m.load_state_dict(to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=777)))
         pipe = TSVADPipeline(StreamingWindowDecoder(m, wl["chunk"], wl["left"]), segment_shift=1, batch_size=64)
         wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
