@@ -8,15 +8,22 @@ segment_shift 1 s, 64 windows per batch, bf16 MFMA.  One step = the whole hot
 path over one meeting: wav already in HBM -> kaldi fbank -> window CMN -> model
 -> sigmoid + overlap-average posteriors (NS, 25 Hz frames).
 
-N GPUs (torchrun, one process per GPU, RCCL): weak scaling — the meeting is N x
-the per-rank length, windows are sharded by contiguous batch ranges and the
-per-window logits are all-gathered (the only exchange) before averaging.
+N GPUs (torchrun, one process per GPU, RCCL): STRONG scaling by default — one
+fixed long meeting (60 min, the C4 long-form shape of BASELINE.json) with the
+headline model, its windows sharded by contiguous ranges of the global 64-window
+batch grid; each rank runs the sub-span fbank + its windows, and the per-window
+logits are all-gathered (the only exchange) before the ordered overlap average.
+`--scaling weak` restores N x 10-min meetings.  `--workload c4` runs the C4 model
+(CAM++ + transformer, rs_len 4) on the same 60-min strong-scaling meeting.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
+import subprocess
 import sys
 import time
 
@@ -28,8 +35,9 @@ sys.path.insert(0, HERE)
 WORKLOADS = {
     "c2": dict(variant=1, rs_len=6, minutes=10.0, desc="C2: AliMeeting-shaped 4-spk meeting, TS-VAD "
                "CAM++_ots_vad + 6-layer Conformer + BiLSTM (ots_vad_style v1), rs_len 6 s, shift 1 s"),
-    "c4": dict(variant=0, rs_len=4, minutes=60.0, desc="C4: 4-spk long-form meeting, TS-VAD CAM++ + "
-               "transformer (default TSVADConfig), rs_len 4 s, shift 1 s"),
+    "c4": dict(variant=0, rs_len=4, minutes=60.0, strong=True,
+               desc="C4: 4-spk long-form meeting, TS-VAD CAM++ + transformer (default TSVADConfig), "
+                    "rs_len 4 s, shift 1 s"),
     # secondary workloads (EEND family); not the BASELINE headline line
     "c1": dict(kind="eda", model_type="TransformerEda", layers=2, n_spk=2, minutes=10.0, num_speakers=2,
                desc="C1: 2-spk 16 kHz recording, EEND-EDA TransformerEda 2-layer (infer_eda.py: logmel23_mn, "
@@ -47,8 +55,8 @@ WORKLOADS = {
     "tss": dict(kind="tsvad_stream", n_spk=4, minutes=10.0, chunk=25, left=-1,
                 desc="Chunk-streaming TS-VAD (ts_vad2_streaming, run_ts_vad2_streaming.sh decode: rs_len 10 s, "
                      "segment_shift 1 s, decoding_chunk_size 25 (1 s), num_decoding_left_chunks -1, "
-                     "simulate_streaming), 4 speakers, reference batches of 64 windows fused 4 per device call; "
-                     "replicas only"),
+                     "simulate_streaming), 4 speakers, every window decoded at its own length, 256 windows "
+                     "per device call; replicas only"),
     "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
                 desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
                      "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
@@ -57,6 +65,7 @@ WORKLOADS = {
 
 PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                        # GB/s
+ATTN_KERNELS = ("attention_bf16", "attention_f32")
 
 
 def parse():
@@ -65,11 +74,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--minutes", type=float, default=None, help="meeting minutes per GPU")
+    ap.add_argument("--minutes", type=float, default=None,
+                    help="weak scaling: meeting minutes per GPU; strong scaling: total meeting minutes")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="default: strong (fixed 60-min meeting) when WORLD_SIZE > 1, else one 10-min meeting")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64, help="reference batch (windows, zero-pad unit)")
     ap.add_argument("--device-batch", type=int, default=640, help="windows per device launch (a 10-min meeting in one launch)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline budget (3 timed runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--chunk", type=int, default=None, help="c5s: model frames per streaming push")
@@ -77,16 +89,73 @@ def parse():
     return ap.parse_args()
 
 
-def roofline_of(name, st):
-    """Roofline of one kernel family from the live HIP-event timer: the bound is the roof the
-    family's algorithmic work sits closer to (max(flops/peak_flops,
+# ----------------------------------------------------------------------------- host facts
+def _cgroup_cpus():
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except Exception:
+        return None
+
+
+def host_threads():
+    """Threads for the CPU baseline: every host core this process may use (BASELINE.md §2:
+    os.cpu_count()), capped by the cgroup CPU quota and OMP_NUM_THREADS (the GPU box
+    grants one GPU's job a 16-CPU share of a much larger machine)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except Exception:
+        pass
+    cg = _cgroup_cpus()
+    if cg:
+        n = min(n, cg)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def host_info(threads):
+    model = platform.processor() or ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        nproc = None
+    return {"cores": threads, "nproc": nproc, "os_cpu_count": os.cpu_count(), "cgroup_cpus": _cgroup_cpus(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model}
+
+
+def median3(fn):
+    """one warm-up run (done by the caller), then the median of 3."""
+    ts = []
+    out = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), ts, out
+
+
+# ----------------------------------------------------------------------------- rooflines
+def roofline_of(name, st, traffic=None):
+    """Roofline of one kernel from the live HIP-event timer: the bound is the roof the
+    kernel's algorithmic work sits closer to (max(flops/peak_flops,
     bytes/peak_bw) over the measured time), and `achieved` is quoted in that roof's unit."""
     secs = st["ms"] * 1e-3
-    dt = "bf16" if name.endswith("bf16") else "f32"
+    dt = "f32" if name.endswith("f32") else "bf16"
     tf = st["flops"] / secs / 1e12 if st["flops"] > 0 else 0.0
     gbs = st["bytes"] / secs / 1e9
     f_mfma, f_hbm = tf / PEAKS[dt], gbs / HBM_PEAK
-    common = dict(traffic=None, kernel=name, launches=st["launches"],
+    common = dict(traffic=traffic, kernel=name, launches=st["launches"],
                   avg_launch_ms=round(st["ms"] / st["launches"], 4),
                   flops_per_launch=st["flops"] / st["launches"],
                   algorithmic_bytes_per_launch=round(st["bytes"] / st["launches"]),
@@ -97,28 +166,141 @@ def roofline_of(name, st):
     return dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK, unit="GB/s", frac=round(f_hbm, 4), **common)
 
 
-def cpu_baseline(cfg, sd_np, meeting, ts, target_s):
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None
+    try:
+        return json.load(open(pmc)).get(workload, {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def live_kernels(step):
+    """One extra step under the libsdiar HIP-event timer (events on the launch stream)."""
+    import torch
+    from speaker_diarization_amd import _lib
+    lib = _lib.load()
+    lib.sd_prof_reset()
+    lib.sd_prof_enable(1)
+    step()
+    torch.cuda.synchronize()
+    lib.sd_prof_enable(0)
+    kernels = _lib.prof_stats()
+    lib.sd_prof_reset()
+    return kernels
+
+
+def kernel_report(kernels, workload, ms_per_step, precision):
+    """roofline (dominant single kernel), attention_roofline, whole-step work and a
+    per-kernel table, all from the live timer."""
+    if not kernels:
+        return {}
+    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    out = {"roofline": roofline_of(dom, kernels[dom], pmc_traffic(workload, dom))}
+    att = [k for k in ATTN_KERNELS if k in kernels]
+    if att:
+        out["attention_roofline"] = roofline_of(att[0], kernels[att[0]], pmc_traffic(workload, att[0]))
+    flops = sum(v["flops"] for v in kernels.values())
+    byts = sum(v["bytes"] for v in kernels.values())
+    kms = sum(v["ms"] for v in kernels.values())
+    dt = "f32" if precision == "fp32" else "bf16"
+    s = ms_per_step * 1e-3
+    out["step_work"] = {"algorithmic_gflop_per_step": round(flops / 1e9, 2),
+                        "algorithmic_gb_per_step": round(byts / 1e9, 3),
+                        "kernel_ms_per_step": round(kms, 3), "ms_per_step": round(ms_per_step, 3),
+                        "achieved_tflops": round(flops / s / 1e12, 1), "mfma_frac": round(flops / s / 1e12 / PEAKS[dt], 4),
+                        "achieved_gbs": round(byts / s / 1e9, 1), "hbm_frac": round(byts / s / 1e9 / HBM_PEAK, 4)}
+    tab = {}
+    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:14]:
+        r = roofline_of(k, v)
+        tab[k] = {"share": round(v["ms"] / kms, 3), "ms": round(v["ms"], 3), "launches": v["launches"],
+                  "bound": r["bound"], "frac": r["frac"]}
+    out["kernels"] = tab
+    return out
+
+
+# ----------------------------------------------------------------------------- distributed helpers
+def dist_setup():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def timed(step, warmup, steps, world, dev):
+    """W untimed warm-up steps, then exactly K steps bracketed by barrier + synchronize on
+    both sides; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+# ----------------------------------------------------------------------------- TS-VAD (C2 / C4)
+def cpu_baseline(cfg, sd_np, meeting, ts, budget_s):
     """The CPU oracle (PyTorch-CPU restatement of the reference inference loop,
-    parity-pinned by tests/golden) on a bounded sample of the same meeting."""
+    parity-pinned by tests/golden) on a bounded sample of the same meeting, BASELINE.md §2
+    protocol: all usable host cores, 1 warm-up + median of 3, model-only (wav -> posteriors)
+    and end-to-end (-> RTTM text at the 10 recipe thresholds, oracle/postprocess_ref.py)."""
     import torch
     from oracle.pipeline_ref import meeting_posteriors
+    from oracle.postprocess_ref import rttm_lines
     from speaker_diarization_amd.weights import to_torch
+    threads = host_threads()
+    torch.set_num_threads(threads)
     sd = to_torch(sd_np)
-    threads = torch.get_num_threads()
     n_lab = meeting.labels.shape[1]
     probe = 8
-    t0 = time.perf_counter()
+    t0 = time.perf_counter()      # the warm-up run also sizes the sample
     meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=probe, max_windows=probe)
     per_win = (time.perf_counter() - t0) / probe
-    n = int(max(probe, min(256, target_s / max(per_win, 1e-6))))
+    n = int(max(probe, min(320, budget_s / 3.0 / max(per_win, 1e-6))))
     n = max(probe, (n // probe) * probe)
-    t0 = time.perf_counter()
-    post = meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=min(64, n), max_windows=n)
-    dt = time.perf_counter() - t0
-    frames = n * 100 * 1   # each window advances the meeting by segment_shift (1 s) = 100 frames
-    return dict(value=frames / dt, unit="frames/s", cores=threads, kind="port",
+    post = {}
+
+    def model_only():
+        post["p"] = meeting_posteriors(sd, cfg, meeting.wav, ts, n_lab, shift=1, batch_size=min(64, n),
+                                       max_windows=n)
+    t_model, runs, _ = median3(model_only)
+    span = n * 100 // 4   # label frames fully covered by the sample's windows (1 window per second)
+    keys = {f"{meeting.name}-{i + 1}": post["p"][i, :span] for i in range(4)}
+    t_post, _, _ = median3(lambda: rttm_lines(keys))
+    frames = n * 100          # each window advances the meeting by segment_shift (1 s) = 100 frames
+    info = host_info(threads)
+    return dict(value=round(frames / t_model, 2), unit="frames/s", kind="port",
+                end_to_end_value=round(frames / (t_model + t_post), 2),
                 sample=f"first {n} windows ({n} s of meeting, fp32, batch {min(64, n)}) of the same meeting "
-                       f"through oracle/pipeline_ref.py on {threads} host threads: {dt:.1f} s"), post, n
+                       f"through oracle/pipeline_ref.py (+ oracle/postprocess_ref.py for end-to-end) on "
+                       f"{threads} host threads; 1 warm-up + median of 3 runs "
+                       f"({', '.join('%.2f' % r for r in runs)} s model-only, {t_post:.3f} s RTTM)",
+                **info), post["p"], n
 
 
 def der_parity(meeting, gpu_post, cpu_post, span_s, n_real=4, label_rate=25):
@@ -148,35 +330,27 @@ def der_parity(meeting, gpu_post, cpu_post, span_s, n_real=4, label_rate=25):
             "note": "seeded random weights: absolute DER is meaningless, the GPU-vs-reference difference is the check"}
 
 
-def main():
-    a = parse()
+def main(a, wl):
     import torch
-    import torch.distributed as dist
-    from speaker_diarization_amd import _lib
     from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
     from speaker_diarization_amd.ts_vad.model import TSVADModel
     from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    from speaker_diarization_amd.ts_vad.postprocess import posteriors_to_rttm_gpu
     from speaker_diarization_amd.weights import TSVADConfig, to_torch, tsvad_state_dict
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
-    wl = WORKLOADS[a.workload]
-    minutes = a.minutes if a.minutes is not None else wl["minutes"]
+    world, rank, dev = dist_setup()
+    scaling = a.scaling or ("strong" if (world > 1 or wl.get("strong")) else "weak")
+    if scaling == "strong":
+        total_min = a.minutes if a.minutes is not None else 60.0
+    else:
+        total_min = (a.minutes if a.minutes is not None else wl["minutes"]) * world
     cfg = TSVADConfig(rs_len=wl["rs_len"]) if wl["variant"] == 0 else TSVADConfig.ots_vad_v1(rs_len=wl["rs_len"])
     sd_np = tsvad_state_dict(cfg, seed=777)
     model = TSVADModel(cfg, device=dev, precision=a.precision, max_batch=max(a.batch, a.device_batch))
     model.load_state_dict(to_torch(sd_np))
     pipe = TSVADPipeline(model, segment_shift=1, batch_size=a.batch)
 
-    total_s = minutes * 60.0 * world
-    meeting = make_meeting(total_s, n_spk=4, seed=777)
+    meeting = make_meeting(total_min * 60.0, n_spk=4, seed=777)
     ts_np = speaker_embeddings(4, seed=777)
     wav = torch.from_numpy(meeting.wav).to(dev)
     ts = torch.from_numpy(ts_np).to(dev)
@@ -186,50 +360,20 @@ def main():
     def step():
         return pipe.posteriors(wav, ts, n_lab)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        post = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, post = timed(step, a.warmup, a.steps, world, dev)
     ms_per_step = elapsed / a.steps * 1000.0
     value = frames_per_step * a.steps / elapsed
 
-    # Live kernel timing (HIP events on the launch stream) over one extra step.
-    roofline, kernels = None, None
-    if not a.no_kernel_timing:
-        lib = _lib.load()
-        lib.sd_prof_reset()
-        lib.sd_prof_enable(1)
-        step()
-        torch.cuda.synchronize()
-        lib.sd_prof_enable(0)
-        kernels = _lib.prof_stats()
-        lib.sd_prof_reset()
-        dom = max(kernels, key=lambda k: kernels[k]["ms"])
-        st = kernels[dom]
-        avg_ms = st["ms"] / st["launches"]
-        roofline = roofline_of(dom, st)
-        pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                tr = json.load(open(pmc)).get(a.workload, {}).get(dom)
-                if tr:
-                    roofline["traffic"] = tr
-            except Exception:
-                pass
+    # End-to-end (wav in HBM -> RTTM text at the 10 recipe thresholds): median of 3.
+    keys = [f"{meeting.name}-{i + 1}" for i in range(4)]
+
+    def e2e():
+        p = pipe.posteriors(wav, ts, n_lab)
+        return posteriors_to_rttm_gpu(keys, p) if rank == 0 else None
+    e2e()
+    t_e2e, _, _ = median3(e2e)
+
+    kernels = None if a.no_kernel_timing else live_kernels(step)
 
     cpu, der = None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -237,6 +381,7 @@ def main():
         der = der_parity(meeting, post, cpu_post, float(n_cpu))
 
     if rank == 0:
+        plan = pipe.plan(n_lab)
         line = {
             "metric": "diarized frames/sec (10 ms hop)",
             "value": round(value, 1),
@@ -246,51 +391,128 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": a.precision,
             "data": "synthetic 16 kHz 4-speaker meeting (speaker_diarization_amd/synth.py), seeded random "
                     "weights of the reference architecture",
-            "config": {"workload": wl["desc"], "meeting_minutes": minutes * world,
-                       "minutes_per_gpu": minutes, "windows": pipe.plan(n_lab).n_win,
-                       "global_batch": a.batch * world, "batch_per_gpu": a.batch,
-                       "device_batch": max(a.batch, a.device_batch),
-                       "parallelism": f"window-shard x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "der": der,
+            "config": {"workload": wl["desc"], "meeting_minutes": total_min,
+                       "minutes_per_gpu": round(total_min / world, 3), "windows": plan.n_win,
+                       "global_batch": a.batch, "device_batch": max(a.batch, a.device_batch),
+                       "parallelism": (f"window-shard x{world} on the 64-window batch grid + RCCL all-gather of "
+                                       f"window logits" if world > 1 else "1 GPU")},
+            "end_to_end": {"ms_per_step": round(t_e2e * 1e3, 3), "value": round(frames_per_step / t_e2e, 1),
+                           "what": "wav in HBM -> posteriors -> GPU medfilt/threshold/run-length -> RTTM lines "
+                                   "(10 thresholds), median of 3"},
         }
+        line.update(kernel_report(kernels, a.workload, ms_per_step, a.precision))
+        line["cpu_baseline"] = cpu
+        line["der"] = der
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-        if kernels:
-            tot = sum(v["ms"] for v in kernels.values())
-            line["kernel_ms_share"] = {k: round(v["ms"] / tot, 3) for k, v in
-                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
+            line["end_to_end"]["speedup_vs_cpu"] = round(frames_per_step / t_e2e / cpu["end_to_end_value"], 1)
         print(json.dumps(line))
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
-def main_eend(a, wl):
-    """EEND-EDA (c1/c3) and FS-EEND (c5): wav in HBM -> frontend -> model -> activities.
-    Multi-GPU: EEND-EDA shards chunks (all-gather of activities); FS-EEND runs replicas."""
+# ----------------------------------------------------------------------------- EEND family
+def eda_cpu_baseline(wl, meeting, sd_np, num_speakers):
+    """oracle/eend_ref.py (infer_eda.py:92-124 restated, fp32) over the whole recording."""
     import torch
-    import torch.distributed as dist
-    from speaker_diarization_amd import _lib
+    from oracle import eend_ref
+    from speaker_diarization_amd.weights import EDAConfig, to_torch
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    cfg = EDAConfig(model_type=wl["model_type"], n_speakers=wl["n_spk"], n_layers=wl["layers"])
+    sd = to_torch(sd_np)
+    wav = meeting.wav.astype(np.float64)
+
+    def run():
+        Y = eend_ref.features(wav)
+        outs = []
+        g = torch.Generator().manual_seed(777)
+        for s, e in eend_ref.gen_chunk_indices(len(Y), 2000):
+            src = [torch.from_numpy(np.ascontiguousarray(Y[s:e], np.float32))]
+            act, probs = eend_ref.infer_full(sd, cfg, src, eend_ref.chunk_perms([e - s], g))
+            try:
+                outs.append(eend_ref.select(act, probs, cfg.variant, num_speakers)[0])
+            except IndexError:        # the reference's top-n quirk; the forward has run
+                pass
+        return outs
+    run()
+    t, runs, _ = median3(run)
+    frames = meeting.wav.size // 160
+    return dict(value=round(frames / t, 2), unit="frames/s", kind="port",
+                sample=f"the whole {meeting.wav.size / 16000 / 60:.0f}-min recording through oracle/eend_ref.py "
+                       f"(librosa-restated frontend + encoder + EDA LSTMs, fp32) on {threads} threads; 1 warm-up "
+                       f"+ median of 3 ({', '.join('%.2f' % r for r in runs)} s)", **host_info(threads))
+
+
+def fseend_cpu_baseline(meeting, sd_np, budget_s):
+    """oracle/fseend_ref.py test() over the whole recording (one call, as fs_eend/model.py:198)."""
+    import torch
+    from oracle import eend_ref, fseend_ref
+    from speaker_diarization_amd.weights import FSEENDConfig, to_torch
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    cfg = FSEENDConfig()
+    sd = to_torch(sd_np)
+    Y = eend_ref.features(meeting.wav.astype(np.float64), 8000, 200, 80, 7, 10, "logmel23")
+    T = len(Y)
+    x = torch.from_numpy(np.ascontiguousarray(Y[:T], np.float32))[None]
+
+    def run():
+        with torch.no_grad():
+            return fseend_ref.fseend_test(sd, cfg, x, [T], 6)
+    run()
+    t, runs, _ = median3(run)
+    return dict(value=round(T * 10 / t, 2), unit="frames/s", kind="port",
+                sample=f"the whole recording ({T} model frames, {T / 10:.0f} s) through oracle/fseend_ref.py test() (fp32, "
+                       f"{threads} threads); 1 warm-up + median of 3 ({', '.join('%.2f' % r for r in runs)} s)",
+                **host_info(threads))
+
+
+def embed_cpu_baseline(wavs, sd_np, budget_s):
+    """oracle/tsvad_ref.extract_embed (FBank povey + CAM++ + stats pooling) on the first
+    speaker's enrollment audio, truncated to a bounded number of 6-s chunks."""
+    import torch
+    from oracle.tsvad_ref import extract_embed
+    from speaker_diarization_amd.weights import to_torch
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    sd = to_torch(sd_np)
+    w = wavs[0].cpu().numpy().astype(np.float64)
+    n_sec = 6 + 23      # 24 chunks of 6 s every 1 s
+    w = w[: n_sec * 16000 + 1]
+
+    def run():
+        with torch.no_grad():
+            return extract_embed(sd, w, batch_size=96)
+    run()
+    t, runs, out = median3(run)
+    return dict(value=round((len(w) // 160) / t, 2), unit="frames/s", kind="port",
+                sample=f"{out.shape[0]} chunks (first {n_sec} s of one speaker's audio) through oracle/tsvad_ref.py "
+                       f"extract_embed (fp32, {threads} threads); 1 warm-up + median of 3 "
+                       f"({', '.join('%.2f' % r for r in runs)} s)", **host_info(threads))
+
+
+def main_eend(a, wl):
+    """EEND-EDA (c1/c3), FS-EEND (c5), embeddings and streaming TS-VAD: wav in HBM ->
+    frontend -> model -> activities.  Multi-GPU: EEND-EDA shards chunks (all-gather of
+    activities); the others run replicas."""
+    import torch
     from speaker_diarization_amd.synth import make_meeting
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    world, rank, dev = dist_setup()
     minutes = a.minutes if a.minutes is not None else wl["minutes"]
     kind = wl["kind"]
     prec = a.precision
+    cpu_fn = None
+    extra = {}
     if kind == "eda":
-        from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, infer_recording
+        from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, infer_chunks, stitch
         from speaker_diarization_amd.eend_eda.models import EendEdaModel, TransformerEdaModel
         from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
         total_s = minutes * 60.0 * world          # weak scaling: chunks of an N x longer recording
@@ -299,21 +521,25 @@ def main_eend(a, wl):
         kw = dict(n_speakers=wl["n_spk"], in_size=345, n_heads=4, n_units=256, n_layers=wl["layers"],
                   precision=prec, max_seqs=32, max_frames=2000)
         m = TransformerEdaModel(**kw) if wl["model_type"] == "TransformerEda" else EendEdaModel(**kw)
-        cfg = EDAConfig(model_type=wl["model_type"], n_layers=wl["layers"])
+        cfg = EDAConfig(model_type=wl["model_type"], n_speakers=wl["n_spk"], n_layers=wl["layers"])
         sd_np = eda_state_dict(cfg, seed=777)
         m.load_state_dict(to_torch(sd_np))
         iargs = EdaInferArgs(num_speakers=wl["num_speakers"])
         wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
 
-        def step():
-            try:
-                return infer_recording(m, wav, iargs)
-            except (ValueError, IndexError):
-                # the reference's own selection quirks on random weights: threshold mode np.vstack of
-                # chunks with different speaker counts, TransformerEda top-n IndexError;
-                # the device forward of every chunk has completed either way
-                return None
+        def step():      # infer_eda.py:99-113 for every chunk: frontend, forward, selection
+            return infer_chunks(m, wav, iargs)
         frames = meeting.wav.size // 160
+
+        def cpu_fn():
+            return eda_cpu_baseline(wl, meeting, sd_np, wl["num_speakers"])
+
+        def after(out_chunks):   # the h5 stitch (infer_eda.py:115-121), outside the timed region
+            try:
+                extra["T_hat"] = list(stitch(out_chunks, iargs).shape)
+            except ValueError as e:
+                extra["T_hat"] = ("np.vstack ValueError, as the reference raises for chunks with different "
+                                  "threshold-selected speaker counts: %s" % str(e)[:80])
     elif kind == "embed":
         from speaker_diarization_amd.ts_vad.embedding import CAMPPlus, extract_embed
         from speaker_diarization_amd.weights import campplus_state_dict, to_torch
@@ -321,18 +547,22 @@ def main_eend(a, wl):
         wavs = [torch.from_numpy(make_meeting(per, n_spk=1, seed=900 + 10 * rank + i).wav.astype(np.float32)).to(dev)
                 for i in range(wl["n_spk"])]
         m = CAMPPlus(feat_dim=80, embedding_size=192, device=dev, precision=prec, max_batch=96)
-        m.load_state_dict(to_torch(campplus_state_dict(777, 192)))
+        sd_np = campplus_state_dict(777, 192)
+        m.load_state_dict(to_torch(sd_np))
 
         def step():
             return [extract_embed(w, m, batch_size=96) for w in wavs]
         frames = sum(w.numel() for w in wavs) // 160 * world
+
+        def cpu_fn():
+            return embed_cpu_baseline(wavs, sd_np, a.cpu_seconds)
     elif kind == "tsvad_stream":
         from speaker_diarization_amd.synth import speaker_embeddings
         from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
         from speaker_diarization_amd.ts_vad.streaming import StreamingWindowDecoder, TSVADStreamingModel
         from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
         meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank)
-        n_dev = int(os.environ.get("SDIAR_TSS_WINDOWS", "256"))   # windows per device call (64: 61.8 ms)
+        n_dev = int(os.environ.get("SDIAR_TSS_WINDOWS", "256"))   # windows per device call
         m = TSVADStreamingModel(device=dev, precision=prec, max_labels=250, max_windows=n_dev)
         m.load_state_dict(to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=777)))
         pipe = TSVADPipeline(StreamingWindowDecoder(m, wl["chunk"], wl["left"]), segment_shift=1, batch_size=64)
@@ -343,6 +573,9 @@ def main_eend(a, wl):
         def step():   # replicas: every rank decodes its own meeting
             return pipe.average(pipe.window_logits(wav, ts, plan), plan)
         frames = meeting.wav.size // 160 * world
+
+        def cpu_fn():
+            return tss_cpu_baseline(meeting, plan, wl)
     else:
         from speaker_diarization_amd.feature import eend_features
         from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
@@ -352,8 +585,7 @@ def main_eend(a, wl):
         n_sub = -(-((meeting.wav.size // 80)) // 10) + 1
         m = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=prec,
                                            max_seqs=1, max_frames=max(n_sub, 16), max_nspks=6)
-        cfg = FSEENDConfig()
-        sd_np = fseend_state_dict(cfg, seed=777)
+        sd_np = fseend_state_dict(FSEENDConfig(), seed=777)
         m.load_state_dict(to_torch(sd_np))
         wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
 
@@ -361,53 +593,31 @@ def main_eend(a, wl):
             f = eend_features(wav, 8000, 200, 80, "logmel23", 7, 10, ld=m.in_ld)
             return m.test_device(f[None], [f.shape[0]], 6, want_emb=False, want_attractors=False)
         frames = meeting.wav.size // 80 * world
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kernels = None
-    if not a.no_kernel_timing:
-        lib = _lib.load()
-        lib.sd_prof_reset()
-        lib.sd_prof_enable(1)
-        step()
-        torch.cuda.synchronize()
-        lib.sd_prof_enable(0)
-        kernels = _lib.prof_stats()
+
+        def cpu_fn():
+            return fseend_cpu_baseline(meeting, sd_np, a.cpu_seconds)
+    elapsed, out = timed(step, a.warmup, a.steps, world, dev)
+    if kind == "eda":
+        after(out)
+    ms_per_step = elapsed / a.steps * 1000.0
+    kernels = None if a.no_kernel_timing else live_kernels(step)
     if rank == 0:
         line = {"metric": "diarized frames/sec (10 ms hop)", "value": round(frames * a.steps / elapsed, 1),
                 "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-                "ms_per_step": round(elapsed / a.steps * 1000.0, 3), "higher_is_better": True,
+                "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": prec,
                 "data": "synthetic recording (speaker_diarization_amd/synth.py), seeded random weights",
                 "config": {"workload": wl["desc"], "minutes_per_gpu": minutes,
                            "parallelism": ("chunk-shard x%d + RCCL all-gather" % world if kind == "eda" else
                                            "replicas x%d" % world) if world > 1 else "1 GPU"}}
-        if kind == "tsvad_stream" and world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = tss_cpu_baseline(meeting, plan, wl)
+        line.update(extra)
+        line.update(kernel_report(kernels, a.workload, ms_per_step, prec))
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_fn()
             line["speedup_vs_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
-        if kernels:
-            tot = sum(v["ms"] for v in kernels.values())
-            line["kernel_ms_share"] = {k: round(v["ms"] / tot, 3) for k, v in
-                                       sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:10]}
-            dom = max(kernels, key=lambda k: kernels[k]["ms"])
-            line["roofline"] = roofline_of(dom, kernels[dom])
         print(json.dumps(line))
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
@@ -415,50 +625,50 @@ def tss_cpu_baseline(meeting, plan, wl, n_win=8):
     """The reference's streaming decode on the host: oracle/tsvad_stream_ref.py (the literal
     forward_chunk_by_chunk_temp1 cache loop, one window per call like infer_debug) over the
     first n_win windows of the same meeting (window fbank + CMN, oracle/fbank_ref.py), fp32,
-    16 torch threads.  Meeting frames/s = windows/s x (meeting frames / windows)."""
+    all usable host threads, 1 warm-up + median of 3.  Meeting frames/s = windows/s x
+    (meeting frames / windows)."""
     import torch
     from oracle.fbank_ref import window_fbank
     from oracle.tsvad_stream_ref import forward_chunk_by_chunk
     from speaker_diarization_amd.synth import speaker_embeddings
     from speaker_diarization_amd.weights import TSVADStreamingConfig, to_torch, tsvad_streaming_state_dict
-    torch.set_num_threads(16)
+    threads = host_threads()
+    torch.set_num_threads(threads)
     sd = to_torch(tsvad_streaming_state_dict(TSVADStreamingConfig(), seed=777))
     ts = torch.from_numpy(speaker_embeddings(4, seed=777))[None]
     spl = plan.samples_per_label
     wins = [(torch.from_numpy(window_fbank(meeting.wav[int(plan.starts[w]) * spl:int(plan.ends[w]) * spl]))[None],
              int(plan.lens[w])) for w in range(min(n_win, plan.n_win))]
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        for f, n in wins:
-            forward_chunk_by_chunk(sd, f, ts, n, wl["chunk"], wl["left"])
-    dt = time.perf_counter() - t0
+
+    def run():
+        with torch.no_grad():
+            for f, n in wins:
+                forward_chunk_by_chunk(sd, f, ts, n, wl["chunk"], wl["left"])
+    run()
+    t, runs, _ = median3(run)
     frames_per_win = (meeting.wav.size // 160) / plan.n_win
-    return dict(value=round(len(wins) * frames_per_win / dt, 2), unit="frames/s", cores=16, kind="port",
+    return dict(value=round(len(wins) * frames_per_win / t, 2), unit="frames/s", kind="port",
                 sample="first %d windows (10 s each) of the same meeting through oracle/tsvad_stream_ref.py "
-                       "(literal chunk loop with KV caches, fp32, 16 host threads): %.1f s" % (len(wins), dt))
+                       "(literal chunk loop with KV caches, fp32, %d host threads); 1 warm-up + median of 3 (%s s)"
+                       % (len(wins), threads, ", ".join("%.2f" % r for r in runs)), **host_info(threads))
 
 
 def main_stream(a, wl):
     """C5 latency mode: one recording per GPU streamed chunk by chunk through the C ABI
     (sd_fseend_stream_push on device feature rows); every push is synchronised, as a
     live caller waiting for each chunk's scores would be.  value = 10 ms frames/s of the
-    streamed recording (N replicas: summed); per-chunk latency percentiles alongside."""
+    streamed recording (N replicas: summed); per-chunk latency percentiles alongside.
+    Chunks are whole model frames: FS-EEND's model frame is 100 ms (8 kHz, hop 80,
+    subsampling 10), so BASELINE's 80 ms push is not realisable; 1 frame = 100 ms."""
     import ctypes
     import torch
-    import torch.distributed as dist
     from speaker_diarization_amd import _lib
     from speaker_diarization_amd.feature import eend_features
     from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
     from speaker_diarization_amd.synth import make_meeting
     from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    world, rank, dev = dist_setup()
     minutes = a.minutes if a.minutes is not None else wl["minutes"]
     chunk = a.chunk or wl["chunk"]
     meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank, sample_rate=8000)
@@ -494,23 +704,8 @@ def main_stream(a, wl):
         torch.cuda.synchronize()
         assert out + cnt.value == T, (out, cnt.value, T)
 
-    for _ in range(a.warmup):
-        step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, _ = timed(lambda: step(True), a.warmup, a.steps, world, dev)
+    lat[:] = lat[-(len(lat) // (a.warmup + a.steps)) * a.steps:]   # timed steps only
     # parity spot check of this very run against the whole-recording forward of the first
     # 2000 frames (its last 9 frames see zero look-ahead there, so they are not compared)
     Tc = min(T, 2000)
@@ -541,14 +736,16 @@ def main_stream(a, wl):
                 "max_abs_diff_vs_test": err}
         print(json.dumps(line))
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
     _a = parse()
-    if WORKLOADS[_a.workload].get("kind") == "fseend_stream":
-        main_stream(_a, WORKLOADS[_a.workload])
-    elif WORKLOADS[_a.workload].get("kind") in ("eda", "fseend", "embed", "tsvad_stream"):
-        main_eend(_a, WORKLOADS[_a.workload])
+    _wl = WORKLOADS[_a.workload]
+    if _wl.get("kind") == "fseend_stream":
+        main_stream(_a, _wl)
+    elif _wl.get("kind") in ("eda", "fseend", "embed", "tsvad_stream"):
+        main_eend(_a, _wl)
     else:
-        main()
+        main(_a, _wl)

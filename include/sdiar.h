@@ -276,6 +276,13 @@ int sd_window_cmn(const float* feats, int n_mels, const int* win_start, const in
  * every `dis` frames and span at most `chunk`.  out: device (NS, n_frames). */
 int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start,
                        const int* len, int dis, int chunk, int n_frames, float* out, void* stream);
+/* The same mean over already-sigmoided probabilities (the res_dict lists of
+ * TSVADModel.infer, model.py:945-966, averaged by infer.py:90-94): bit-identical to
+ * np.mean of each frame's float32 list in window order (float32 sum from 0 in window
+ * order, then one correctly rounded division by the count).  NaN where no window
+ * covers a frame. */
+int sd_overlap_mean(const float* probs, int n_win, int NS, int Tw, const int* start,
+                    const int* len, int dis, int chunk, int n_frames, float* out, void* stream);
 
 /* ------------------------------------------------------------------ postprocess
  * Replaces the host loop of ts_vad2/infer.py:72-130 (postprocess): per track

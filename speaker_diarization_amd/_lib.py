@@ -154,6 +154,8 @@ _SIGS = {
     "sd_window_cmn": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sd_overlap_average": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                    c_void_p, c_void_p]),
+    "sd_overlap_mean": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                c_void_p, c_void_p]),
     "sd_postprocess_segments": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "sd_op_add_layernorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_int,

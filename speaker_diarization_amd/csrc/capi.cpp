@@ -108,6 +108,10 @@ int sd_tsvad_create(const sd_tsvad_config* c, sd_tsvad** out) {
     SD_CHECK(c->variant == 0 || c->variant == 1, sd::kErrInvalid, "unknown TS-VAD variant");
     SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
     SD_CHECK(c->max_batch > 0 && c->max_fbank_frames > 0, sd::kErrInvalid, "bad workspace sizes");
+    SD_CHECK(c->max_num_speaker > 0 && c->num_transformer_layer >= 1 && c->transformer_ffn_embed_dim > 0 &&
+                 c->speaker_embed_dim > 0, sd::kErrInvalid, "bad model dimensions");
+    SD_CHECK(c->num_attention_head > 0 && c->transformer_embed_dim % c->num_attention_head == 0, sd::kErrInvalid,
+             "transformer_embed_dim must be divisible by num_attention_head");
     sd::TsvadConfig t;
     t.variant = c->variant;
     t.max_num_speaker = c->max_num_speaker;
@@ -368,6 +372,9 @@ int sd_tsvad_stream_create(const sd_tsvad_stream_config* c, sd_tsvad_stream** ou
              "bad workspace sizes");
     SD_CHECK(c->num_attention_head > 0 && c->transformer_embed_dim % c->num_attention_head == 0, sd::kErrInvalid,
              "transformer_embed_dim must be divisible by num_attention_head");
+    SD_CHECK(c->num_transformer_layer >= 1, sd::kErrInvalid, "num_transformer_layer must be >= 1");
+    SD_CHECK(c->transformer_ffn_embed_dim > 0 && c->speaker_embed_dim > 0, sd::kErrInvalid,
+             "transformer_ffn_embed_dim and speaker_embed_dim must be > 0");
     sd::TsvadStreamConfig t;
     t.max_num_speaker = c->max_num_speaker;
     t.max_labels = c->max_labels;
@@ -477,6 +484,14 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
   return guard([&] {
     SD_CHECK(dis > 0 && chunk > 0, sd::kErrInvalid, "overlap_average: bad window geometry");
     sd::overlap_average(logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out, S(stream));
+  });
+}
+
+int sd_overlap_mean(const float* probs, int n_win, int NS, int Tw, const int* start, const int* len, int dis,
+                    int chunk, int n_frames, float* out, void* stream) {
+  return guard([&] {
+    SD_CHECK(dis > 0 && chunk > 0, sd::kErrInvalid, "overlap_mean: bad window geometry");
+    sd::overlap_average(probs, n_win, NS, Tw, start, len, dis, chunk, n_frames, out, S(stream), false);
   });
 }
 

@@ -89,7 +89,7 @@ void EdaModel::finalize() {
   att_ = ws((int64_t)cfg_.max_seqs * cfg_.max_n_speakers * E);
   hT_ = ws((int64_t)cfg_.max_seqs * E);
   cT_ = ws((int64_t)cfg_.max_seqs * E);
-  lstm_work_ = ws(3 * (int64_t)cfg_.max_seqs * E);
+  lstm_work_ = ws(lstm_work_floats(cfg_.max_seqs, E, 1));
   finalized_ = true;
 }
 
@@ -119,10 +119,10 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   gather_rows(X_, S, T, E, perm, lengths, Y_, st);
   conv_gemm(lin(Tens{Y_, false}, rows, E, enc_ih_, enc_b_, Tens{G_, false}, 4 * E), bf, st);
   lstm_recurrence(G_, S, T, E, 1, enc_hh_, lengths, nullptr, nullptr, nullptr, 0, hT_, cT_, lstm_work_, st,
-                  enc_hh_bf_);
+                  enc_hh_bf_, lstm_err_.get());
   fill_rows(dec_b_, 4 * E, S * NA, Gd_, st);
   lstm_recurrence(Gd_, S, NA, E, 1, dec_hh_, nullptr, hT_, cT_, att_, E, nullptr, nullptr, lstm_work_, st,
-                  dec_hh_bf_);
+                  dec_hh_bf_, lstm_err_.get());
   attractor_scores(X_, S, T, E, att_, NA, lin_w_, lin_b_, probs, act, st);
 }
 

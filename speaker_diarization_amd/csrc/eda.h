@@ -44,6 +44,7 @@ class EdaModel {
   EdaConfig cfg_;
   ParamStore ps_;
   DeviceArena arena_;
+  PinnedFlag lstm_err_;   // deferred poll-timeout report of the persistent LSTM (lstm.hip)
   bool finalized_ = false;
   int in_ld_ = 352;
 

@@ -288,35 +288,35 @@ void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st) {
   const double flops = 2.0 * M * p.N * (double)p.K;
   const double bytes = ab * p.B * p.H * p.W * p.Cin + 2.0 * p.N * p.K + ob * M * p.N +
                        (p.res ? (p.res_bf16 ? 2.0 : 4.0) * M * p.N : 0.0);
+  // Path selection first, so the live timer (bench.py roofline) is keyed by the kernel that runs.
+  enum Path { kFcm, kAreg, kRing, kStream, kDma, kReg } path = kReg;
+  if (fcm_conv_supported(p))              // CAM++ FCM 3x3 32->32 convs (fcm_conv.hip)
+    path = kFcm;
+  else if (gemm_areg_supported(p))        // A read once, weights streamed (gemm_areg.hip)
+    path = kAreg;
+  else if (p.K > 384 && p.N >= 256 && gemm_ring_supported(p))   // stream would split N into 64-col panels
+    path = kRing;
+  else if (gemm_stream_supported(p))      // weight-resident streaming path (gemm_stream.hip)
+    path = kStream;
+  else if (gemm_ring_supported(p))        // 3-stage ring, BN-ReLU prologue (gemm_ring.hip)
+    path = kRing;
+  else if (gemm_dma_supported(p))         // LDS-DMA fast path (gemm_dma.hip)
+    path = kDma;
+  static const char* kNames[] = {"fcm_conv3x3_band", "gemm_areg", "gemm_ring", "gemm_stream", "gemm_dma",
+                                 "gemm_bf16_reg"};
   static const bool detail = getenv("SDIAR_PROF_DETAIL") != nullptr;
-  std::string key = "conv_gemm_bf16";
+  std::string key = kNames[path];
   if (detail && prof_enabled())
     key += " M=" + std::to_string(M) + " N=" + std::to_string(p.N) + " K=" + std::to_string(p.K) +
            " taps=" + std::to_string(p.kh * p.kw) + (p.a_bf16 ? " Abf" : " Af32") + (p.pre_scale ? " pre" : "");
   ProfScope prof(key.c_str(), flops, bytes, st);
-  if (fcm_conv_supported(p)) {      // CAM++ FCM 3x3 32->32 convs (fcm_conv.hip)
-    conv_fcm3x3(p, st);
-    return;
-  }
-  if (gemm_areg_supported(p)) {     // A read once, weights streamed (gemm_areg.hip)
-    conv_gemm_areg(p, st);
-    return;
-  }
-  if (p.K > 384 && p.N >= 256 && gemm_ring_supported(p)) {   // stream would split N into 64-col panels
-    conv_gemm_ring(p, st);
-    return;
-  }
-  if (gemm_stream_supported(p)) {   // weight-resident streaming path (gemm_stream.hip)
-    conv_gemm_stream(p, st);
-    return;
-  }
-  if (gemm_ring_supported(p)) {     // 3-stage ring, BN-ReLU prologue (gemm_ring.hip)
-    conv_gemm_ring(p, st);
-    return;
-  }
-  if (gemm_dma_supported(p)) {   // LDS-DMA fast path (gemm_dma.hip)
-    conv_gemm_dma(p, st);
-    return;
+  switch (path) {
+    case kFcm: conv_fcm3x3(p, st); return;
+    case kAreg: conv_gemm_areg(p, st); return;
+    case kRing: conv_gemm_ring(p, st); return;
+    case kStream: conv_gemm_stream(p, st); return;
+    case kDma: conv_gemm_dma(p, st); return;
+    case kReg: break;
   }
   const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
   const bool big = (int64_t)cdiv(M, 128) * cdiv(p.N, bn) >= 512;

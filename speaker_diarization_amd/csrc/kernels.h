@@ -193,9 +193,15 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 // h0/c0 optional (ndir, B, H); hT/cT optional outputs (ndir, B, H).
 // whh_bf16 (optional, same layout in bf16 bits): bf16-MFMA recurrence (bf16 mode); the
 // cell state, gates and h stay fp32, h is rounded to bf16 only as the MFMA operand.
+// work: per-handle device scratch of lstm_work_floats(B, H, ndir) floats (the persistent bf16
+// kernel keeps its h exchange and counters there).  host_err (optional, pinned, per handle):
+// receives a stream-ordered copy of the persistent kernel's poll-timeout flag; a set flag is
+// reported (kErrHip) by the next call on that handle.
+int64_t lstm_work_floats(int B, int H, int ndir);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
-                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr);
+                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr,
+                     int* host_err = nullptr);
 
 // ---------------------------------------------------------------- frontend
 // Kaldi fbank (torchaudio.compliance.kaldi.fbank semantics used by
@@ -218,8 +224,9 @@ void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16,
 }  // namespace sd
 
 namespace sd {
+// sigmoid=false: inputs are probabilities already (sd_overlap_mean).
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
-                     int dis, int chunk, int n_frames, float* out, hipStream_t st);
+                     int dis, int chunk, int n_frames, float* out, hipStream_t st, bool sigmoid = true);
 
 // ---------------------------------------------------------------- postprocess.hip
 struct ThresholdSet {

@@ -9,6 +9,8 @@
 // semantics (encoder_decoder_attractor.py:45-49): the reverse direction starts
 // at len-1 and states freeze after a sequence ends.
 // Serves ts_vad2/model.py:360-366,752 (BiLSTM) and eend_eda EDA LSTMs.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -347,10 +349,21 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     }
     publish((step + 1) & 1);   // h_step
   }
+  // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
+  // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
+  const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const float qnan = __int_as_float(0x7fc00000);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int b = b0 + mt * 16 + l15;
     if (b >= B) continue;
+    if (bad) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hr[mt][r] = c[mt][r] = qnan;
+      if (out)
+        for (int t = 0; t < len[mt]; ++t)
+          *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) = make_float4(qnan, qnan, qnan, qnan);
+    }
     const int64_t si = ((int64_t)d * B + b) * H + ub;
     if (hT) *reinterpret_cast<float4*>(hT + si) = make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
     if (cT) *reinterpret_cast<float4*>(cT + si) = make_float4(c[mt][0], c[mt][1], c[mt][2], c[mt][3]);
@@ -369,45 +382,72 @@ void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL(lstm_group_bf16_kernel<MT>, dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
-                     reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
-                     counters, err);
+  // Cooperative launch: the runtime checks the grid against the occupancy query and refuses a
+  // grid whose workgroups could not all be resident (hipErrorCooperativeLaunchTooLarge -> kErrHip)
+  // instead of letting the group hand-off wait on a workgroup that never starts.
+  const uint16_t* w = reinterpret_cast<const uint16_t*>(whh_bf16);
+  void* args[] = {(void*)&gx, (void*)&B, (void*)&T, (void*)&ndir, (void*)&w, (void*)&lengths, (void*)&h0,
+                  (void*)&c0, (void*)&out, (void*)&ldo, (void*)&hT, (void*)&cT, (void*)&hx, (void*)&Bp,
+                  (void*)&counters, (void*)&err};
+  SD_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>), dim3(4 * groups),
+                                    dim3(256), args, (unsigned)smem, st));
 }
+
+int lstm_group_mt(int B, int ndir) {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  for (int m = 1; m <= LS_MAXMT; ++m)   // smallest row block (16 * MT) whose 4 x groups fit one WG per CU
+    if (4 * ndir * cdiv(B, 16 * m) <= n_cu) return m;
+  return 0;
+}
+
+// Layout of the persistent kernel's scratch inside the caller's `work`: the double-buffered bf16
+// h exchange, then (16-B aligned) one counter per group and the err word.
+size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
 
 }  // namespace
 
+int64_t lstm_work_floats(int B, int H, int ndir) {
+  int64_t step_path = 3LL * ndir * B * H;
+  if (H != LS_H) return step_path;
+  // persistent path at the largest row block it may pick (Bp <= B + 16 * LS_MAXMT)
+  const int Bp = (B + 16 * LS_MAXMT);
+  const int64_t grp = (int64_t)ndir * cdiv(B, 16) + 2;
+  const int64_t bytes = (int64_t)lstm_group_hx_bytes(Bp, ndir) + 4 * grp + 16;
+  return std::max<int64_t>(step_path, (bytes + 3) / 4);
+}
+
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
-                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16) {
+                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16, int* host_err) {
   SD_CHECK(H % 32 == 0, kErrInvalid, "lstm: H must be a multiple of 32");
   static const bool no_seq = getenv("SDIAR_NO_LSTM_SEQ") != nullptr;
+  if (host_err) {
+    // Deferred report of an earlier launch on this handle whose bounded polls timed out (its
+    // outputs were poisoned with NaN); the flag is the stream-ordered copy of its err word.
+    const int prev = __atomic_load_n(host_err, __ATOMIC_ACQUIRE);
+    __atomic_store_n(host_err, 0, __ATOMIC_RELEASE);
+    SD_CHECK(prev == 0, kErrHip, "lstm: a previous persistent LSTM launch lost workgroup co-residency "
+                                 "(its outputs were poisoned with NaN)");
+  }
   if (whh_bf16 && H == LS_H && !no_seq && (ldo % 4 == 0 || !out)) {
-    // Smallest row block (16 * MT) whose 4 x groups fit one workgroup per CU.
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      SD_HIP(hipGetDevice(&dev));
-      SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    int mt = 0;
-    for (int m = 1; m <= LS_MAXMT && !mt; ++m)
-      if (4 * ndir * cdiv(B, 16 * m) <= n_cu) mt = m;
+    const int mt = lstm_group_mt(B, ndir);
     if (mt) {
       const int Bp = cdiv(B, 16 * mt) * 16 * mt;
       const int groups = ndir * cdiv(B, 16 * mt);
-      // Exchange buffers + counters: one device scratch, grown on demand.
-      static void* scratch = nullptr;
-      static size_t scratch_bytes = 0;
-      const size_t hx_bytes = (size_t)2 * ndir * Bp * H * 2;
+      // Exchange buffers + counters live in the caller's per-handle `work` (lstm_work_floats), so
+      // recurrences of different handles / streams / devices never share scratch.
+      const size_t hx_bytes = lstm_group_hx_bytes(Bp, ndir);
       const size_t ctl_bytes = ((size_t)(groups + 1) * 4 + 15) / 16 * 16;
-      if (hx_bytes + ctl_bytes > scratch_bytes) {
-        if (scratch) SD_HIP(hipFree(scratch));
-        scratch_bytes = hx_bytes + ctl_bytes;
-        SD_HIP(hipMalloc(&scratch, scratch_bytes));
-      }
-      unsigned* ctl = reinterpret_cast<unsigned*>(static_cast<char*>(scratch) + hx_bytes);
+      SD_CHECK((int64_t)((hx_bytes + ctl_bytes + 3) / 4) <= lstm_work_floats(B, H, ndir), kErrInvalid,
+               "lstm: work buffer too small");
+      uint16_t* hx = reinterpret_cast<uint16_t*>(work);
+      unsigned* ctl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + hx_bytes);
       SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
-      uint16_t* hx = static_cast<uint16_t*>(scratch);
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       int* err = reinterpret_cast<int*>(ctl + groups);
@@ -419,7 +459,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
         case 5: launch_lstm_group<5>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         default: launch_lstm_group<6>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
       }
-      SD_LAUNCH_CHECK();
+      if (host_err) SD_HIP(hipMemcpyAsync(host_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
       return;
     }
   }

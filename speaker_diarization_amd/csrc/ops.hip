@@ -891,6 +891,10 @@ namespace sd {
 // windows covering a frame, in window order) with the sigmoid of model.py:945-946
 // fused.  logits: (n_win, NS, Tw); window w covers label frames
 // [start_w, start_w + len_w).  out: (NS, n_frames); frames no window covers -> NaN.
+// np.mean semantics (infer.py:90-94 over float32 lists): float32 sum from 0 in window order, then
+// one correctly rounded float32 division (hipcc keeps fp32 '/' IEEE by default) — bit-identical
+// to numpy for the same probabilities.  No FMA can form (adds only).
+template <bool kSigmoid>
 __global__ void overlap_average_kernel(const float* __restrict__ logits, int n_win, int NS, int Tw,
                                        const int* __restrict__ start, const int* __restrict__ len,
                                        int dis, int chunk, int n_frames, float* __restrict__ out) {
@@ -906,18 +910,19 @@ __global__ void overlap_average_kernel(const float* __restrict__ logits, int n_w
   for (int w = w_lo; w <= w_hi; ++w) {
     int off = t - start[w];
     if (off < 0 || off >= len[w]) continue;
-    float x = logits[((int64_t)w * NS + spk) * Tw + off];
-    acc += 1.f / (1.f + expf(-x));
+    const float x = logits[((int64_t)w * NS + spk) * Tw + off];
+    acc = __fadd_rn(acc, kSigmoid ? 1.f / (1.f + expf(-x)) : x);
     ++cnt;
   }
-  out[i] = cnt ? acc / (float)cnt : __int_as_float(0x7fc00000);
+  out[i] = cnt ? __fdiv_rn(acc, (float)cnt) : __int_as_float(0x7fc00000);
 }
 
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
-                     int dis, int chunk, int n_frames, float* out, hipStream_t st) {
+                     int dis, int chunk, int n_frames, float* out, hipStream_t st, bool sigmoid) {
   int64_t total = (int64_t)NS * n_frames;
   if (total == 0) return;
-  hipLaunchKernelGGL(overlap_average_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+  auto k = sigmoid ? overlap_average_kernel<true> : overlap_average_kernel<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out);
   SD_LAUNCH_CHECK();
 }

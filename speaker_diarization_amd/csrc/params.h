@@ -44,6 +44,20 @@ class DeviceArena {
   size_t total_ = 0;
 };
 
+// Pinned host int per handle: the target of a stream-ordered device->host copy of a device-side
+// failure flag (the persistent LSTM's poll timeout), read back on the handle's next call.
+class PinnedFlag {
+ public:
+  PinnedFlag() { SD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), sizeof(int), hipHostMallocDefault)); *p_ = 0; }
+  ~PinnedFlag() { if (p_) (void)hipHostFree(p_); }
+  PinnedFlag(const PinnedFlag&) = delete;
+  PinnedFlag& operator=(const PinnedFlag&) = delete;
+  int* get() const { return p_; }
+
+ private:
+  int* p_ = nullptr;
+};
+
 struct Folded {        // per-channel affine y = x*scale + shift
   const float* scale = nullptr;
   const float* shift = nullptr;

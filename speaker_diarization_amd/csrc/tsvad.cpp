@@ -99,7 +99,7 @@ void TsvadModel::alloc_workspace() {
   H_ = ws(rows * std::max<int64_t>({(int64_t)cfg_.ffn_dim, 2 * E, (int64_t)cfg_.conformer_ffn}));
   X2_ = ws(rows * E);
   partial_ = ws(Bm * NS * ((E + 63) / 64) * 2);
-  lstm_work_ = ws(3 * 2 * Bm * cfg_.lstm_hidden);
+  lstm_work_ = ws(lstm_work_floats((int)Bm, cfg_.lstm_hidden, 2));
 }
 
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
@@ -144,7 +144,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
-                    nullptr, lstm_work_, st, lstm_hh_bf_);
+                    nullptr, lstm_work_, st, lstm_hh_bf_, lstm_err_.get());
     ConvGemmArgs f = cam_conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);

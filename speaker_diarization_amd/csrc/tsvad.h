@@ -45,6 +45,7 @@ class TsvadModel {
   TsvadConfig cfg_;
   ParamStore ps_;
   DeviceArena arena_;
+  PinnedFlag lstm_err_;   // deferred poll-timeout report of the persistent LSTM (lstm.hip)
   bool finalized_ = false;
 
   CamTrunk cam_;     // speech_encoder.* (CAM++ get_time_out=True)

@@ -124,13 +124,12 @@ void TsvadStreamModel::forward(const float* feats, const float* ts, int B, int T
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_windows, kErrInvalid, "windows per call exceed max_windows");
   SD_CHECK(T_lab >= 1 && T_lab <= cfg_.max_labels, kErrInvalid, "label frames exceed max_labels");
-  SD_CHECK(chunk >= 2, kErrInvalid, "decoding_chunk_size must be >= 2 (8 fbank frames per chunk)");
+  SD_CHECK(chunk >= 1, kErrInvalid, "decoding_chunk_size must be >= 1");
   const bool bf = cfg_.bf16;
   const int E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim, NS = cfg_.max_num_speaker;
   // positional-encoding rows used: start(c) + C <= T_lab + C
   SD_CHECK(T_lab + chunk <= pe_len_, kErrShape, "window longer than pos_encoder max_len");
   const int n_full = T_lab / chunk, tail = T_lab % chunk;
-  SD_CHECK(tail == 0 || tail >= 2, kErrInvalid, "last chunk must hold >= 2 label frames (8 fbank frames)");
   // Chunk runs: windows are contiguous, so without a tail every window's chunks form one run of
   // B * n_full equal chunks; with a tail, each window's full chunks and its tail are separate runs.
   // ---- embed: CAM++ (get_time_out) + speech_down_or_up per chunk (chunk c of the window holds

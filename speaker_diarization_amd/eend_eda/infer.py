@@ -88,12 +88,11 @@ def chunk_activities(model, feats, args: EdaInferArgs, perms, c0: int = 0, c1: O
     return acts, (torch.cat(probs).cpu() if probs else torch.zeros(0, args.max_n_speakers))
 
 
-def infer_recording(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) -> np.ndarray:
-    """wav: 1-D float32 CUDA tensor -> T_hat (T, n_spk) float32, the array infer_eda.py
-    writes to <recid>.h5 (:115-124)."""
+def infer_chunks(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) -> List[np.ndarray]:
+    """The per-chunk loop of infer_eda.py:99-113: wav (1-D float32 CUDA tensor) ->
+    out_chunks, one (T_c, n_spk) float32 array per 2000-frame chunk, in chunk order."""
     import torch
     import torch.distributed as dist
-    from scipy.ndimage import shift
 
     feats = recording_features(model, wav, args)
     chunks = list(gen_chunk_indices(feats.shape[0], args.chunk_size))
@@ -105,23 +104,41 @@ def infer_recording(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None)
         rank = dist.get_rank(group)
         c0, c1 = shard_chunks(len(chunks), world, rank)
         local, lprobs = chunk_activities(model, feats, args, perms, c0, c1)
-        acts, probs = gather_chunks(local, lprobs, chunks, args, world, group)
+        acts, probs = gather_chunks(local, lprobs, chunks, args, world, group, device=feats.device)
     lens = [e - s for s, e in chunks]
     out_chunks = []
     for c, a in enumerate(acts):
         y = model.select(a[None], probs[c: c + 1], [lens[c]], args.num_speakers, args.attractor_threshold)[0]
         out_chunks.append(y.cpu().numpy())
+    return out_chunks
+
+
+def stitch(out_chunks: List[np.ndarray], args: EdaInferArgs = EdaInferArgs()) -> np.ndarray:
+    """infer_eda.py:115-121: np.vstack of the chunk outputs (raises ValueError, as the
+    reference does, when threshold-mode chunks selected different speaker counts), then
+    the label-delay shift."""
+    from scipy.ndimage import shift
     outdata = np.vstack(out_chunks)
     if args.label_delay != 0:
         outdata = shift(outdata, (-args.label_delay, 0))
     return outdata
 
 
-def gather_chunks(local: List, lprobs, chunks, args: EdaInferArgs, world: int, group=None):
-    """All-gather of per-chunk activities + attractor probabilities in chunk order."""
+def infer_recording(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) -> np.ndarray:
+    """wav: 1-D float32 CUDA tensor -> T_hat (T, n_spk) float32, the array infer_eda.py
+    writes to <recid>.h5 (:115-124)."""
+    return stitch(infer_chunks(model, wav, args, group), args)
+
+
+def gather_chunks(local: List, lprobs, chunks, args: EdaInferArgs, world: int, group=None, device=None):
+    """All-gather of per-chunk activities + attractor probabilities in chunk order.
+    `device` is where the gather buffer lives (the rank's GPU; a rank may own no chunk
+    when world > n_chunks, so it cannot be taken from `local`)."""
     import torch
     import torch.distributed as dist
-    dev = local[0].device if local else torch.device("cuda", torch.cuda.current_device())
+    if device is None:
+        device = local[0].device if local else torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device(device)
     na = args.max_n_speakers
     ranges = [shard_chunks(len(chunks), world, r) for r in range(world)]
     maxn = max(b - a for a, b in ranges)

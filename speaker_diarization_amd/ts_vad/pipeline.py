@@ -22,6 +22,8 @@ class TSVADPipeline:
         self.model = model
         self.cfg = model.cfg
         self.segment_shift = segment_shift
+        # a model that fixes the reference batch (the streaming decoder: batch 1) overrides it
+        batch_size = getattr(model, "reference_batch_size", batch_size)
         self.batch_size = min(batch_size, model.max_batch)
 
     def plan(self, n_labels: int) -> WindowPlan:
@@ -67,6 +69,21 @@ class TSVADPipeline:
             else:
                 groups.append((b0, b1) + key)
         return groups
+
+    @staticmethod
+    def mean_probs(probs, plan: WindowPlan):
+        """(n_win, NS, chunk) probabilities -> (NS, n_labels): infer.py:90-94's np.mean over each
+        frame's list of window values, bit-identical (sd_overlap_mean)."""
+        import torch
+        dev = probs.device
+        NS = probs.shape[1]
+        out = torch.empty(NS, plan.n_labels, device=dev, dtype=torch.float32)
+        st = torch.from_numpy(plan.starts.astype(np.int32)).to(dev)
+        ln = torch.from_numpy(plan.lens.astype(np.int32)).to(dev)
+        _lib.call("sd_overlap_mean", _lib.ptr(probs.contiguous()), plan.n_win, NS, probs.shape[2],
+                  _lib.ptr(st), _lib.ptr(ln), plan.dis, plan.chunk, plan.n_labels, _lib.ptr(out),
+                  _lib.stream_ptr(dev))
+        return out
 
     @staticmethod
     def average(logits, plan: WindowPlan):

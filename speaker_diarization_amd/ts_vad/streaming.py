@@ -116,8 +116,14 @@ class StreamingWindowDecoder:
     overlap average) drive the chunk-streaming model: the streaming recipe's decode
     (run_ts_vad2_streaming.sh: rs_len 10, segment_shift 1, decoding_chunk_size 25,
     num_decoding_left_chunks -1; infer.py window loop -> infer_debug -> forward_chunk_by_chunk_temp1).
-    Each batch of windows is padded / trimmed to 4 x labels (model.py:614-618) and decoded in one
-    sd_tsvad_stream_forward call."""
+    The recipe decodes one window per batch (run_ts_vad2_streaming.sh:74 batch_size=1; forward_chunk
+    asserts B == 1, model.py:720), so every window is decoded at its own length: the adapter sets
+    `reference_batch_size = 1` and TSVADPipeline then fuses only consecutive windows of identical
+    length into one sd_tsvad_stream_forward call (a tail window is never padded with another
+    window's frames, which would turn its partial last chunk into a full one).  Each window's fbank
+    is padded / trimmed to 4 x labels (model.py:614-618)."""
+
+    reference_batch_size = 1
 
     def __init__(self, model: TSVADStreamingModel, decoding_chunk_size: int = 25, num_decoding_left_chunks: int = -1,
                  rs_len: int = 10, label_rate: int = 25, sample_rate: int = 16000):

@@ -213,6 +213,7 @@ TSVAD_STREAM_CASES = {
     "tsvad_stream_c25": (100, 25, -1, 400, 61, 811),
     "tsvad_stream_c10_l2": (60, 10, 2, 240, 62, 812),
     "tsvad_stream_tail": (70, 25, -1, 277, 63, 813),     # short last chunk; xs padded to 4 * T_label
+    "tsvad_stream_tail1": (76, 25, -1, 304, 64, 814),    # 1-label last chunk: 4 fbank frames -> CAM++ 2 -> 1
 }
 
 

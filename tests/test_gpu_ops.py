@@ -342,16 +342,47 @@ def test_window_cmn(gpu):
         assert (out[i, n:] == 0).all()
 
 
+def _np_mean_lists(prob, plan):
+    """infer.py:90-94 literally: per frame, np.mean of the float32 list of window values in
+    window order (what res_dict[name-spk][start+t].append(p) builds, model.py:960-966)."""
+    from collections import defaultdict
+    ns = prob.shape[1]
+    res = [defaultdict(list) for _ in range(ns)]
+    for w in range(plan.n_win):
+        for t in range(int(plan.lens[w])):
+            for i in range(ns):
+                res[i][int(plan.starts[w]) + t].append(prob[w, i, t])
+    ref = np.full((ns, plan.n_labels), np.nan, np.float32)
+    for i in range(ns):
+        for t, v in res[i].items():
+            ref[i, t] = np.mean(v)
+    return ref
+
+
+@pytest.mark.parametrize("n_lab,rs,shift", [(1000, 6, 1), (777, 4, 1), (613, 6, 2), (3, 4, 1)])
+def test_overlap_mean_bit_exact(gpu, n_lab, rs, shift):
+    """sd_overlap_mean == np.mean over the res_dict lists, bit for bit (values chosen to make
+    float32 rounding order matter)."""
+    from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    from speaker_diarization_amd.ts_vad.windows import plan_windows
+    plan = plan_windows(n_lab, rs, shift)
+    rng = np.random.default_rng(n_lab)
+    prob = rng.random((plan.n_win, 4, plan.chunk)).astype(np.float32)
+    prob[:, 1] = (prob[:, 1] * 1e-4 + np.float32(0.5)).astype(np.float32)    # many ulp-level carries
+    prob[:, 2] = np.float32(0.1)                                              # 0.1 is inexact in binary
+    out = TSVADPipeline.mean_probs(torch.from_numpy(prob).to(gpu), plan).cpu().numpy()
+    ref = _np_mean_lists(prob, plan)
+    np.testing.assert_array_equal(out, ref)
+
+
 def test_overlap_average(gpu):
+    """sigmoid on the GPU + the same bit-exact mean: equals np.mean over torch-CPU sigmoid
+    probabilities up to the sigmoid's own last-ulp differences (expf implementations differ)."""
     from speaker_diarization_amd.ts_vad.windows import plan_windows
     from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
     plan = plan_windows(1000, 6, 1)
     g = torch.Generator().manual_seed(4)
     logits = torch.randn(plan.n_win, 4, plan.chunk, generator=g)
     out = TSVADPipeline.average(logits.to(gpu), plan).cpu().numpy()
-    prob = torch.sigmoid(logits).numpy()
-    ref = np.zeros((4, 1000), np.float32)
-    for t in range(1000):
-        vals = [prob[w, :, t - plan.starts[w]] for w in range(plan.n_win) if plan.starts[w] <= t < plan.ends[w]]
-        ref[:, t] = np.mean(np.stack(vals), axis=0)
-    np.testing.assert_allclose(out, ref, atol=1e-6, rtol=1e-6)
+    ref = _np_mean_lists(torch.sigmoid(logits).numpy(), plan)
+    np.testing.assert_array_max_ulp(out, ref, maxulp=4)

@@ -93,3 +93,33 @@ def test_eend_make_rttm(gpu, T, nspk, median, thr):
     got = make_rttm.session_lines("rec1", torch.from_numpy(t_hat).cuda(), threshold=thr, frame_shift=80,
                                   subsampling=10, median=median, sampling_rate=8000)
     assert got == want
+
+
+@pytest.mark.parametrize("name", ["postprocess_smooth", "postprocess_edges", "postprocess_tiny"])
+def test_gpu_writer_matches_reference_run(gpu, name):
+    """posteriors_to_rttm_gpu (medfilt + thresholds + run-length filters on the GPU) reproduces
+    the res_rttm_<thr> files the reference's own infer.postprocess wrote (make_postprocess_golden.py),
+    byte for byte; tracks of one meeting share a row block like the pipeline's (NS, T) output."""
+    import os
+    from make_postprocess_golden import THRESHOLDS, load_res_dict
+    from speaker_diarization_amd.ts_vad.postprocess import posteriors_to_rttm_gpu
+    path = os.path.join(os.path.dirname(__file__), "golden", name + ".npz")
+    g = np.load(path)
+    res = load_res_dict(path)
+    post = {k: np.array([np.mean(v) for v in lists], np.float32) for k, lists in res.items()}
+    out = {t: [] for t in THRESHOLDS}
+    keys = list(post)
+    i = 0
+    while i < len(keys):          # consecutive keys of one meeting -> one device call
+        name_i = keys[i].rsplit("-", 1)[0]
+        j = i
+        while j < len(keys) and keys[j].rsplit("-", 1)[0] == name_i:
+            j += 1
+        rows = torch.from_numpy(np.stack([post[k] for k in keys[i:j]])).to(gpu)
+        part = posteriors_to_rttm_gpu(keys[i:j], rows)
+        for t in THRESHOLDS:
+            out[t].extend(part[t])
+        i = j
+    # the reference writes key by key into every threshold file: same order, same bytes
+    for jt, thr in enumerate(THRESHOLDS):
+        assert "".join(out[thr]) == str(g["rttm"][jt]), thr

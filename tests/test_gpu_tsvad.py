@@ -110,3 +110,31 @@ def test_tsvad_v1_large_batch_uses_wide_gemm_paths(gpu):
     err = np.abs(out - ref).max()
     print(f"B={B} bf16: max|logit diff| = {err:.3e}")
     assert err < BF16_ATOL
+
+
+def test_tsvad_infer_res_dict_matches_reference(gpu):
+    """TSVADModel.infer (model.py:923-970) -> (result, res_dict) vs the reference's own infer on
+    the same seeded batch (tests/golden/tsvad_infer.npz, make_postprocess_golden.py): partial
+    label lengths, absent speakers (-1 ids), two meetings.  Keys, frame keys and their insertion
+    order, list lengths exact; probabilities fp32 <= 1e-5; the 0.5-thresholded DER/ACC/MI/FA/CF
+    exact; the BCE loss <= 1e-5."""
+    import os
+    from make_postprocess_golden import INFER_CASE as c, infer_labels
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "tsvad_infer.npz"))
+    cfg = TSVADConfig(rs_len=4)
+    m = TSVADModel(cfg, device=gpu, precision="fp32", max_batch=c["B"])
+    m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=c["wseed"])))
+    x, ts = tsvad_inputs(c["B"], c["T_fb"], c["n_lab"], seed=c["iseed"])
+    result, res_dict = m.infer(torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu),
+                               torch.from_numpy(infer_labels()), torch.tensor(c["lens"]), file_path=c["files"],
+                               speaker_ids=c["spk"], start=c["starts"])
+    assert list(res_dict) == [str(k) for k in g["keys"]]
+    for i, k in enumerate(res_dict):
+        assert list(res_dict[k]) == list(g[f"order_{i}"])
+        frames = sorted(res_dict[k])
+        assert [len(res_dict[k][t]) for t in frames] == list(g[f"counts_{i}"])
+        vals = np.array([v for t in frames for v in res_dict[k][t]], np.float32)
+        assert np.abs(vals - g[f"values_{i}"]).max() <= 1e-5
+    got = np.array([result[k] for k in ("DER", "ACC", "MI", "FA", "CF")], np.float64)
+    np.testing.assert_allclose(got, g["metrics"], rtol=0, atol=1e-12)
+    assert abs(float(result["losses"]["diar"]) - float(g["loss"])) <= 1e-5
