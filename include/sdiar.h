@@ -105,7 +105,8 @@ int sd_tsvad_stream_finalize(sd_tsvad_stream* h);
 /* B independent windows, each decoded as the reference's chunk loop decodes one (infer_debug,
  * batch 1, model.py:951-975).  feats: device (B, 4 * T_label, 80) fbank, already padded / trimmed
  * to 4 x labels (model.py:614-618); ts: device (B, max_num_speaker, speaker_embed_dim); chunk:
- * decoding_chunk_size (>= 2 label frames, and the last partial chunk >= 2); left_chunks:
+ * decoding_chunk_size (>= 1 label frame; a last partial chunk of any length, even 1 label = 4 fbank
+ * frames, is decoded as the reference decodes it); left_chunks:
  * num_decoding_left_chunks (< 0: all history); logits: device (B, max_num_speaker, T_label),
  * pre-sigmoid. */
 int sd_tsvad_stream_forward(sd_tsvad_stream* h, const float* feats, const float* ts, int B, int T_label, int chunk,
@@ -137,6 +138,49 @@ int sd_campp_finalize(sd_campp* h);
 int sd_campp_forward(sd_campp* h, const float* feats, int B, int T, float* emb, float* time_out, void* stream);
 int64_t sd_campp_device_bytes(const sd_campp* h);
 int sd_campp_destroy(sd_campp* h);
+
+/* ------------------------------------------------------------------ SSND
+ * Replaces SSNDModel.infer (egs/alimeeting/ssnd/ssnd_model.py:752-776) with extractor
+ * 'CAM++_wo_gsp' (:107-124), SSNDConformerEncoder (:172-195), DetectionDecoder (:274-296: the
+ * speaker-query cross-attention decoder, SWDecoderBlockV2 :224-272) and RepresentationDecoder
+ * (:343-370); construction :373-441 (training=False).  State-dict keys are SSNDModel's.  The
+ * decoders always run exact fp32; precision selects the extractor / encoder arithmetic. */
+typedef struct sd_ssnd sd_ssnd;
+
+typedef struct {
+  int max_batch;         /* workspace: blocks per call                                        */
+  int max_fbank_frames;  /* workspace: fbank frames per block (800 = 8 s)                    */
+  int max_speakers;      /* N: det_query_emb rows                                             */
+  int feat_dim;          /* 80 */
+  int emb_dim;           /* 256 */
+  int q_det_aux_dim;     /* 256 */
+  int q_rep_aux_dim;     /* 256 */
+  int d_model;           /* 256 */
+  int nhead;             /* 8 */
+  int d_ff;              /* 512 */
+  int num_layers;        /* 4 (encoder and both decoders) */
+  int vad_out_len;       /* label frames per block (det_decoder.out_proj rows), 200 for 8 s */
+  int pos_emb_dim;       /* 256 */
+  int max_seq_len;       /* 1000 (pos_emb rows) */
+  int n_all_speakers;    /* 1000 (E_all rows) */
+  int conformer_kernel;  /* 15 (SSNDConformerEncoder cnn_kernel_size) */
+  int precision;         /* 0: fp32, 1: bf16 MFMA extractor + encoder */
+} sd_ssnd_config;
+
+int sd_ssnd_create(const sd_ssnd_config* cfg, sd_ssnd** out);
+int sd_ssnd_set_param(sd_ssnd* h, const char* name, const float* host_data, const int64_t* shape, int ndim);
+int sd_ssnd_finalize(sd_ssnd* h);
+/* SSNDModel.infer: feats device (B, T_fbank, 80) with (T_fbank - 1) / 2 + 1 CAM++ frames giving
+ * vad_out_len label frames; speaker_embs device (B, max_speakers, emb_dim);
+ * vad_pred device (B, max_speakers, vad_out_len) pre-sigmoid; emb_pred device (B, max_speakers, emb_dim). */
+int sd_ssnd_infer(sd_ssnd* h, const float* feats, const float* speaker_embs, int B, int T_fbank, float* vad_pred,
+                  float* emb_pred, void* stream);
+/* The two decoders alone (infer after the encoder, :762-776): enc_out device (B, T, d_model),
+ * x_fea device (B, T, emb_dim) (the extractor output), T == vad_out_len. */
+int sd_ssnd_decode(sd_ssnd* h, const float* enc_out, const float* x_fea, const float* speaker_embs, int B, int T,
+                   float* vad_pred, float* emb_pred, void* stream);
+int64_t sd_ssnd_device_bytes(const sd_ssnd* h);
+int sd_ssnd_destroy(sd_ssnd* h);
 
 /* ------------------------------------------------------------------ EEND-EDA
  * Replaces TransformerEdaModel (speaker_diarization/eend_eda/models.py:161-347) and

@@ -85,6 +85,13 @@ class CamppConfig(ctypes.Structure):
     ]
 
 
+class SsndConfig(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "max_batch", "max_fbank_frames", "max_speakers", "feat_dim", "emb_dim", "q_det_aux_dim", "q_rep_aux_dim",
+        "d_model", "nhead", "d_ff", "num_layers", "vad_out_len", "pos_emb_dim", "max_seq_len", "n_all_speakers",
+        "conformer_kernel", "precision")]
+
+
 class TsvadStreamConfig(ctypes.Structure):
     _fields_ = [
         ("max_num_speaker", c_int),
@@ -119,6 +126,13 @@ _SIGS = {
                                         c_void_p]),
     "sd_tsvad_stream_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_stream_destroy": (c_int, [c_void_p]),
+    "sd_ssnd_create": (c_int, [POINTER(SsndConfig), POINTER(c_void_p)]),
+    "sd_ssnd_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "sd_ssnd_finalize": (c_int, [c_void_p]),
+    "sd_ssnd_infer": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sd_ssnd_decode": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sd_ssnd_device_bytes": (c_int64, [c_void_p]),
+    "sd_ssnd_destroy": (c_int, [c_void_p]),
     "sd_campp_create": (c_int, [POINTER(CamppConfig), POINTER(c_void_p)]),
     "sd_campp_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_campp_finalize": (c_int, [c_void_p]),

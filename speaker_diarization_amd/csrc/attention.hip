@@ -493,6 +493,7 @@ void attention(const AttnArgs& a, bool bf16, hipStream_t st) {
   const double bytes = (a.io_bf16 ? 2.0 : 4.0) * a.S * a.T * (3.0 * a.D + a.D);
   ProfScope prof(bf16 ? "attention_bf16" : "attention_f32", flops, bytes, st);
   switch (hd) {
+    case 32: launch_hd<32>(a, bf16, st); break;
     case 48: launch_hd<48>(a, bf16, st); break;
     case 64: launch_hd<64>(a, bf16, st); break;
     case 96: launch_hd<96>(a, bf16, st); break;

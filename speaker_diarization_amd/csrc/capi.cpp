@@ -16,6 +16,7 @@
 #include "tsvad.h"
 #include "campp.h"
 #include "tsvad_stream.h"
+#include "ssnd.h"
 
 namespace sd {
 static thread_local std::string g_err;
@@ -33,6 +34,10 @@ struct sd_eda {
 
 struct sd_campp {
   std::unique_ptr<sd::CamppModel> model;
+};
+
+struct sd_ssnd {
+  std::unique_ptr<sd::SsndModel> model;
 };
 
 struct sd_tsvad_stream {
@@ -468,6 +473,70 @@ int sd_campp_forward(sd_campp* h, const float* feats, int B, int T, float* emb, 
 int64_t sd_campp_device_bytes(const sd_campp* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
 
 int sd_campp_destroy(sd_campp* h) {
+  return guard([&] { delete h; });
+}
+
+int sd_ssnd_create(const sd_ssnd_config* c, sd_ssnd** out) {
+  return guard([&] {
+    SD_CHECK(c && out, sd::kErrInvalid, "null argument");
+    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->max_batch > 0 && c->max_fbank_frames >= 8 && c->max_speakers > 0, sd::kErrInvalid,
+             "bad workspace sizes");
+    SD_CHECK(c->num_layers >= 1 && c->nhead > 0 && c->d_model > 0 && c->d_ff > 0 && c->emb_dim > 0 &&
+                 c->q_det_aux_dim > 0 && c->q_rep_aux_dim > 0 && c->pos_emb_dim > 0 && c->vad_out_len > 0 &&
+                 c->max_seq_len >= c->vad_out_len && c->n_all_speakers > 0,
+             sd::kErrInvalid, "bad model dimensions");
+    SD_CHECK(c->conformer_kernel >= 1 && c->conformer_kernel % 2 == 1 && c->conformer_kernel <= 31, sd::kErrInvalid,
+             "conformer_kernel must be odd and <= 31");
+    SD_CHECK(c->q_det_aux_dim == c->emb_dim, sd::kErrInvalid,
+             "q_det_aux_dim must equal emb_dim (the speaker embeddings are the detection queries)");
+    sd::SsndConfig t;
+    t.max_batch = c->max_batch; t.max_fbank_frames = c->max_fbank_frames; t.max_speakers = c->max_speakers;
+    t.feat_dim = c->feat_dim; t.emb_dim = c->emb_dim; t.q_det_aux_dim = c->q_det_aux_dim;
+    t.q_rep_aux_dim = c->q_rep_aux_dim; t.d_model = c->d_model; t.nhead = c->nhead; t.d_ff = c->d_ff;
+    t.num_layers = c->num_layers; t.vad_out_len = c->vad_out_len; t.pos_emb_dim = c->pos_emb_dim;
+    t.max_seq_len = c->max_seq_len; t.n_all_speakers = c->n_all_speakers; t.conformer_kernel = c->conformer_kernel;
+    t.bf16 = c->precision == 1;
+    auto* h = new sd_ssnd;
+    h->model.reset(new sd::SsndModel(t));
+    *out = h;
+  });
+}
+
+int sd_ssnd_set_param(sd_ssnd* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  return guard([&] {
+    SD_CHECK(h && name && (data || ndim == 0), sd::kErrInvalid, "null argument");
+    SD_CHECK(!h->model->finalized(), sd::kErrState, "set_param after finalize");
+    h->model->params().set(name, data, shape, ndim);
+  });
+}
+
+int sd_ssnd_finalize(sd_ssnd* h) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null handle");
+    h->model->finalize();
+  });
+}
+
+int sd_ssnd_infer(sd_ssnd* h, const float* feats, const float* spk, int B, int T_fbank, float* vad, float* emb,
+                  void* stream) {
+  return guard([&] {
+    SD_CHECK(h && feats && spk && vad && emb, sd::kErrInvalid, "null argument");
+    h->model->infer(feats, spk, B, T_fbank, vad, emb, S(stream));
+  });
+}
+
+int sd_ssnd_decode(sd_ssnd* h, const float* enc, const float* x, const float* spk, int B, int T, float* vad,
+                   float* emb, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && enc && x && spk && vad && emb, sd::kErrInvalid, "null argument");
+    h->model->decode(enc, x, spk, B, T, vad, emb, S(stream));
+  });
+}
+
+int64_t sd_ssnd_device_bytes(const sd_ssnd* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
+
+int sd_ssnd_destroy(sd_ssnd* h) {
   return guard([&] { delete h; });
 }
 

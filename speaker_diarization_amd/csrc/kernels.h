@@ -150,6 +150,26 @@ struct AttnArgs {
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
+// ---------------------------------------------------------------- ssnd_ops.hip
+// Multi-head attention core on separate fp32 q / k / v row sets (SSND decoder cross and self
+// attention, ssnd_model.py:261-266): row i of batch b at ptr + b * bs + i * ld, head h at
+// columns h*hd..; out (B, Nq) rows likewise.  key_len (device int32 per b) optional.
+struct MhaSmallArgs {
+  const float* q = nullptr; int ldq = 0; int64_t q_bs = 0;
+  const float* k = nullptr; int ldk = 0; int64_t k_bs = 0;
+  const float* v = nullptr; int ldv = 0; int64_t v_bs = 0;
+  float* o = nullptr; int ldo = 0; int64_t o_bs = 0;
+  int B = 0, Nq = 0, Tk = 0, nh = 0, hd = 0;
+  float scale = 1.f;
+  const int* key_len = nullptr;
+};
+void mha_small(const MhaSmallArgs& a, hipStream_t st);
+// dst row r = src row r % src_rows (D floats per row).
+void tile_rows(const float* src, int src_rows, int D, float* dst, int dst_rows, hipStream_t st);
+// out[r, j] = mean_t sigmoid(x[r, t]) * w[j] + b[j], t < T, j < N.
+void mean_sigmoid_affine(const float* x, int rows, int T, int ldx, const float* w, const float* b, int N, float* out,
+                         int ldo, hipStream_t st);
+
 // ---------------------------------------------------------------- ts-vad glue
 // rows (b, spk, t) of a (B*NS*T, 2E) buffer: [ts[b,spk,:] | mix[b,t,:]] (+ pe[t]).
 // mix rows t >= Tmix read as zeros (the pad of model.py:703-710 / :852-854).

@@ -240,6 +240,8 @@ def _init(rng: np.random.Generator, shape: Shape, kind: str) -> np.ndarray:
         v = 1.0 + rng.standard_normal(n) * 0.05
     elif kind == "zero":
         v = np.zeros(n)
+    elif kind == "randn":                 # nn.Parameter(torch.randn(...)) (ssnd_model.py:415-431)
+        v = rng.standard_normal(n)
     else:
         raise ValueError(kind)
     return v.astype(np.float32).reshape(shape)
@@ -503,3 +505,81 @@ def fseend_state_dict(cfg: FSEENDConfig, seed: int = 777):
             for i in range(1, cfg.dec_n_layers):
                 sd[k.replace(".0.", f".{i}.", 1)] = sd[k]
     return sd
+
+
+# ----------------------------------------------------------------------------- SSND
+@dataclass
+class SSNDConfig:
+    """SSNDModel constructor arguments (egs/alimeeting/ssnd/ssnd_model.py:373-412) the inference
+    path reads; extractor 'CAM++_wo_gsp' (ssnd_model.py:107-124)."""
+    extractor_model_type: str = "CAM++_wo_gsp"
+    feat_dim: int = 80
+    emb_dim: int = 256
+    q_det_aux_dim: int = 256
+    q_rep_aux_dim: int = 256
+    d_model: int = 256
+    nhead: int = 8
+    d_ff: int = 512
+    num_layers: int = 4
+    max_speakers: int = 4
+    vad_out_len: int = 200
+    pos_emb_dim: int = 256
+    max_seq_len: int = 1000
+    n_all_speakers: int = 1000
+    conformer_kernel: int = 15      # SSNDConformerEncoder cnn_kernel_size (ssnd_model.py:174)
+
+
+def _swdecoder(k: list, p: str, d: int, ff: int, d_aux: int, d_pos: int):
+    """SWDecoderBlockV2 (ssnd_model.py:225-244) parameter names."""
+    k.append((p + "fq.linear.weight", (d, d_aux), "linear"))
+    k.append((p + "fq.linear.bias", (d,), "small"))
+    k.append((p + "fk.linear.weight", (d, d_pos), "linear"))
+    k.append((p + "fk.linear.bias", (d,), "small"))
+    _mha(k, p + "cross_attn.", d)
+    _mha(k, p + "self_attn.", d)
+    k.append((p + "ffn.0.weight", (ff, d), "linear"))
+    k.append((p + "ffn.0.bias", (ff,), "small"))
+    k.append((p + "ffn.3.weight", (d, ff), "linear"))
+    k.append((p + "ffn.3.bias", (d,), "small"))
+    for n in (1, 2, 3):
+        _ln(k, p + f"norm{n}", d)
+
+
+def ssnd_layout(cfg: SSNDConfig) -> list:
+    """Key layout of SSNDModel(cfg) (ssnd_model.py:373-441), extractor CAM++_wo_gsp."""
+    if cfg.extractor_model_type != "CAM++_wo_gsp":
+        raise ValueError(f"the MI355X SSND backend builds extractor CAM++_wo_gsp, got {cfg.extractor_model_type}")
+    d, e = cfg.d_model, cfg.emb_dim
+    k: list = [("pos_emb", (1, cfg.max_seq_len, cfg.pos_emb_dim), "randn"),
+               ("E_all", (cfg.n_all_speakers, e), "randn"), ("e_pse", (1, e), "randn"), ("e_non", (1, e), "randn"),
+               ("det_query_emb", (cfg.max_speakers, d), "randn"),
+               ("rep_query_emb", (cfg.max_speakers, cfg.vad_out_len), "randn")]
+    k += campplus_layout("extractor.speech_encoder.", 192)
+    k.append(("extractor.speech_encoder.output_proj.weight", (e, 512), "linear"))
+    k.append(("extractor.speech_encoder.output_proj.bias", (e,), "small"))
+    k.append(("extractor.speech_down_or_up.0.weight", (e, e, 5), "conv1d"))
+    k.append(("extractor.speech_down_or_up.0.bias", (e,), "small"))
+    _bn(k, "extractor.speech_down_or_up.1.bn", e)
+    k.append(("encoder.input_proj.weight", (d, e), "linear"))
+    k.append(("encoder.input_proj.bias", (d,), "small"))
+    for i in range(cfg.num_layers):
+        _conformer_layer(k, f"encoder.encoder.conformer_layers.{i}.", d, cfg.d_ff, cfg.conformer_kernel, False)
+    for i in range(cfg.num_layers):
+        _swdecoder(k, f"det_decoder.layers.{i}.", d, cfg.d_ff, cfg.q_det_aux_dim, cfg.pos_emb_dim)
+    k.append(("det_decoder.out_proj.weight", (cfg.vad_out_len, d), "linear"))
+    k.append(("det_decoder.out_proj.bias", (cfg.vad_out_len,), "zero"))
+    k.append(("rep_decoder.input_proj.weight", (d, e), "linear"))
+    k.append(("rep_decoder.input_proj.bias", (d,), "small"))
+    k.append(("rep_decoder.xdec_proj.weight", (d, 1), "randn"))
+    k.append(("rep_decoder.xdec_proj.bias", (d,), "small"))
+    k.append(("rep_decoder.qaux_proj.weight", (cfg.q_rep_aux_dim, 1), "randn"))
+    k.append(("rep_decoder.qaux_proj.bias", (cfg.q_rep_aux_dim,), "small"))
+    for i in range(cfg.num_layers):
+        _swdecoder(k, f"rep_decoder.layers.{i}.", d, cfg.d_ff, cfg.q_rep_aux_dim, cfg.pos_emb_dim)
+    k.append(("rep_decoder.out_proj.weight", (e, d), "linear"))
+    k.append(("rep_decoder.out_proj.bias", (e,), "small"))
+    return k
+
+
+def ssnd_state_dict(cfg: SSNDConfig, seed: int = 777):
+    return synthetic_state_dict(ssnd_layout(cfg), seed)
