@@ -382,15 +382,38 @@ void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  // Cooperative launch: the runtime checks the grid against the occupancy query and refuses a
-  // grid whose workgroups could not all be resident (hipErrorCooperativeLaunchTooLarge -> kErrHip)
-  // instead of letting the group hand-off wait on a workgroup that never starts.
-  const uint16_t* w = reinterpret_cast<const uint16_t*>(whh_bf16);
-  void* args[] = {(void*)&gx, (void*)&B, (void*)&T, (void*)&ndir, (void*)&w, (void*)&lengths, (void*)&h0,
-                  (void*)&c0, (void*)&out, (void*)&ldo, (void*)&hT, (void*)&cT, (void*)&hx, (void*)&Bp,
-                  (void*)&counters, (void*)&err};
-  SD_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>), dim3(4 * groups),
-                                    dim3(256), args, (unsigned)smem, st));
+  hipLaunchKernelGGL(lstm_group_bf16_kernel<MT>, dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
+                     reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
+                     counters, err);
+}
+
+// Workgroups of lstm_group_bf16_kernel<MT> the occupancy query admits per CU (0 if none fit).
+// This is the check hipLaunchCooperativeKernel would make (MI355X guide, "Residency and
+// cooperative launch": a plain launch of the same grid has the same residency); a cooperative
+// launch itself is avoided because its queue's teardown crashes rocprofv3's exit path here.
+template <int MT>
+int lstm_group_blocks_per_cu() {
+  static int nb = -1;
+  if (nb < 0) {
+    const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    int v = 0;
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT>, 256, smem));
+    nb = v;
+  }
+  return nb;
+}
+
+int lstm_group_capacity(int mt) {
+  switch (mt) {
+    case 1: return lstm_group_blocks_per_cu<1>();
+    case 2: return lstm_group_blocks_per_cu<2>();
+    case 3: return lstm_group_blocks_per_cu<3>();
+    case 4: return lstm_group_blocks_per_cu<4>();
+    case 5: return lstm_group_blocks_per_cu<5>();
+    default: return lstm_group_blocks_per_cu<6>();
+  }
 }
 
 int lstm_group_mt(int B, int ndir) {
@@ -400,8 +423,11 @@ int lstm_group_mt(int B, int ndir) {
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  for (int m = 1; m <= LS_MAXMT; ++m)   // smallest row block (16 * MT) whose 4 x groups fit one WG per CU
-    if (4 * ndir * cdiv(B, 16 * m) <= n_cu) return m;
+  // Smallest row block (16 * MT) whose 4 x groups fit one workgroup per CU, provided the occupancy
+  // query admits the kernel at all (co-residency of every workgroup of the grid); else 0 and the
+  // caller takes the per-step launches.
+  for (int m = 1; m <= LS_MAXMT; ++m)
+    if (4 * ndir * cdiv(B, 16 * m) <= n_cu) return lstm_group_capacity(m) >= 1 ? m : 0;
   return 0;
 }
 

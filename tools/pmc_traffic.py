@@ -19,7 +19,12 @@ from collections import defaultdict
 
 # sd_prof category -> HIP kernel symbols dispatched under it.
 CATEGORIES = {
-    "conv_gemm_bf16": r"gemm_\w*kernel|fcm_conv3x3\w*kernel",
+    "gemm_ring": r"gemm_ring_kernel",
+    "gemm_stream": r"gemm_stream_kernel",
+    "gemm_areg": r"gemm_areg_kernel",
+    "gemm_dma": r"gemm_dma_kernel",
+    "gemm_bf16_reg": r"gemm_bf16_kernel",
+    "fcm_conv3x3_band": r"fcm_conv3x3\w*kernel",
     "attention_bf16": r"attn_\w*kernel|attention\w*kernel",
     "lstm_recurrence": r"lstm\w*kernel",
     "dwconv": r"glu_dwconv_kernel",
