@@ -154,13 +154,30 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   layernorm(X, rows, E, E, L.f1_lng, L.f1_lnb, 1e-5f, y.p, E, bf, st);
   ffn_body(L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
   // self attention block (key_padding_mask from lengths)
-  add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
-  conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
-  AttnArgs a;
-  a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
-  a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
-  a.key_len = key_len;
-  attention(a, bf, st);
+  if (mha_block_supported(E, nh, T, bf)) {
+    // in-projection + attention in one launch (mha_block.hip); SDIAR_MHA_LN=1 also folds the residual
+    // add + self_attn_layer_norm into its prologue, else they run as the HBM-rate add_layernorm
+    static const bool fold_ln = getenv("SDIAR_MHA_LN") && atoi(getenv("SDIAR_MHA_LN")) == 1;
+    MhaBlockArgs m;
+    if (fold_ln) {
+      m.X = X; m.t = y.p;
+    } else {
+      add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
+      m.y = y.p;
+    }
+    m.ln_g = L.at_lng; m.ln_b = L.at_lnb; m.eps = 1e-5f;
+    m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
+    m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
+    mha_block(m, st);
+  } else {
+    add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
+    conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
+    AttnArgs a;
+    a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
+    a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
+    a.key_len = key_len;
+    attention(a, bf, st);
+  }
   conv_gemm(lin(ao, rows, E, L.out_proj, L.out_b, y, E), bf, st);
   // convolution module (no padding mask in torchaudio's conv module)
   add_layernorm(X, y.p, bf, rows, E, L.cv_lng, L.cv_lnb, 1e-5f, true, y.p, bf, st);

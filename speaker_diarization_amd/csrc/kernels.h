@@ -150,6 +150,31 @@ struct AttnArgs {
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
+// ---------------------------------------------------------------- mha_block.hip
+// Conformer self-attention block in one launch (bf16, D 384, 8 heads, T <= 160): X += t (t bf16,
+// nullable), y = LN(X) * g + b, q|k|v = y · W_inᵀ + bias (W_in packed bf16 (3D, D)), per head
+// softmax(q kᵀ * scale) v -> out (S*T rows of stride ldo, bf16).  key_len (device int32 per
+// sequence) optional.
+struct MhaBlockArgs {
+  float* X = nullptr;
+  const void* t = nullptr;
+  const void* y = nullptr;   // when set: bf16 rows already normalised; X / t / ln_* unused
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float eps = 1e-5f;
+  const void* W = nullptr;
+  const float* bias = nullptr;
+  void* out = nullptr;
+  int ldo = 0;
+  int S = 0, T = 0, D = 0, nh = 0;
+  float scale = 1.f;
+  const int* key_len = nullptr;
+  int probe = 0;   // timing probes (SDIAR_MHA_PROBE bits): 1 no attention, 2 no projection MFMA, 4 no
+                   // weight DMA, 8 no LayerNorm statistics pass — outputs are wrong with any bit set
+};
+bool mha_block_supported(int D, int nh, int T, bool bf16);
+void mha_block(const MhaBlockArgs& a, hipStream_t st);
+
 // ---------------------------------------------------------------- ssnd_ops.hip
 // Multi-head attention core on separate fp32 q / k / v row sets (SSND decoder cross and self
 // attention, ssnd_model.py:261-266): row i of batch b at ptr + b * bs + i * ld, head h at

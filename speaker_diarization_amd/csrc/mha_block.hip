@@ -1,0 +1,342 @@
+// Conformer self-attention block fused for gfx950 (C2: torchaudio ConformerLayer, ts_vad2/model.py:259-267,
+// restated in oracle/tsvad_ref.py conformer()): the residual add of the ffn1 output, self_attn_layer_norm,
+// the packed in-projection (Q, K, V) and the multi-head attention core in ONE launch.  Replaces
+// add_layernorm + the QKV GEMM (gemm_areg) + attn_short, whose (S*T, 3D) bf16 QKV intermediate made a
+// full HBM round trip (2.3 KiB per token each way at D = 384).
+//
+// A workgroup owns TWO sequences (10 waves; wave w: sequence w / 5, tokens 32 (w % 5) .. +31, i.e. two
+// 16-token MFMA row tiles), D = 384, 8 heads of 48:
+//   prologue  x = X + t (fp32), two-pass LayerNorm per token (row re-read from L1 between passes),
+//             X <- x; the normalised rows become the wave's MFMA B-operand fragments (2 x 16 tokens x
+//             384, 96 VGPRs), read once from HBM;
+//   pieces    16 in-projection rows (one head's 16 features of q, k or v), 12 KiB, stream through a
+//             3-slot LDS-DMA ring (buffer_load ... lds, 16-B chunk c of row r at c ^ (r & 7)), two pieces
+//             in flight behind counted vmcnt waits; each weight fragment read from LDS feeds both row
+//             tiles (the LDS read rate, not MFMA, bounded the one-tile-per-wave version); transposed MFMA
+//             (weights as A operand) leaves 4 consecutive features per lane for one token: + bias, q
+//             scaled by 1/sqrt(hd), 8-B LDS stores into the sequence's Q / K (row stride 64, features
+//             48..63 zero) and V (row stride 48) images;
+//   attention after a head's last V piece: Sᵀ = K·Qᵀ, online softmax, Oᵀ = Vᵀ·Pᵀ with Vᵀ from
+//             ds_read_b64_tr_b16 (the attn_short scheme), 8-B bf16 stores of the head's 48 features.
+// The in-projection weights (864 KiB bf16) come from L2 once per workgroup, i.e. once per two sequences;
+// HBM sees X (read + write, fp32), t and the attention output only.
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kD = 384, kHD = 48, kNH = 8;
+constexpr int kKT32 = kD / 32;                 // 32-wide k-steps of the projection
+constexpr int kKC = kD / 64;                   // 64-wide k-blocks of a weight piece
+constexpr int kTP = 160;                       // padded tokens per sequence
+constexpr int kSeq = 2;                        // sequences per workgroup
+constexpr int kWavesPerSeq = kTP / 32;         // 5 waves x 32 tokens
+constexpr int kWaves = kSeq * kWavesPerSeq;
+constexpr int kThreads = kWaves * 64;
+constexpr int kPR = 16;                        // weight rows per piece (one MFMA column tile)
+constexpr int kSlot = kKC * kPR * 64;          // bf16 elements per ring slot (12 KiB)
+constexpr int kNSlot = 3;
+constexpr int kDmaPerPiece = kKC * (kPR / 8);  // 1-KiB DMA instructions per piece (12)
+constexpr int kQS = 64;                        // Q / K row stride (features 48..63 stay zero)
+constexpr int kVS = 48;                        // V row stride
+constexpr int kSeqLds = 2 * kTP * kQS + kTP * kVS;   // bf16 elements of one sequence's Q, K, V images
+constexpr int kPieces = kNH * 3 * (kHD / kPR); // 72
+constexpr uint32_t kOOB = 0x80000000u;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+constexpr size_t kSmemBytes = sizeof(uint16_t) * ((size_t)kNSlot * kSlot + (size_t)kSeq * kSeqLds) +
+                              sizeof(float) * 3 * kD;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
+  extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
+  uint16_t* Ws = sm;                                          // [kNSlot][kKC][16][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lk = lane >> 4;
+  const int sq = w / kWavesPerSeq;                            // this wave's sequence slot
+  uint16_t* Qs = Ws + kNSlot * kSlot + sq * kSeqLds;          // [kTP][kQS]
+  uint16_t* Ks = Qs + kTP * kQS;                              // [kTP][kQS]
+  uint16_t* Vs = Ks + kTP * kQS;                              // [kTP][kVS]
+  float* s_bias = reinterpret_cast<float*>(Ws + kNSlot * kSlot + kSeq * kSeqLds);   // [3 * kD]
+  const int s = blockIdx.x * kSeq + sq;
+  const bool seq_ok = s < a.S;
+  const int T = a.T;
+  const int r0 = (w % kWavesPerSeq) * 32 + l15;               // token of row tile 0 (tile 1: +16)
+
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0,
+                                                                      (int)kOOB, 0x00020000);
+  const int lrow = lane >> 3, lch = lane & 7;
+  // Piece i: head h = i / 9, component c = (i / 3) % 3, feature tile ft = i % 3 -> in_proj rows
+  // c*D + 48h + 16ft .. +15, all K, as 12 1-KiB DMA instructions (k-block kc, 8-row group) over the
+  // waves (waves 0 and 1 issue two, the others one).
+  auto issue_piece = [&](int i) {
+    const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
+    uint16_t* slot = Ws + (i % kNSlot) * kSlot;
+    for (int j = w; j < kDmaPerPiece; j += kWaves) {
+      const int kc = j >> 1, rg = j & 1;
+      const int r = rg * 8 + lrow;
+      const uint32_t off =
+          (uint32_t)((((int64_t)(c * kD + h * kHD + ft * kPR + r)) * kD + kc * 64 + ((lch ^ (r & 7)) * 8)) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(slot + ((size_t)kc * kPR + rg * 8) * 64), 16, off, 0,
+                                               0, 0);
+    }
+  };
+  const int my_dma = (w < kDmaPerPiece - kWaves) ? 2 : 1;      // instructions this wave issues per piece
+  if (!(a.probe & 4)) {
+    issue_piece(0);
+    issue_piece(1);
+  }
+  for (int i = tid; i < 3 * kD; i += kThreads) s_bias[i] = a.bias[i];
+  for (int i = tid; i < kSeq * kTP * 2; i += kThreads) {   // zero Q/K features 48..63 (never written later)
+    const int q = i / (kTP * 2), r = (i >> 1) % kTP, c = kHD + (i & 1) * 8;
+    uint16_t* qs = Ws + kNSlot * kSlot + q * kSeqLds;
+    *reinterpret_cast<uint4*>(qs + r * kQS + c) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(qs + kTP * kQS + r * kQS + c) = make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  // ---- prologue: per row tile, x = X + t, LayerNorm, X <- x; af[rt][kk] = LN(x)[32kk + 8lk .. +7]
+  bf16x8 af[2][kKT32];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int row = r0 + 16 * rt;
+    const bool live = seq_ok && row < T;
+    const int64_t grow = (int64_t)s * T + row;
+    if (a.y) {   // already-normalised bf16 rows (the LayerNorm ran as its own HBM-rate kernel)
+      const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + grow * kD;
+#pragma unroll
+      for (int kk = 0; kk < kKT32; ++kk)
+        af[rt][kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(yr + 32 * kk + 8 * lk)
+                                                     : make_uint4(0u, 0u, 0u, 0u));
+      continue;
+    }
+    const float* xr = a.X + grow * kD;
+    const uint16_t* tr = reinterpret_cast<const uint16_t*>(a.t) + grow * kD;
+    auto load8 = [&](int kk, float* v) {
+      const int k = 32 * kk + 8 * lk;
+      const float4 x0 = *reinterpret_cast<const float4*>(xr + k);
+      const float4 x1 = *reinterpret_cast<const float4*>(xr + k + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      if (a.t) {
+        const uint4 tv = *reinterpret_cast<const uint4*>(tr + k);
+        const uint32_t tw[4] = {tv.x, tv.y, tv.z, tv.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[2 * u] += __uint_as_float(tw[u] << 16);
+          v[2 * u + 1] += __uint_as_float(tw[u] & 0xffff0000u);
+        }
+      }
+    };
+    float mean = 0.f, rstd = 0.f;
+    if (live && !(a.probe & 8)) {
+      float sum = 0.f;
+      for (int kk = 0; kk < kKT32; ++kk) {
+        float v[8];
+        load8(kk, v);
+        sum += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+      }
+      asm volatile("" ::: "memory");   // re-read the row below (L1 hit) instead of keeping 96 values live
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      mean = sum / (float)kD;
+      float q = 0.f;
+      for (int kk = 0; kk < kKT32; ++kk) {
+        float v[8];
+        load8(kk, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q += (v[j] - mean) * (v[j] - mean);
+      }
+      asm volatile("" ::: "memory");
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      rstd = rsqrtf(q / (float)kD + a.eps);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kKT32; ++kk) {
+      uint32_t pk[4] = {0u, 0u, 0u, 0u};
+      if (live) {
+        const int k = 32 * kk + 8 * lk;
+        float v[8];
+        load8(kk, v);
+        if (a.t) {
+          float* xw = a.X + grow * kD + k;
+          *reinterpret_cast<float4*>(xw) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(xw + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+        const float4 g0 = *reinterpret_cast<const float4*>(a.ln_g + k);
+        const float4 g1 = *reinterpret_cast<const float4*>(a.ln_g + k + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(a.ln_b + k);
+        const float4 b1 = *reinterpret_cast<const float4*>(a.ln_b + k + 4);
+        const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          pk[u] = pack_bf16x2((v[2 * u] - mean) * rstd * gg[2 * u] + bb[2 * u],
+                              (v[2 * u + 1] - mean) * rstd * gg[2 * u + 1] + bb[2 * u + 1]);
+      }
+      af[rt][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      asm volatile("" ::: "memory");   // one k-step's loads at a time (register pressure)
+    }
+  }
+
+  const int klen = seq_ok ? (a.key_len ? min(a.key_len[s], T) : T) : 0;
+  const int tr_off = ((4 * lk + (l15 >> 2)) * kVS + 4 * (l15 & 3)) * 2;
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
+  bool drain = true;   // VMEM ops younger than the last DMA issue are pending: wait for everything
+
+  for (int i = 0; i < kPieces; ++i) {
+    // Piece i landed: the only younger DMA is piece i+1's (this wave's my_dma instructions), unless
+    // stores were issued after it (prologue X stores, attention outputs) -> full drain.
+    if (drain || i + 1 >= kPieces || (a.probe & 4)) wait_vm<0>();
+    else if (my_dma == 2) wait_vm<2>();
+    else wait_vm<1>();
+    drain = false;
+    __syncthreads();   // every wave's part of piece i is in LDS; slot (i+2) % 3 (piece i-1) is free
+    if (i + 2 < kPieces && !(a.probe & 4)) issue_piece(i + 2);
+    const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
+    const uint16_t* slot = Ws + (i % kNSlot) * kSlot;
+    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    auto wfrag = [&](int kk) {
+      const int kc = kk >> 1, cc = (kk & 1) * 4 + lk;
+      return *reinterpret_cast<const bf16x8*>(slot + (kc * kPR + l15) * 64 + ((cc ^ (l15 & 7)) * 8));
+    };
+    // The fragment of k-step kk + 1 is read while kk's two MFMAs run; the empty asm keeps the
+    // compiler from hoisting every step's reads to the top.
+    bf16x8 wcur = wfrag(0);
+#pragma unroll
+    for (int kk = 0; kk < kKT32; ++kk) {
+      bf16x8 wnext = wcur;
+      if (kk + 1 < kKT32) wnext = wfrag(kk + 1);
+      if (!(a.probe & 2)) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
+      }
+      asm volatile("" ::: "memory");
+      wcur = wnext;
+    }
+    // lane holds features 16ft + 4lk + r of token r0 + 16rt
+    uint16_t* dst = c == 0 ? Qs : (c == 1 ? Ks : Vs);
+    const int ld = c == 2 ? kVS : kQS;
+    const float scl = c == 0 ? a.scale : 1.f;
+    const int n0 = ft * 16 + 4 * lk;
+    const float4 bv = *reinterpret_cast<const float4*>(s_bias + c * kD + h * kHD + n0);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+      *reinterpret_cast<uint2*>(dst + (r0 + 16 * rt) * ld + n0) =
+          make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
+                     pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
+    if (c != 2 || ft != 2) continue;
+    __syncthreads();   // head h's Q, K, V images complete (both sequences)
+    if ((a.probe & 1) || !seq_ok) continue;
+
+    // ---- attention of head h for this wave's two 16-query tiles
+#pragma unroll 1
+    for (int rt = 0; rt < 2; ++rt) {
+      const int row = r0 + 16 * rt;
+      bf16x8 qf[2];
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(Qs + row * kQS + kc * 32 + lk * 8);
+      floatx4 o[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      float m_run = -INFINITY, l_run = 0.f;
+      for (int k0 = 0; k0 < klen; k0 += 32) {
+        floatx4 sc[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          floatx4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < 2; ++kc) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + st * 16 + l15) * kQS + kc * 32 + lk * 8);
+            sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], sacc, 0, 0, 0);
+          }
+          sc[st] = sacc;
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + st * 16 + lk * 4 + r;
+            const float v = key < klen ? sc[st][r] : -INFINITY;
+            sc[st][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = (m_new == -INFINITY) ? 0.f : __expf(sc[st][r] - m_new);
+            sc[st][r] = pv;
+            psum += pv;
+          }
+        psum += __shfl_xor(psum, 16, 64);
+        psum += __shfl_xor(psum, 32, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+        bf16x8 pb;   // Pᵀ operand: k-index 8g + j <-> key k0 + 4g + j (j < 4), k0 + 16 + 4g + j - 4
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sc[j >> 2][j & 3];
+        const uint32_t vbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)Vs) +
+                               (uint32_t)(k0 * kVS * 2) + (uint32_t)tr_off;
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt) {
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + 16 * kVS * 2 + dt * 32));
+          const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
+        }
+      }
+      if (row < T) {
+        const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + ((int64_t)s * T + row) * a.ldo + h * kHD;
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt)
+          *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * lk) =
+              make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+        drain = true;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool mha_block_supported(int D, int nh, int T, bool bf16) {
+  static const bool off = getenv("SDIAR_NO_MHA_BLOCK") != nullptr;   // A/B switch: the unfused path
+  return !off && bf16 && D == kD && nh == kNH && T >= 1 && T <= kTP;
+}
+
+void mha_block(const MhaBlockArgs& a, hipStream_t st) {
+  SD_CHECK(mha_block_supported(kD, a.nh, a.T, true) && a.D == kD, kErrInvalid, "mha_block: unsupported shape");
+  SD_CHECK(a.ldo % 4 == 0, kErrInvalid, "mha_block: output row stride must be a multiple of 4");
+  if (a.S <= 0) return;
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
+    attr = true;
+  }
+  const double rows = (double)a.S * a.T;
+  const double flops = 2.0 * rows * 3 * kD * kD + 4.0 * a.S * (double)a.T * a.T * kD;
+  const double bytes = rows * kD * (a.y ? 2.0 + 2.0 : 4.0 + (a.t ? 2.0 + 4.0 : 0.0) + 2.0) + 2.0 * 3 * kD * kD;
+  ProfScope prof("mha_block", flops, bytes, st);
+  static const int probe = getenv("SDIAR_MHA_PROBE") ? atoi(getenv("SDIAR_MHA_PROBE")) : 0;
+  MhaBlockArgs b = a;
+  b.probe = probe;
+  hipLaunchKernelGGL(mha_block_kernel, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd
