@@ -65,7 +65,7 @@ WORKLOADS = {
 
 PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                        # GB/s
-ATTN_KERNELS = ("attention_bf16", "attention_f32")
+ATTN_KERNELS = ("mha_block", "attention_bf16", "attention_f32")   # fused block first (C2 conformer)
 
 
 def parse():
