@@ -185,6 +185,8 @@ _SIGS = {
                                 c_void_p]),
     "sd_op_attention_chunk": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                       c_void_p]),
+    "sd_probe_attention_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                        c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "sd_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "sd_op_lstm": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p]),

@@ -28,6 +28,23 @@ __device__ __forceinline__ KeyWindow chunk_window(const AttnArgs& a, int q) {
   const int qc = q / a.chunk;
   return {a.left < 0 ? 0 : max(0, qc - a.left) * a.chunk, (qc + 1) * a.chunk};
 }
+// Key visibility of query myq (key_len, causal and chunk terms).  mask_form 1 is the per-key
+// division form of the chunk term, mask_form 2 that form over the unclipped key range 0 .. klen
+// (the round-1 kernel before the key-window change); diagnostics only (sd_probe_attention_mask).
+// a.mask_dump records the decision of every visited (query, key) pair of sequence 0, head 0.
+__device__ __forceinline__ bool key_visible(const AttnArgs& a, const KeyWindow& kw, int klen, int key, int myq) {
+  bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
+  if (a.mask_form != 0 && a.chunk) {
+    const int kc = key / a.chunk, qc = myq / a.chunk;
+    ok = ok && kc <= qc && (a.left < 0 || kc >= qc - a.left);
+  } else {
+    ok = ok && key >= kw.lo && key < kw.hi;
+  }
+  return ok;
+}
+__device__ __forceinline__ void dump_mask(const AttnArgs& a, int s, int h, int T, int key, int myq, bool ok) {
+  if (a.mask_dump && s == 0 && h == 0 && myq < T && key < T) a.mask_dump[(int64_t)myq * T + key] = ok ? 1 : 2;
+}
 constexpr int kKT = 32;   // keys per tile
 
 constexpr int f32_stride(int hd) { return hd + (((4 - hd) % 32) + 32) % 32; }
@@ -98,9 +115,10 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const KeyWindow kw = chunk_window(a, myq);
   int k_end = klen;
   if (a.causal) k_end = min(k_end, blockIdx.x * kQB + kQB + a.causal_delay);
-  if (a.chunk) k_end = min(k_end, ((blockIdx.x * kQB + kQB - 1) / a.chunk + 1) * a.chunk);
+  const bool clip = a.chunk && a.mask_form != 2;
+  if (clip) k_end = min(k_end, ((blockIdx.x * kQB + kQB - 1) / a.chunk + 1) * a.chunk);
   // left >= 0: tiles wholly before the block's first query window hold no visible key
-  const int k_begin = (a.chunk && a.left >= 0) ? chunk_window(a, blockIdx.x * kQB).lo / kKT * kKT : 0;
+  const int k_begin = (clip && a.left >= 0) ? chunk_window(a, blockIdx.x * kQB).lo / kKT * kKT : 0;
   for (int k0 = k_begin; k0 < k_end; k0 += kKT) {
     __syncthreads();
     // Stage K and V for keys [k0, k0+32).
@@ -176,7 +194,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int key = k0 + st * 16 + g * 4 + r;
-        bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay) && key >= kw.lo && key < kw.hi;
+        bool ok = key_visible(a, kw, klen, key, myq);
+        dump_mask(a, s, h, T, key, myq, ok);
         float v = ok ? sc[st][r] : -INFINITY;
         sc[st][r] = v;
         tmax = fmaxf(tmax, v);
@@ -362,8 +381,9 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
       const KeyWindow kw = chunk_window(a, myq);
       int k_end = klen;
       if (a.causal) k_end = min(k_end, q0 + 16 + a.causal_delay);
-      if (a.chunk) k_end = min(k_end, ((q0 + 15) / a.chunk + 1) * a.chunk);
-      const int k_begin = (a.chunk && a.left >= 0) ? chunk_window(a, q0).lo / 32 * 32 : 0;
+      const bool clip = a.chunk && a.mask_form != 2;
+      if (clip) k_end = min(k_end, ((q0 + 15) / a.chunk + 1) * a.chunk);
+      const int k_begin = (clip && a.left >= 0) ? chunk_window(a, q0).lo / 32 * 32 : 0;
       for (int k0 = k_begin; k0 < k_end; k0 += 32) {
         floatx4 sc[2];
 #pragma unroll
@@ -382,7 +402,8 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = k0 + st * 16 + g * 4 + r;
-            const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay) && key >= kw.lo && key < kw.hi;
+            const bool ok = key_visible(a, kw, klen, key, myq);
+            dump_mask(a, s, h, T, key, myq, ok);
             const float v = ok ? sc[st][r] : -INFINITY;
             sc[st][r] = v;
             tmax = fmaxf(tmax, v);
@@ -485,7 +506,11 @@ void launch_hd(const AttnArgs& a, bool bf16, hipStream_t st) {
 
 }  // namespace
 
-void attention(const AttnArgs& a, bool bf16, hipStream_t st) {
+void attention(const AttnArgs& a_in, bool bf16, hipStream_t st) {
+  // SDIAR_ATTN_MASK_FORM=1|2 runs whole models with a diagnostic chunk-term form (see key_visible)
+  static const int env_form = getenv("SDIAR_ATTN_MASK_FORM") ? atoi(getenv("SDIAR_ATTN_MASK_FORM")) : 0;
+  AttnArgs a = a_in;
+  if (!a.mask_form && env_form >= 1 && env_form <= 2) a.mask_form = env_form;
   SD_CHECK(a.nh > 0 && a.D % a.nh == 0, kErrInvalid, "attention: D % nh != 0");
   SD_CHECK(a.ld_qkv % 4 == 0 && a.D % 4 == 0, kErrInvalid, "attention: ld_qkv % 4 != 0");
   const int hd = a.D / a.nh;

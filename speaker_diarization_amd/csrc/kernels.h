@@ -147,6 +147,11 @@ struct AttnArgs {
   int64_t seq_outer = 0;
   int seq_inner_stride = 0;
   int tok_stride = 1;
+  // Diagnostics (sd_probe_attention_mask): 1 = per-key division form of the chunk term, 2 = that
+  // form over the unclipped key range (the round-1 kernel);
+  // mask_dump (T*T int32, zeroed) receives 1/2 = visible/masked for each visited pair of seq 0, head 0.
+  int mask_form = 0;
+  int* mask_dump = nullptr;
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
