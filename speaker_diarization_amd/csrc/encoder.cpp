@@ -108,6 +108,24 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
   { ConvL a = linear(p + ".ffn2.sequential.1"); L.f2_w1 = a.w; L.f2_b1 = a.beta; }
   { ConvL a = linear(p + ".ffn2.sequential.4", 0.5f); L.f2_w2 = a.w; L.f2_b2 = a.beta; }
   L.fin_g = up(p + ".final_layer_norm.weight"); L.fin_b = up(p + ".final_layer_norm.bias");
+  if (bf16 && rowprog_supported(L.out_proj.N, L.f1_w1.N, true) && L.f2_w1.N == L.f1_w1.N &&
+      L.pw2.N == L.out_proj.N && L.pw2.K == L.out_proj.N) {
+    auto put = [&](const std::vector<uint16_t>& h) {
+      void* d = arena.alloc(h.size() * 2);
+      SD_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+      return static_cast<const void*>(d);
+    };
+    auto w32 = [&](const std::string& key, float mult) {
+      int N, Cin, kh, kw;
+      return ps.pack(key, N, Cin, kh, kw, mult);
+    };
+    const int E = L.out_proj.N, Hd = L.f1_w1.N;
+    L.rp_hidden = Hd;
+    L.rp_f1 = put(rowprog_pack_ffn(w32(p + ".ffn1.sequential.1.weight", 1.f), w32(p + ".ffn1.sequential.4.weight", 0.5f), Hd));
+    L.rp_f2 = put(rowprog_pack_ffn(w32(p + ".ffn2.sequential.1.weight", 1.f), w32(p + ".ffn2.sequential.4.weight", 0.5f), Hd));
+    L.rp_out = put(rowprog_pack_pre(w32(p + ".self_attn.out_proj.weight", 1.f), E, E));
+    L.rp_pw2 = put(rowprog_pack_pre(w32(p + ".conv_module.sequential.5.weight", 1.f), E, E));
+  }
   return L;
 }
 
@@ -198,6 +216,84 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   add_layernorm(X, y.p, bf, rows, E, L.f2_lng, L.f2_lnb, 1e-5f, true, y.p, bf, st);
   ffn_body(L.f2_w1, L.f2_b1, L.f2_w2, L.f2_b2);
   add_layernorm(X, y.p, bf, rows, E, L.fin_g, L.fin_b, 1e-5f, false, X, false, st);
+}
+
+void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int T, int E, int nh, int kernel,
+                         const int* key_len, const EncoderWork& w, hipStream_t st) {
+  bool fused = w.bf16 && !Ls.empty();
+  for (const ConformerL& L : Ls) fused = fused && L.rp_f1 && rowprog_supported(E, L.rp_hidden, true);
+  if (!fused) {
+    for (const ConformerL& L : Ls) run_conformer(L, X, S, T, E, nh, kernel, key_len, w, st);
+    return;
+  }
+  // Per layer: [ffn1 + attn-LN] (first layer only; later layers get it from the previous program) ->
+  // attention on y -> [out_proj + residual + conv-LN] -> pw1/GLU -> dwconv (-> GroupNorm+SiLU) ->
+  // [pw2 + residual + ffn2 + final LN (+ next layer's ffn1 + attn-LN)].  X stays the fp32 residual stream.
+  const int rows = S * T;
+  const Tens y{w.Y, true}, qkv{w.QKV, true}, ao{w.AO, true}, h{w.H, true};
+  auto ffn = [](const ConformerL& L, bool second) {
+    RowFfnArgs f;
+    f.w = second ? L.rp_f2 : L.rp_f1;
+    f.hidden = L.rp_hidden;
+    f.ln_g = second ? L.f2_lng : L.f1_lng;
+    f.ln_b = second ? L.f2_lnb : L.f1_lnb;
+    f.b1 = second ? L.f2_b1 : L.f1_b1;
+    f.b2 = second ? L.f2_b2 : L.f1_b2;
+    if (second) { f.post_g = L.fin_g; f.post_b = L.fin_b; }
+    return f;
+  };
+  {
+    RowProgArgs r;
+    r.X = X; r.Xo = X; r.M = rows;
+    r.n_ffn = 1; r.ffn[0] = ffn(Ls[0], false);
+    r.y = y.p; r.y_g = Ls[0].at_lng; r.y_b = Ls[0].at_lnb;
+    rowprog(r, "rowprog_ffn", st);
+  }
+  for (size_t li = 0; li < Ls.size(); ++li) {
+    const ConformerL& L = Ls[li];
+    if (mha_block_supported(E, nh, T, true)) {
+      MhaBlockArgs m;
+      m.y = y.p;
+      m.ln_g = L.at_lng; m.ln_b = L.at_lnb; m.eps = 1e-5f;
+      m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
+      m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
+      mha_block(m, st);
+    } else {
+      conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), true, st);
+      AttnArgs a;
+      a.qkv = qkv.p; a.io_bf16 = true; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
+      a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
+      a.key_len = key_len;
+      attention(a, true, st);
+    }
+    {
+      RowProgArgs r;
+      r.X = X; r.Xo = X; r.M = rows;
+      r.A = ao.p; r.w0 = L.rp_out; r.b0 = L.out_b;
+      r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
+      rowprog(r, "rowprog_out", st);
+    }
+    ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
+    p1.glu = 1;
+    const bool glu_epi = gemm_stream_supported(p1);
+    if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
+    conv_gemm(p1, true, st);
+    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
+               !glu_epi, true, st);
+    if (L.group_norm) groupnorm_silu(ao.p, S, T, E, w.partial, L.gn_g, L.gn_b, 1e-5f, true, st);
+    {
+      RowProgArgs r;
+      r.X = X; r.Xo = X; r.M = rows;
+      r.A = ao.p; r.w0 = L.rp_pw2; r.b0 = L.pw2_b;
+      r.n_ffn = 1; r.ffn[0] = ffn(L, true);
+      if (li + 1 < Ls.size()) {
+        const ConformerL& Ln = Ls[li + 1];
+        r.n_ffn = 2; r.ffn[1] = ffn(Ln, false);
+        r.y = y.p; r.y_g = Ln.at_lng; r.y_b = Ln.at_lnb;
+      }
+      rowprog(r, "rowprog_pw2_ffn", st);
+    }
+  }
 }
 
 }  // namespace sd

@@ -5,6 +5,7 @@
 // in bf16 mode.
 #pragma once
 #include <string>
+#include <vector>
 #include "kernels.h"
 #include "params.h"
 
@@ -46,6 +47,9 @@ struct ConformerL {       // torchaudio.models.conformer.ConformerLayer (conv af
   const float *f2_lng, *f2_lnb, *f2_b1, *f2_b2;
   PackedW f2_w1, f2_w2;
   const float *fin_g, *fin_b;
+  // rowprog.hip pieces (bf16 mode, D 384): ffn1 / ffn2 (W1 | ½W2), out_proj, pointwise_conv2
+  const void *rp_f1 = nullptr, *rp_f2 = nullptr, *rp_out = nullptr, *rp_pw2 = nullptr;
+  int rp_hidden = 0;
 };
 
 // Reads reference state_dict entries (strict: every key it touches is marked used).
@@ -76,5 +80,9 @@ void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int n
                      const EncoderWork& w, hipStream_t st, int causal = 0, int causal_delay = 0);
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
                    const int* key_len, const EncoderWork& w, hipStream_t st);
+// All layers of a torchaudio Conformer; runs the per-token parts as rowprog.hip programs when every
+// layer has its pieces (bf16, D 384), else run_conformer per layer.
+void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int T, int E, int nh, int kernel,
+                         const int* key_len, const EncoderWork& w, hipStream_t st);
 
 }  // namespace sd

@@ -1,6 +1,7 @@
 // Launchers for the gfx950 kernels (internal C++ API; the C-ABI is in capi.cpp).
 #pragma once
 #include <type_traits>
+#include <vector>
 #include "common.h"
 
 namespace sd {
@@ -178,6 +179,36 @@ struct MhaBlockArgs {
                    // weight DMA, 8 no LayerNorm statistics pass — outputs are wrong with any bit set
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
+
+// ---------------------------------------------------------------- rowprog.hip
+// Conformer per-token row program (bf16 weights, D 384): acc = X; [acc += A·W0ᵀ + b0];
+// per FFN i: acc += W2·silu(W1·LN_i(acc) + b1) + b2 (the ½ folded into W2 / b2), [acc = LN_post_i(acc)];
+// Xo = acc (may alias X); [y = LN_y(acc) bf16].  Weights packed by rowprog_pack_pre / rowprog_pack_ffn.
+struct RowFfnArgs {
+  const void* w = nullptr;     // rowprog_pack_ffn pieces
+  int hidden = 0;
+  const float *ln_g = nullptr, *ln_b = nullptr;
+  const float *b1 = nullptr, *b2 = nullptr;
+  const float *post_g = nullptr, *post_b = nullptr;
+};
+struct RowProgArgs {
+  const float* X = nullptr;
+  float* Xo = nullptr;
+  int M = 0;
+  const void* A = nullptr;     // (M, 384) bf16 rows of the pre-GEMM
+  const void* w0 = nullptr;    // rowprog_pack_pre pieces (384 x 384)
+  const float* b0 = nullptr;
+  int n_ffn = 0;
+  RowFfnArgs ffn[2];
+  const float *y_g = nullptr, *y_b = nullptr;
+  void* y = nullptr;
+  float eps = 1e-5f;
+};
+bool rowprog_supported(int D, int hidden, bool bf16);
+void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);
+// Host packers (bf16 MFMA fragment pieces): W0 (384, 384) row-major; W1 (hidden, 384), W2 (384, hidden).
+std::vector<uint16_t> rowprog_pack_pre(const std::vector<float>& W, int N, int K);
+std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::vector<float>& W2, int hidden);
 void mha_block(const MhaBlockArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------- ssnd_ops.hip

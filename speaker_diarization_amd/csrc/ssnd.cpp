@@ -246,7 +246,7 @@ void SsndModel::infer(const float* feats, const float* spk, int B, int Tf, float
   // encoder: input_proj + Conformer (all frames valid: lengths = T, :191)
   conv_gemm(lin(Tens{x_, false}, B * T, E, enc_in_.w, enc_in_.beta, Tens{X_, false}, D), bf, st);
   const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf};
-  for (const ConformerL& L : conf_) run_conformer(L, X_, B, T, D, cfg_.nhead, cfg_.conformer_kernel, nullptr, w, st);
+  run_conformer_stack(conf_, X_, B, T, D, cfg_.nhead, cfg_.conformer_kernel, nullptr, w, st);
   decode(X_, x_, spk, B, T, vad, emb, st);
 }
 

@@ -138,8 +138,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
              "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
     gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
     build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
-    for (const auto& L : conf_)
-      run_conformer(L, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
+    run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
     speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
