@@ -121,8 +121,14 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
     };
     const int E = L.out_proj.N, Hd = L.f1_w1.N;
     L.rp_hidden = Hd;
-    L.rp_f1 = put(rowprog_pack_ffn(w32(p + ".ffn1.sequential.1.weight", 1.f), w32(p + ".ffn1.sequential.4.weight", 0.5f), Hd));
-    L.rp_f2 = put(rowprog_pack_ffn(w32(p + ".ffn2.sequential.1.weight", 1.f), w32(p + ".ffn2.sequential.4.weight", 0.5f), Hd));
+    for (int f = 1; f <= 2; ++f) {
+      const std::string q = p + ".ffn" + std::to_string(f) + ".sequential.";
+      std::vector<float> b1;
+      const void* w = put(rowprog_pack_ffn(w32(q + "1.weight", 1.f), w32(q + "4.weight", 0.5f), Hd, ps.get(q + "0.weight").data,
+                                           ps.get(q + "0.bias").data, ps.get(q + "1.bias").data, b1));
+      (f == 1 ? L.rp_f1 : L.rp_f2) = w;
+      (f == 1 ? L.rp_f1_b1 : L.rp_f2_b1) = arena.upload(b1);
+    }
     L.rp_out = put(rowprog_pack_pre(w32(p + ".self_attn.out_proj.weight", 1.f), E, E));
     L.rp_pw2 = put(rowprog_pack_pre(w32(p + ".conv_module.sequential.5.weight", 1.f), E, E));
   }
@@ -235,9 +241,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
     f.hidden = L.rp_hidden;
-    f.ln_g = second ? L.f2_lng : L.f1_lng;
-    f.ln_b = second ? L.f2_lnb : L.f1_lnb;
-    f.b1 = second ? L.f2_b1 : L.f1_b1;
+    f.b1 = second ? L.rp_f2_b1 : L.rp_f1_b1;
     f.b2 = second ? L.f2_b2 : L.f1_b2;
     if (second) { f.post_g = L.fin_g; f.post_b = L.fin_b; }
     return f;

@@ -185,10 +185,9 @@ bool mha_block_supported(int D, int nh, int T, bool bf16);
 // per FFN i: acc += W2·silu(W1·LN_i(acc) + b1) + b2 (the ½ folded into W2 / b2), [acc = LN_post_i(acc)];
 // Xo = acc (may alias X); [y = LN_y(acc) bf16].  Weights packed by rowprog_pack_pre / rowprog_pack_ffn.
 struct RowFfnArgs {
-  const void* w = nullptr;     // rowprog_pack_ffn pieces
+  const void* w = nullptr;     // rowprog_pack_ffn pieces (the FFN's LayerNorm affine folded in)
   int hidden = 0;
-  const float *ln_g = nullptr, *ln_b = nullptr;
-  const float *b1 = nullptr, *b2 = nullptr;
+  const float *b1 = nullptr, *b2 = nullptr;   // b1 folded by rowprog_pack_ffn
   const float *post_g = nullptr, *post_b = nullptr;
 };
 struct RowProgArgs {
@@ -208,7 +207,10 @@ bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);
 // Host packers (bf16 MFMA fragment pieces): W0 (384, 384) row-major; W1 (hidden, 384), W2 (384, hidden).
 std::vector<uint16_t> rowprog_pack_pre(const std::vector<float>& W, int N, int K);
-std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::vector<float>& W2, int hidden);
+// The FFN's LayerNorm (ln_g, ln_b) is folded: W1' = W1 diag(ln_g), b1_folded = W1 ln_b + b1.
+std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::vector<float>& W2, int hidden,
+                                       const std::vector<float>& ln_g, const std::vector<float>& ln_b,
+                                       const std::vector<float>& b1, std::vector<float>& b1_folded);
 void mha_block(const MhaBlockArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------- ssnd_ops.hip

@@ -37,17 +37,16 @@ namespace {
 constexpr int kD = 384;
 constexpr int kFT = kD / 16;          // 24 feature tiles of 16
 constexpr int kKK = kD / 32;          // 12 k-steps over D
-constexpr int kWaves = 8;             // two per SIMD
-constexpr int kThreads = 64 * kWaves;
-constexpr int kRows = 16 * kWaves;    // tokens per tile (one 16-token MFMA column tile per wave)
+constexpr int kRows = 128;            // tokens per tile
 constexpr int kFrag = 512;            // bf16 per fragment (64 lanes x 8)
 constexpr int kPieceFrags = 24;
 constexpr int kPiece = kPieceFrags * kFrag;   // 12288 bf16 = 24 KiB
 constexpr int kNSlot = 5;
-constexpr int kDmaPerWave = kPieceFrags / kWaves;   // 3 x 1 KiB per wave and piece
 constexpr int kMaxHidden = 1024;
-// LDS parameter block (floats): b0 | per FFN: ln_g ln_b post_g post_b b2 (D each) b1 (kMaxHidden) | y_g y_b
-constexpr int kPrmFfn = 5 * kD + kMaxHidden;
+constexpr int kPD = 3;                // fragment reads in flight ahead of the MFMA that uses them
+constexpr int kRefillAt = 3;          // the DMA refill is issued after this many MFMAs of a piece
+// LDS parameter block (floats): b0 | per FFN: post_g post_b b2 (D each) b1 (kMaxHidden) | y_g y_b
+constexpr int kPrmFfn = 3 * kD + kMaxHidden;
 constexpr int kPrmB0 = 0, kPrmFfn0 = kD, kPrmY = kD + 2 * kPrmFfn;
 constexpr int kPrmFloats = (kPrmY + 2 * kD + 255) / 256 * 256;   // padded to whole KiB
 constexpr size_t kSmemBytes = sizeof(uint16_t) * (size_t)kNSlot * kPiece + sizeof(float) * kPrmFloats;
@@ -59,19 +58,24 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// Piece g has landed once at most `younger` pieces' DMAs (kDmaPerWave per wave each) are outstanding; any other
+// Piece g has landed once at most `younger` pieces' DMAs (DPW per wave each) are outstanding; any other
 // VMEM operation issued after g's DMAs only makes the count conservative.
+template <int DPW>
 __device__ __forceinline__ void wait_piece(int younger) {
   static_assert(kNSlot == 5, "wait_piece counts");
   if (younger <= 0) wait_vm<0>();
-  else if (younger == 1) wait_vm<kDmaPerWave>();
-  else if (younger == 2) wait_vm<2 * kDmaPerWave>();
-  else wait_vm<3 * kDmaPerWave>();
+  else if (younger == 1) wait_vm<DPW>();
+  else if (younger == 2) wait_vm<2 * DPW>();
+  else wait_vm<3 * DPW>();
 }
 
 __device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
 
+// TT 16-token MFMA column tiles per wave; 8 / TT waves per 128-token tile.
+template <int TT>
 struct Ring {
+  static constexpr int kWaves = 8 / TT;
+  static constexpr int kDpw = kPieceFrags / kWaves;   // 1-KiB DMA instructions per wave and piece
   const uint16_t *w0, *wf0, *wf1;   // piece sources: pre-GEMM, FFN 0, FFN 1
   uint16_t* ring;
   int P;        // pieces per tile
@@ -79,6 +83,7 @@ struct Ring {
   int n_f0;     // pieces of FFN 0
   int total;    // pieces this workgroup consumes
   int w, lane;
+  bool dma;     // probe: false skips the weight stream
 
   __device__ __forceinline__ const uint16_t* src(int q) const {
     if (q < n_pre) return w0 + (size_t)q * kPiece;
@@ -87,36 +92,42 @@ struct Ring {
     return wf1 + (size_t)(q - n_f0) * kPiece;
   }
   __device__ __forceinline__ void issue(int g) const {
-    if (g >= total) return;
+    if (g >= total || !dma) return;
     const uint16_t* s = src(g % P);
     uint16_t* slot = ring + (g % kNSlot) * kPiece;
 #pragma unroll
-    for (int j = 0; j < kDmaPerWave; ++j) {
+    for (int j = 0; j < kDpw; ++j) {
       const int f = w + kWaves * j;
       __builtin_amdgcn_global_load_lds((const void*)(s + f * kFrag + lane * 8), (lds_ptr_t)(slot + f * kFrag), 16,
                                        0, 0);
     }
   }
-  // Wait for piece g, make every wave's part visible, refill the slot of piece g - 1, return g's slot.
-  __device__ __forceinline__ const uint16_t* next(int& g) const {
-    wait_piece(min(kNSlot - 2, total - 1 - g));
+  // Wait for piece g and make every wave's part visible; returns g's slot.  The slot of piece g - 1 is
+  // free from here on: refill(g) (called a few MFMAs into the piece) streams piece g + kNSlot - 1 into it.
+  __device__ __forceinline__ const uint16_t* wait(int g) const {
+    wait_piece<kDpw>(min(kNSlot - 2, total - 1 - g));
     __syncthreads();
-    issue(g + kNSlot - 1);
-    const uint16_t* slot = ring + (g % kNSlot) * kPiece;
-    ++g;
-    return slot;
+    return ring + (g % kNSlot) * kPiece;
   }
+  __device__ __forceinline__ void refill(int g) const { issue(g + kNSlot - 1); }
 };
 
 __device__ __forceinline__ bf16x8 frag(const uint16_t* slot, int f, int lane) {
   return *reinterpret_cast<const bf16x8*>(slot + f * kFrag + lane * 8);
 }
 
-// LayerNorm statistics of this lane's token (two-pass, biased variance, as torch).
-__device__ __forceinline__ void ln_stats(const floatx4 (&acc)[kFT], float eps, float& mean, float& rstd) {
+template <bool ON>
+__device__ __forceinline__ floatx4 mfma(const bf16x8& a, const bf16x8& b, const floatx4& c) {
+  if constexpr (ON) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return c;
+}
+
+// LayerNorm statistics of this lane's token of column tile tt (two-pass, biased variance, as torch).
+template <int TT>
+__device__ __forceinline__ void ln_stats(const floatx4 (&acc)[kFT][TT], int tt, float eps, float& mean, float& rstd) {
   float s = 0.f;
 #pragma unroll
-  for (int ft = 0; ft < kFT; ++ft) s += (acc[ft][0] + acc[ft][1]) + (acc[ft][2] + acc[ft][3]);
+  for (int ft = 0; ft < kFT; ++ft) s += (acc[ft][tt][0] + acc[ft][tt][1]) + (acc[ft][tt][2] + acc[ft][tt][3]);
   s += __shfl_xor(s, 16, 64);
   s += __shfl_xor(s, 32, 64);
   const float m = s * (1.f / kD);
@@ -124,24 +135,30 @@ __device__ __forceinline__ void ln_stats(const floatx4 (&acc)[kFT], float eps, f
 #pragma unroll
   for (int ft = 0; ft < kFT; ++ft)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) q += (acc[ft][r] - m) * (acc[ft][r] - m);
+    for (int r = 0; r < 4; ++r) q += (acc[ft][tt][r] - m) * (acc[ft][tt][r] - m);
   q += __shfl_xor(q, 16, 64);
   q += __shfl_xor(q, 32, 64);
   mean = m;
   rstd = rsqrtf(q * (1.f / kD) + eps);
 }
 
-__device__ __forceinline__ void add_bias(floatx4 (&acc)[kFT], const float* b, int g4) {
+template <int TT>
+__device__ __forceinline__ void add_bias(floatx4 (&acc)[kFT][TT], const float* b, int g4) {
 #pragma unroll
   for (int ft = 0; ft < kFT; ++ft) {
     const float4 v = *reinterpret_cast<const float4*>(b + 16 * ft + g4);
-    acc[ft][0] += v.x; acc[ft][1] += v.y; acc[ft][2] += v.z; acc[ft][3] += v.w;
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      acc[ft][tt][0] += v.x; acc[ft][tt][1] += v.y; acc[ft][tt][2] += v.z; acc[ft][tt][3] += v.w;
+    }
     asm volatile("" ::: "memory");   // parameter reads one tile at a time (register pressure)
   }
 }
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int TT, int PROBE>
+__global__ __launch_bounds__(512 / TT) __attribute__((amdgpu_waves_per_eu(2 / TT, 2 / TT)))
 void rowprog_kernel(RowProgArgs a) {
+  constexpr int kWaves = 8 / TT, kThreads = 64 * kWaves;
   extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
   // parameters first: their addresses stay within ds_read's 16-bit immediate offset of one base register
   float* prm = reinterpret_cast<float*>(sm);
@@ -149,6 +166,7 @@ void rowprog_kernel(RowProgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g4 = (lane >> 4) * 4;
+  constexpr bool do_mfma = !(PROBE & 1), do_lds = !(PROBE & 4);
 
   // parameters -> LDS (before the first DMA, so the compiler's waits for these loads do not drain the ring)
   auto cp = [&](int off, const float* p, int n) {
@@ -161,12 +179,10 @@ void rowprog_kernel(RowProgArgs a) {
     if (i >= a.n_ffn) break;
     const RowFfnArgs& f = a.ffn[i];
     const int o = kPrmFfn0 + i * kPrmFfn;
-    cp(o, f.ln_g, kD);
-    cp(o + kD, f.ln_b, kD);
-    cp(o + 2 * kD, f.post_g, kD);
-    cp(o + 3 * kD, f.post_b, kD);
-    cp(o + 4 * kD, f.b2, kD);
-    cp(o + 5 * kD, f.b1, f.hidden);
+    cp(o, f.post_g, kD);
+    cp(o + kD, f.post_b, kD);
+    cp(o + 2 * kD, f.b2, kD);
+    cp(o + 3 * kD, f.b1, f.hidden);
   }
   cp(kPrmY, a.y_g, kD);
   cp(kPrmY + kD, a.y_b, kD);
@@ -174,7 +190,7 @@ void rowprog_kernel(RowProgArgs a) {
 
   const int ntiles = (a.M + kRows - 1) / kRows;
   const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  Ring R;
+  Ring<TT> R;
   R.w0 = static_cast<const uint16_t*>(a.w0);
   R.wf0 = static_cast<const uint16_t*>(a.ffn[0].w);
   R.wf1 = static_cast<const uint16_t*>(a.ffn[1].w);
@@ -185,44 +201,66 @@ void rowprog_kernel(RowProgArgs a) {
   R.total = my_tiles * R.P;
   R.w = w;
   R.lane = lane;
+  R.dma = !(PROBE & 2);
   for (int g = 0; g < kNSlot - 1; ++g) R.issue(g);
   int g = 0;
+  // probe 4: fragments from registers instead of LDS
+  const bf16x8 wconst = __builtin_bit_cast(bf16x8, make_uint4(0x3c003c00u, 0u, 0u, 0u));
+  auto rd = [&](const uint16_t* slot, int f) {
+    if constexpr (do_lds) return frag(slot, f, lane);
+    else return wconst;
+  };
 
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
-    const int64_t row = (int64_t)tile * kRows + w * 16 + l15;   // this lane's token
-    const bool live = row < a.M;
+    int64_t row[TT];
+    bool live[TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      row[tt] = (int64_t)tile * kRows + w * 16 * TT + 16 * tt + l15;   // this lane's token of column tile tt
+      live[tt] = row[tt] < a.M;
+    }
 
-    floatx4 acc[kFT];
-    {
-      const float* xr = a.X + row * kD + g4;
+    floatx4 acc[kFT][TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const float* xr = a.X + row[tt] * kD + g4;
 #pragma unroll
       for (int ft = 0; ft < kFT; ++ft) {
-        const float4 v = live ? *reinterpret_cast<const float4*>(xr + 16 * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
-        acc[ft] = floatx4{v.x, v.y, v.z, v.w};
+        const float4 v = live[tt] ? *reinterpret_cast<const float4*>(xr + 16 * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
       }
     }
 
     // ---- pre-GEMM: acc += A · W0ᵀ + b0 (A rows in natural k order, 16 B per lane and k-step)
     if (a.w0) {
-      bf16x8 af[kKK];
-      const uint16_t* ar = static_cast<const uint16_t*>(a.A) + row * kD + 2 * g4;
+      bf16x8 af[TT][kKK];
 #pragma unroll
-      for (int kk = 0; kk < kKK; ++kk)
-        af[kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(ar + 32 * kk) : make_uint4(0u, 0u, 0u, 0u));
+      for (int tt = 0; tt < TT; ++tt) {
+        const uint16_t* ar = static_cast<const uint16_t*>(a.A) + row[tt] * kD + 2 * g4;
+#pragma unroll
+        for (int kk = 0; kk < kKK; ++kk)
+          af[tt][kk] = __builtin_bit_cast(
+              bf16x8, live[tt] ? *reinterpret_cast<const uint4*>(ar + 32 * kk) : make_uint4(0u, 0u, 0u, 0u));
+      }
 #pragma unroll
       for (int kk = 0; kk < kKK; ++kk) {
-        const uint16_t* slot = R.next(g);
-        bf16x8 wc = frag(slot, 0, lane);
+        const uint16_t* slot = R.wait(g);
+        bf16x8 wq[kPD];
+#pragma unroll
+        for (int q = 0; q < kPD; ++q) wq[q] = rd(slot, q);
 #pragma unroll
         for (int ft = 0; ft < kFT; ++ft) {
-          const bf16x8 wn = ft + 1 < kFT ? frag(slot, ft + 1, lane) : wc;
-          acc[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc, af[kk], acc[ft], 0, 0, 0);
-          asm volatile("" ::: "memory");   // one fragment read ahead, not the whole piece
-          wc = wn;
+          const bf16x8 wc = wq[ft % kPD];
+          if (ft + kPD < kFT) wq[ft % kPD] = rd(slot, ft + kPD);
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) acc[ft][tt] = mfma<do_mfma>(wc, af[tt][kk], acc[ft][tt]);
+          if (ft == kRefillAt) R.refill(g);
+          asm volatile("" ::: "memory");   // kPD fragment reads ahead, not the whole piece
         }
+        ++g;
       }
-      add_bias(acc, prm + kPrmB0, g4);
+      add_bias<TT>(acc, prm + kPrmB0, g4);
     }
 
     // ---- FFN modules (torchaudio _FeedForwardModule, residual x * 0.5 folded into W2 / b2)
@@ -230,99 +268,121 @@ void rowprog_kernel(RowProgArgs a) {
     for (int i = 0; i < 2; ++i) {
       if (i >= a.n_ffn) break;
       const float* pf = prm + kPrmFfn0 + i * kPrmFfn;
-      float mean, rstd;
-      ln_stats(acc, a.eps, mean, rstd);
-      bf16x8 af[kKK];
+      bf16x8 af[TT][kKK];
 #pragma unroll
-      for (int kk = 0; kk < kKK; ++kk) {
-        const float4 ga = *reinterpret_cast<const float4*>(pf + 32 * kk + g4);
-        const float4 gb = *reinterpret_cast<const float4*>(pf + 32 * kk + 16 + g4);
-        const float4 ba = *reinterpret_cast<const float4*>(pf + kD + 32 * kk + g4);
-        const float4 bb = *reinterpret_cast<const float4*>(pf + kD + 32 * kk + 16 + g4);
-        const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
-        const float bv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
-        uint32_t pk[4];
+      for (int tt = 0; tt < TT; ++tt) {
+        // the LayerNorm affine is folded into W1 / b1 (rowprog_pack_ffn): only (x - mean) * rstd here
+        float mean, rstd;
+        ln_stats<TT>(acc, tt, a.eps, mean, rstd);
+        const float nm = -mean * rstd;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j0 = 2 * u, j1 = 2 * u + 1;
-          pk[u] = pack_bf16x2((acc[2 * kk + (j0 >> 2)][j0 & 3] - mean) * rstd * gg[j0] + bv[j0],
-                              (acc[2 * kk + (j1 >> 2)][j1 & 3] - mean) * rstd * gg[j1] + bv[j1]);
+        for (int kk = 0; kk < kKK; ++kk) {
+          uint32_t pk[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j0 = 2 * u, j1 = 2 * u + 1;
+            pk[u] = pack_bf16x2(fmaf(acc[2 * kk + (j0 >> 2)][tt][j0 & 3], rstd, nm),
+                                fmaf(acc[2 * kk + (j1 >> 2)][tt][j1 & 3], rstd, nm));
+          }
+          af[tt][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         }
-        af[kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-        asm volatile("" ::: "memory");
       }
       const int nch = a.ffn[i].hidden / 32;
-      const float* b1 = pf + 5 * kD;
+      const float* b1 = pf + 3 * kD;
 #pragma unroll 1
       for (int c = 0; c < nch; ++c) {
         // up projection: hidden features 32c + 16f + 4g + r
-        const uint16_t* up = R.next(g);
-        floatx4 u0 = {0.f, 0.f, 0.f, 0.f}, u1 = {0.f, 0.f, 0.f, 0.f};
-        bf16x8 w0c = frag(up, 0, lane), w1c = frag(up, kKK, lane);
+        const uint16_t* up = R.wait(g);
+        floatx4 u[2][TT];
 #pragma unroll
-        for (int kk = 0; kk < kKK; ++kk) {
-          const bf16x8 w0n = kk + 1 < kKK ? frag(up, kk + 1, lane) : w0c;
-          const bf16x8 w1n = kk + 1 < kKK ? frag(up, kKK + kk + 1, lane) : w1c;
-          u0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0c, af[kk], u0, 0, 0, 0);
-          u1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1c, af[kk], u1, 0, 0, 0);
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) u[f][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // fragment order: step j = (k-step j / 2, up tile j % 2) at piece fragment (j % 2) * 12 + j / 2
+        bf16x8 wq[kPD];
+#pragma unroll
+        for (int q = 0; q < kPD; ++q) wq[q] = rd(up, (q & 1) * kKK + (q >> 1));
+#pragma unroll
+        for (int j = 0; j < 2 * kKK; ++j) {
+          const bf16x8 wc = wq[j % kPD];
+          if (j + kPD < 2 * kKK) wq[j % kPD] = rd(up, ((j + kPD) & 1) * kKK + ((j + kPD) >> 1));
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) u[j & 1][tt] = mfma<do_mfma>(wc, af[tt][j >> 1], u[j & 1][tt]);
+          if (j == kRefillAt) R.refill(g);
           asm volatile("" ::: "memory");
-          w0c = w0n;
-          w1c = w1n;
         }
+        ++g;
         const float4 c0 = *reinterpret_cast<const float4*>(b1 + 32 * c + g4);
         const float4 c1 = *reinterpret_cast<const float4*>(b1 + 32 * c + 16 + g4);
-        const bf16x8 hf = __builtin_bit_cast(
-            bf16x8, make_uint4(pack_bf16x2(silu(u0[0] + c0.x), silu(u0[1] + c0.y)),
-                               pack_bf16x2(silu(u0[2] + c0.z), silu(u0[3] + c0.w)),
-                               pack_bf16x2(silu(u1[0] + c1.x), silu(u1[1] + c1.y)),
-                               pack_bf16x2(silu(u1[2] + c1.z), silu(u1[3] + c1.w))));
+        bf16x8 hf[TT];
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+          hf[tt] = __builtin_bit_cast(
+              bf16x8, make_uint4(pack_bf16x2(silu(u[0][tt][0] + c0.x), silu(u[0][tt][1] + c0.y)),
+                                 pack_bf16x2(silu(u[0][tt][2] + c0.z), silu(u[0][tt][3] + c0.w)),
+                                 pack_bf16x2(silu(u[1][tt][0] + c1.x), silu(u[1][tt][1] + c1.y)),
+                                 pack_bf16x2(silu(u[1][tt][2] + c1.z), silu(u[1][tt][3] + c1.w))));
         // down projection: k-step c of W2 for all 24 output tiles
-        const uint16_t* dn = R.next(g);
-        bf16x8 wc = frag(dn, 0, lane);
+        const uint16_t* dn = R.wait(g);
+#pragma unroll
+        for (int q = 0; q < kPD; ++q) wq[q] = rd(dn, q);
 #pragma unroll
         for (int ft = 0; ft < kFT; ++ft) {
-          const bf16x8 wn = ft + 1 < kFT ? frag(dn, ft + 1, lane) : wc;
-          acc[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc, hf, acc[ft], 0, 0, 0);
+          const bf16x8 wc = wq[ft % kPD];
+          if (ft + kPD < kFT) wq[ft % kPD] = rd(dn, ft + kPD);
+#pragma unroll
+          for (int tt = 0; tt < TT; ++tt) acc[ft][tt] = mfma<do_mfma>(wc, hf[tt], acc[ft][tt]);
+          if (ft == kRefillAt) R.refill(g);
           asm volatile("" ::: "memory");
-          wc = wn;
         }
+        ++g;
       }
-      add_bias(acc, pf + 4 * kD, g4);
+      add_bias<TT>(acc, pf + 2 * kD, g4);
       if (a.ffn[i].post_g) {
-        ln_stats(acc, a.eps, mean, rstd);
 #pragma unroll
-        for (int ft = 0; ft < kFT; ++ft) {
-          const float4 gq = *reinterpret_cast<const float4*>(pf + 2 * kD + 16 * ft + g4);
-          const float4 bq = *reinterpret_cast<const float4*>(pf + 3 * kD + 16 * ft + g4);
-          acc[ft][0] = (acc[ft][0] - mean) * rstd * gq.x + bq.x;
-          acc[ft][1] = (acc[ft][1] - mean) * rstd * gq.y + bq.y;
-          acc[ft][2] = (acc[ft][2] - mean) * rstd * gq.z + bq.z;
-          acc[ft][3] = (acc[ft][3] - mean) * rstd * gq.w + bq.w;
-          asm volatile("" ::: "memory");
+        for (int tt = 0; tt < TT; ++tt) {
+          float mean, rstd;
+          ln_stats<TT>(acc, tt, a.eps, mean, rstd);
+#pragma unroll
+          for (int ft = 0; ft < kFT; ++ft) {
+            const float4 gq = *reinterpret_cast<const float4*>(pf + 16 * ft + g4);
+            const float4 bq = *reinterpret_cast<const float4*>(pf + kD + 16 * ft + g4);
+            acc[ft][tt][0] = (acc[ft][tt][0] - mean) * rstd * gq.x + bq.x;
+            acc[ft][tt][1] = (acc[ft][tt][1] - mean) * rstd * gq.y + bq.y;
+            acc[ft][tt][2] = (acc[ft][tt][2] - mean) * rstd * gq.z + bq.z;
+            acc[ft][tt][3] = (acc[ft][tt][3] - mean) * rstd * gq.w + bq.w;
+            asm volatile("" ::: "memory");
+          }
         }
       }
     }
 
     // ---- epilogue: Xo = acc; y = LN_y(acc)
-    if (live) {
-      float* xo = a.Xo + row * kD + g4;
 #pragma unroll
-      for (int ft = 0; ft < kFT; ++ft)
-        *reinterpret_cast<float4*>(xo + 16 * ft) = make_float4(acc[ft][0], acc[ft][1], acc[ft][2], acc[ft][3]);
-    }
-    if (a.y) {
-      float mean, rstd;
-      ln_stats(acc, a.eps, mean, rstd);
-      if (live) {
-        uint16_t* yo = static_cast<uint16_t*>(a.y) + row * kD + g4;
+    for (int tt = 0; tt < TT; ++tt) {
+      if (live[tt]) {
+        float* xo = a.Xo + row[tt] * kD + g4;
 #pragma unroll
-        for (int ft = 0; ft < kFT; ++ft) {
-          const float4 gq = *reinterpret_cast<const float4*>(prm + kPrmY + 16 * ft + g4);
-          const float4 bq = *reinterpret_cast<const float4*>(prm + kPrmY + kD + 16 * ft + g4);
-          *reinterpret_cast<uint2*>(yo + 16 * ft) =
-              make_uint2(pack_bf16x2((acc[ft][0] - mean) * rstd * gq.x + bq.x, (acc[ft][1] - mean) * rstd * gq.y + bq.y),
-                         pack_bf16x2((acc[ft][2] - mean) * rstd * gq.z + bq.z, (acc[ft][3] - mean) * rstd * gq.w + bq.w));
-          asm volatile("" ::: "memory");
+        for (int ft = 0; ft < kFT; ++ft)
+          *reinterpret_cast<float4*>(xo + 16 * ft) =
+              make_float4(acc[ft][tt][0], acc[ft][tt][1], acc[ft][tt][2], acc[ft][tt][3]);
+      }
+      if (a.y) {
+        float mean, rstd;
+        ln_stats<TT>(acc, tt, a.eps, mean, rstd);
+        if (live[tt]) {
+          uint16_t* yo = static_cast<uint16_t*>(a.y) + row[tt] * kD + g4;
+#pragma unroll
+          for (int ft = 0; ft < kFT; ++ft) {
+            const float4 gq = *reinterpret_cast<const float4*>(prm + kPrmY + 16 * ft + g4);
+            const float4 bq = *reinterpret_cast<const float4*>(prm + kPrmY + kD + 16 * ft + g4);
+            *reinterpret_cast<uint2*>(yo + 16 * ft) =
+                make_uint2(pack_bf16x2((acc[ft][tt][0] - mean) * rstd * gq.x + bq.x,
+                                       (acc[ft][tt][1] - mean) * rstd * gq.y + bq.y),
+                           pack_bf16x2((acc[ft][tt][2] - mean) * rstd * gq.z + bq.z,
+                                       (acc[ft][tt][3] - mean) * rstd * gq.w + bq.w));
+            asm volatile("" ::: "memory");
+          }
         }
       }
     }
@@ -367,9 +427,23 @@ std::vector<uint16_t> rowprog_pack_pre(const std::vector<float>& W, int N, int K
   return out;
 }
 
-std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::vector<float>& W2, int hidden) {
-  SD_CHECK(hidden % 32 == 0 && (int64_t)W1.size() == (int64_t)hidden * kD && (int64_t)W2.size() == (int64_t)kD * hidden,
+std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1in, const std::vector<float>& W2, int hidden,
+                                       const std::vector<float>& ln_g, const std::vector<float>& ln_b,
+                                       const std::vector<float>& b1, std::vector<float>& b1_folded) {
+  SD_CHECK(hidden % 32 == 0 && (int64_t)W1in.size() == (int64_t)hidden * kD && (int64_t)W2.size() == (int64_t)kD * hidden &&
+               (int)ln_g.size() == kD && (int)ln_b.size() == kD && (int)b1.size() == hidden,
            kErrInvalid, "rowprog_pack_ffn: shape");
+  // Linear(LN(x)) = (W1 diag(g)) x_hat + (W1 b + b1): the LayerNorm affine folded into the up projection.
+  std::vector<float> W1(W1in.size());
+  b1_folded.assign(hidden, 0.f);
+  for (int n = 0; n < hidden; ++n) {
+    double acc = b1[n];
+    for (int k = 0; k < kD; ++k) {
+      W1[(size_t)n * kD + k] = W1in[(size_t)n * kD + k] * ln_g[k];
+      acc += (double)W1in[(size_t)n * kD + k] * ln_b[k];
+    }
+    b1_folded[n] = (float)acc;
+  }
   std::vector<uint16_t> out;
   out.reserve(W1.size() + W2.size());
   for (int c = 0; c < hidden / 32; ++c) {
@@ -383,7 +457,7 @@ std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(a.n_ffn >= 0 && a.n_ffn <= 2, kErrInvalid, "rowprog: n_ffn");
   for (int i = 0; i < a.n_ffn; ++i)
-    SD_CHECK(rowprog_supported(kD, a.ffn[i].hidden, true) && a.ffn[i].w && a.ffn[i].ln_g && a.ffn[i].ln_b &&
+    SD_CHECK(rowprog_supported(kD, a.ffn[i].hidden, true) && a.ffn[i].w &&
                  a.ffn[i].b1 && a.ffn[i].b2 && (a.ffn[i].post_g != nullptr) == (a.ffn[i].post_b != nullptr),
              kErrInvalid, "rowprog: ffn arguments");
   SD_CHECK(!a.w0 || (a.A && a.b0), kErrInvalid, "rowprog: pre-GEMM arguments");
@@ -391,12 +465,18 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(a.X && a.Xo && (a.w0 || a.n_ffn > 0 || a.y), kErrInvalid, "rowprog: empty program");
   if (a.M <= 0) return;
   static int grid_max = 0;
+  static const int tt = getenv("SDIAR_RP_TT") ? atoi(getenv("SDIAR_RP_TT")) : 1;   // token tiles per wave
+  static const int probe = getenv("SDIAR_RP_PROBE") ? atoi(getenv("SDIAR_RP_PROBE")) : 0;
+  SD_CHECK(tt == 1 || tt == 2, kErrInvalid, "SDIAR_RP_TT must be 1 or 2");
   if (!grid_max) {
     int dev = 0, cus = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rowprog_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
+    const void* ks[] = {reinterpret_cast<const void*>(rowprog_kernel<1, 0>), reinterpret_cast<const void*>(rowprog_kernel<2, 0>),
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 2>),
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 4>), reinterpret_cast<const void*>(rowprog_kernel<1, 3>)};
+    for (const void* k : ks)
+      SD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     grid_max = cus > 0 ? cus : 256;
   }
   const int ntiles = (a.M + kRows - 1) / kRows;
@@ -410,7 +490,13 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   }
   const double bytes = rows * kD * (8.0 + (a.w0 ? 2.0 : 0.0) + (a.y ? 2.0 : 0.0)) + wbytes;
   ProfScope prof(name, flops, bytes, st);
-  hipLaunchKernelGGL(rowprog_kernel, dim3(grid), dim3(kThreads), kSmemBytes, st, a);
+  const dim3 g3(grid);
+  if (tt == 2) hipLaunchKernelGGL((rowprog_kernel<2, 0>), g3, dim3(256), kSmemBytes, st, a);
+  else if (probe == 1) hipLaunchKernelGGL((rowprog_kernel<1, 1>), g3, dim3(512), kSmemBytes, st, a);
+  else if (probe == 2) hipLaunchKernelGGL((rowprog_kernel<1, 2>), g3, dim3(512), kSmemBytes, st, a);
+  else if (probe == 3) hipLaunchKernelGGL((rowprog_kernel<1, 3>), g3, dim3(512), kSmemBytes, st, a);
+  else if (probe == 4) hipLaunchKernelGGL((rowprog_kernel<1, 4>), g3, dim3(512), kSmemBytes, st, a);
+  else hipLaunchKernelGGL((rowprog_kernel<1, 0>), g3, dim3(512), kSmemBytes, st, a);
   SD_LAUNCH_CHECK();
 }
 
