@@ -39,13 +39,23 @@ def _headers_digest():
     return h.hexdigest()
 
 
+def _file_flags(path: str) -> list:
+    """Extra compiler flags a source asks for on a line `// sdiar-build: <flags>` (e.g. LLVM options)."""
+    out = []
+    for line in open(path, encoding="utf-8"):
+        if line.startswith("// sdiar-build:"):
+            out += line.split(":", 1)[1].split()
+    return out
+
+
 def _compile(src: str, hdr: str, force: bool) -> str:
     path = os.path.join(CSRC, src)
-    key = hashlib.sha256(open(path, "rb").read() + hdr.encode() + " ".join(CFLAGS).encode())
+    flags = CFLAGS + _file_flags(path)
+    key = hashlib.sha256(open(path, "rb").read() + hdr.encode() + " ".join(flags).encode())
     obj = os.path.join(OBJDIR, f"{src}.{key.hexdigest()[:16]}.o")
     if os.path.exists(obj) and not force:
         return obj
-    cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", path, "-o", obj]
+    cmd = [HIPCC, *flags, "-x", "hip", "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

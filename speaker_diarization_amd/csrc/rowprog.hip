@@ -25,6 +25,8 @@
 // ds_read_b128 is conflict-free) through a 5-slot LDS ring (global_load_lds, 4 pieces in flight, counted
 // vmcnt waits, one barrier per piece).  The workgroups are persistent over tiles; the ring runs across tile
 // boundaries, so the next tile's first weights are in flight during the current tile's epilogue.
+// MFMA accumulators in the VGPR form: with the default AGPR form the 2-tile variant spills to scratch
+// sdiar-build: -mllvm -amdgpu-mfma-vgpr-form=1
 #include <cstring>
 #include <vector>
 #include "common.h"
