@@ -53,7 +53,11 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// PROBE: timing probes as a compile-time constant (a runtime probe word put a branch around every MFMA
+// pair and split the projection loop into 2-MFMA blocks); -1 = read the bits from a.probe.
+template <int PROBE>
 __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
+  const int probe = PROBE >= 0 ? PROBE : a.probe;
   extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
   uint16_t* Ws = sm;                                          // [kNSlot][kKC][16][64]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -88,7 +92,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     }
   };
   const int my_dma = (w < kDmaPerPiece - kWaves) ? 2 : 1;      // instructions this wave issues per piece
-  if (!(a.probe & 4)) {
+  if (!(probe & 4)) {
     issue_piece(0);
     issue_piece(1);
   }
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
       }
     };
     float mean = 0.f, rstd = 0.f;
-    if (live && !(a.probe & 8)) {
+    if (live && !(probe & 8)) {
       float sum = 0.f;
       for (int kk = 0; kk < kKT32; ++kk) {
         float v[8];
@@ -193,12 +197,12 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   for (int i = 0; i < kPieces; ++i) {
     // Piece i landed: the only younger DMA is piece i+1's (this wave's my_dma instructions), unless
     // stores were issued after it (prologue X stores, attention outputs) -> full drain.
-    if (drain || i + 1 >= kPieces || (a.probe & 4)) wait_vm<0>();
+    if (drain || i + 1 >= kPieces || (probe & 4)) wait_vm<0>();
     else if (my_dma == 2) wait_vm<2>();
     else wait_vm<1>();
     drain = false;
     __syncthreads();   // every wave's part of piece i is in LDS; slot (i+2) % 3 (piece i-1) is free
-    if (i + 2 < kPieces && !(a.probe & 4)) issue_piece(i + 2);
+    if (i + 2 < kPieces && !(probe & 4)) issue_piece(i + 2);
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
     const uint16_t* slot = Ws + (i % kNSlot) * kSlot;
     floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     for (int kk = 0; kk < kKT32; ++kk) {
       bf16x8 wnext = wcur;
       if (kk + 1 < kKT32) wnext = wfrag(kk + 1);
-      if (!(a.probe & 2)) {
+      if (!(probe & 2)) {
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
       }
@@ -233,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
                      pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2) continue;
     __syncthreads();   // head h's Q, K, V images complete (both sequences)
-    if ((a.probe & 1) || !seq_ok) continue;
+    if ((probe & 1) || !seq_ok) continue;
 
     // ---- attention of head h for this wave's two 16-query tiles
 #pragma unroll 1
@@ -324,7 +328,9 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st) {
   if (a.S <= 0) return;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<0>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<-1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     attr = true;
   }
@@ -335,7 +341,8 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st) {
   static const int probe = getenv("SDIAR_MHA_PROBE") ? atoi(getenv("SDIAR_MHA_PROBE")) : 0;
   MhaBlockArgs b = a;
   b.probe = probe;
-  hipLaunchKernelGGL(mha_block_kernel, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
+  if (probe) hipLaunchKernelGGL(mha_block_kernel<-1>, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
+  else hipLaunchKernelGGL(mha_block_kernel<0>, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
   SD_LAUNCH_CHECK();
 }
 
