@@ -150,14 +150,16 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
   const bool bf = bf16_;   // bf16 mode: CAM++ activations stored as bf16
   const int F = 80;
   // ---------------- FCM head (cam_pplus_wespeaker.py:271-308), NHWC (B, F, T, 32)
-  fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA_, bf, st);
   // layer1.0: A(80) -> B(40); shortcut A -> C(40); conv2 B -> A(40) + C
   // layer1.1: A -> B; conv2 B -> C + A
   // layer2.0: C(40) -> A(20); shortcut C -> B(20); conv2 A -> C(20) + B
   // layer2.1: C -> A; conv2 A -> B + C
+  // bf16: layer1.0's conv1 computes the stem (head.conv1 + bn1 + relu) from the fbank in LDS, and the two
+  // strided blocks' shortcuts ride on their conv1's centre tap (fcm_conv.hip FcmFuse).
   float* cur = fcmA_;
   int H = F;
   float* bufs[3] = {fcmA_, fcmB_, fcmC_};
+  bool stem_done = false;
   for (size_t i = 0; i < fcm_blocks_.size(); ++i) {
     const ResBlock& rb = fcm_blocks_[i];
     float* others[2];
@@ -167,12 +169,27 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
     float* t2 = others[1];
     ConvGemmArgs p = conv2d(Tens{cur, bf}, B, H, Tf, rb.c1, rb.stride, 1, 1, 1, Tens{t1, bf});
     p.act = kActRelu;
-    conv_gemm(p, bf, st);
+    FcmFuse fu;
+    if (rb.has_sc) {
+      fu.sc_w = rb.sc.w.w; fu.sc_alpha = rb.sc.alpha; fu.sc_beta = rb.sc.beta; fu.sc_out = t2;
+    }
+    if (i == 0) {
+      fu.fbank = ref; fu.fb_F = F;
+      fu.stem_w = fcm_conv1_.pre_s; fu.stem_alpha = fcm_conv1_.alpha; fu.stem_beta = fcm_conv1_.beta;
+    }
+    const bool fused = bf && !no_fused_ && rb.has_sc && rb.sc.w.N == 32 && rb.sc.w.K == 32 && fcm_fused_supported(p, fu);
+    if (i == 0 && !fused) {
+      fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA_, bf, st);
+      stem_done = true;
+    }
+    SD_CHECK(i != 0 || fused || stem_done, kErrInvalid, "FCM stem not computed");
+    if (fused) conv_fcm3x3_fused(p, fu, st);
+    else conv_gemm(p, bf, st);
     const int Ho = p.Ho;
     const float* res = cur;
     float* outb;
     if (rb.has_sc) {
-      conv_gemm(conv2d(Tens{cur, bf}, B, H, Tf, rb.sc, rb.stride, 1, 0, 0, Tens{t2, bf}), bf, st);
+      if (!fused) conv_gemm(conv2d(Tens{cur, bf}, B, H, Tf, rb.sc, rb.stride, 1, 0, 0, Tens{t2, bf}), bf, st);
       res = t2;
       outb = cur;   // input no longer needed
     } else {

@@ -186,11 +186,20 @@ constexpr uint32_t kFcmOOB = 0x80000000u;
 // one 16-B bf16 store per lane writes a whole 64-B frame row with its 3 neighbours.
 __host__ __device__ inline int band_channel(int i, int nt) { return 8 * (i >> 2) + 4 * nt + (i & 3); }
 
-template <int R, int SH>
-__global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, int n_bands, int n_blk) {
+// Fused variants (FcmFuse, campp.cpp FCM head):
+//   SC    the block's shortcut (1x1 conv, same freq stride, folded BN) as two more MFMAs on the centre tap's
+//         fragment, stored to f.sc_out: the shortcut never re-reads the input map;
+//   STEM  the staged input rows are head.conv1 (1 -> 32, 3x3, pad 1) + BN + ReLU computed in LDS from the
+//         fbank rows they need (cam_pplus_wespeaker.py:277-301), so the 80-bin 32-channel stem map (1.84 GB
+//         for a 10-min C2 meeting) is never written.  Same fmaf order as fcm_conv1_kernel (bit-identical).
+template <int R, int SH, bool STEM = false, bool SC = false>
+__global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, FcmFuse f, int n_bands,
+                                                                       int n_blk) {
   // A band: (image b, R output rows from ho0, time tile tt of n_blk 16-frame blocks).
   constexpr int NR = (R - 1) * SH + 3;
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [NR][TW+2][kPS]
+  // staged 16-B vectors per thread: NR rows x (at most 19 x 16 + 2 = 306 frames) x 4 (band_fits checks it)
+  constexpr int kVP = (NR * 306 * 4 + kBandThreads - 1) / kBandThreads;
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [NR][TW+2][kPS] (+ STEM: fbank tile)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l15 = lane & 15, q = lane >> 4;
   const int W = p.W, Wp = n_blk * 16 + 2;
@@ -199,13 +208,30 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
   const int n_vec = NR * Wp * 4;
 
   bf16x8 wf[9][2];
-  {
-    const uint16_t* Wt = reinterpret_cast<const uint16_t*>(p.Wt);
+  // STEM: the conv weights are re-read per band (L1/L2 hits) behind a laundered pointer so that they and the
+  // stem's 72 weights are not live at the same time (register pressure)
+  auto load_wf = [&](const uint16_t* Wt) {
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         wf[t][nt] = *reinterpret_cast<const bf16x8*>(Wt + band_channel(l15, nt) * 288 + t * 32 + q * 8);
+  };
+  if constexpr (!STEM) load_wf(reinterpret_cast<const uint16_t*>(p.Wt));
+  bf16x8 wsc[2];
+  float sal[2][4], sbe[2][4];
+  if constexpr (SC) {
+    const uint16_t* Ws = reinterpret_cast<const uint16_t*>(f.sc_w);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      wsc[nt] = *reinterpret_cast<const bf16x8*>(Ws + band_channel(l15, nt) * 32 + q * 8);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = band_channel(4 * q + r, nt);
+        sal[nt][r] = f.sc_alpha[c];
+        sbe[nt][r] = f.sc_beta[c];
+      }
+    }
   }
   // Per lane: accumulator (nt, r) is channel 8q + 4nt + r, i.e. channels 8q .. 8q+7.
   float al[2][4], be[2][4];
@@ -231,7 +257,7 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
     const int64_t img = (int64_t)b * p.H * W;
     int px = px_base, rr = rr_base;
 #pragma unroll
-    for (int k = 0; k < kBandVecPer; ++k) {
+    for (int k = 0; k < kVP; ++k) {
       const int i = tid + k * kBandThreads;
       const int ch = (i & 3) * 8;
       const int hi = hb + rr, wi = w0 + px;
@@ -247,18 +273,97 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
     }
   };
 
-  uint4 hv[kBandVecPer];
-  int band = blockIdx.x;
-  if (band < n_bands) load_band(band, hv);
-  for (; band < n_bands; band += gridDim.x) {
+  // STEM: fbank tile [NR + 2 bins][Wp + 2 frames] (fp32) after the staged rows; this thread's 8 stem
+  // channels (channel group tid & 3, fixed because 512 % 4 == 0) keep their 72 weights in registers.
+  float* fbs = reinterpret_cast<float*>(xs + NR * Wp * kPS);
+  const int fb_n = (NR + 2) * (Wp + 2);
+  constexpr int kFbPer = 5;   // fbank tile floats per thread (<= 2560)
+  float s_al[8], s_be[8];
+  if constexpr (STEM) {
+    const int c0 = (tid & 3) * 8;
 #pragma unroll
-    for (int k = 0; k < kBandVecPer; ++k) {
-      const int i = tid + k * kBandThreads;
-      if (i < n_vec) *reinterpret_cast<uint4*>(xs + (i >> 2) * kPS + (i & 3) * 8) = hv[k];
+    for (int u = 0; u < 8; ++u) {
+      s_al[u] = f.stem_alpha[c0 + u];
+      s_be[u] = f.stem_beta[c0 + u];
     }
-    __syncthreads();
-    const int next = band + gridDim.x;
-    if (next < n_bands) load_band(next, hv);   // in flight while this band computes
+  }
+  // fbank value (bin hb - 1 + j, frame w0 - 1 + x) of a band, j < NR + 2, x < Wp + 2; zero outside the map
+  auto load_fb = [&](int band, float* v) {
+    const int tt = band % n_tt, bh = band / n_tt;
+    const int b = bh / n_rb, hb = (bh % n_rb) * R * SH - 1;
+    const int w0 = tt * n_blk * 16 - 1;
+#pragma unroll
+    for (int k = 0; k < kFbPer; ++k) {
+      const int i = tid + k * kBandThreads;   // frame-major: a frame's NR + 2 bins are contiguous in the fbank
+      const int x = i / (NR + 2), j = i - x * (NR + 2);
+      const int bin = hb - 1 + j, fr = w0 - 1 + x;
+      v[k] = (i < fb_n && (unsigned)bin < (unsigned)f.fb_F && (unsigned)fr < (unsigned)W)
+                 ? f.fbank[((int64_t)b * W + fr) * f.fb_F + bin]
+                 : 0.f;
+    }
+  };
+
+  uint4 hv[STEM ? 1 : kVP];
+  float fv[STEM ? kFbPer : 1];
+  int band = blockIdx.x;
+  if (band < n_bands) {
+    if constexpr (STEM) load_fb(band, fv);
+    else load_band(band, hv);
+  }
+  for (; band < n_bands; band += gridDim.x) {
+    if constexpr (STEM) {
+#pragma unroll
+      for (int k = 0; k < kFbPer; ++k) {
+        const int i = tid + k * kBandThreads;
+        const int x = i / (NR + 2), j = i - x * (NR + 2);
+        if (i < fb_n) fbs[j * (Wp + 2) + x] = fv[k];   // LDS tile [bin][frame]
+      }
+      __syncthreads();
+      const int next = band + gridDim.x;
+      if (next < n_bands) load_fb(next, fv);
+      // stem: staged pixel (rr, px) = conv1 row hb + rr, frame w0 + px; zero outside (next conv's padding)
+      const int tt = band % n_tt, bh = band / n_tt;
+      const int hb = (bh % n_rb) * R * SH - 1, w0 = tt * n_blk * 16 - 1;
+      const float* swb = f.stem_w;
+      asm volatile("" : "+s"(swb));
+      const float* swp = swb + (tid & 3) * 72;
+      float sw[8][9];
+#pragma unroll
+      for (int k = 0; k < 72; ++k) sw[k / 9][k % 9] = swp[k];
+      for (int i = tid; i < n_vec; i += kBandThreads) {
+        const int pix = i >> 2, rr = pix / Wp, px = pix - rr * Wp;
+        const bool ok = (unsigned)(hb + rr) < (unsigned)p.H && (unsigned)(w0 + px) < (unsigned)W;
+        float x9[9];
+#pragma unroll
+        for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) x9[dh * 3 + dw] = fbs[(rr + dh) * (Wp + 2) + px + dw];
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float acc = 0.f;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) acc = fmaf(sw[u][k], x9[k], acc);
+          v[u] = ok ? fmaxf(acc * s_al[u] + s_be[u], 0.f) : 0.f;
+        }
+        *reinterpret_cast<uint4*>(xs + pix * kPS + (i & 3) * 8) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+      }
+      const uint16_t* wtp = reinterpret_cast<const uint16_t*>(p.Wt);
+      asm volatile("" : "+s"(wtp));
+      load_wf(wtp);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < kVP; ++k) {
+        const int i = tid + k * kBandThreads;
+        if (i < n_vec) *reinterpret_cast<uint4*>(xs + (i >> 2) * kPS + (i & 3) * 8) = hv[k];
+      }
+      __syncthreads();
+      const int next = band + gridDim.x;
+      if (next < n_bands) load_band(next, hv);   // in flight while this band computes
+    }
 
     const int tt = band % n_tt, bh = band / n_tt;
     const int b = bh / n_rb, ho0 = (bh % n_rb) * R;
@@ -269,6 +374,7 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       const int ho = ho0 + r;
       if (ho >= p.Ho) break;
       floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+      floatx4 sacc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int dh = 0; dh < 3; ++dh)
 #pragma unroll
@@ -278,11 +384,25 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
             acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[dh * 3 + dw][nt], af, acc[nt], 0, 0, 0);
+          if constexpr (SC) {
+            if (dh == 1 && dw == 1)   // input row SH * ho, frame wo: the 1x1 shortcut's operand
+#pragma unroll
+              for (int nt = 0; nt < 2; ++nt)
+                sacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wsc[nt], af, sacc[nt], 0, 0, 0);
+          }
         }
       const int wo = wo0 + blk * 16 + l15;
       if (wo >= p.Wo) continue;
       const int64_t pix = ((int64_t)b * p.Ho + ho) * p.Wo + wo;
       const int c0 = q * 8;
+      if constexpr (SC) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = fmaf(sacc[u >> 2][u & 3], sal[u >> 2][u & 3], sbe[u >> 2][u & 3]);
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(f.sc_out) + pix * 32 + c0) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+      }
       float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (p.res) {
         const int64_t ro = pix * p.res_ld + c0;
@@ -332,35 +452,42 @@ inline int band_blocks(int W) {
   return (nb + n_tt - 1) / n_tt;
 }
 
-template <int R, int SH>
-size_t band_lds(int n_blk) { return (size_t)((R - 1) * SH + 3) * (n_blk * 16 + 2) * kPS * 2; }
+template <int R, int SH, bool STEM = false>
+size_t band_lds(int n_blk) {
+  constexpr int nr = (R - 1) * SH + 3;
+  const size_t fb = STEM ? (size_t)(nr + 2) * (n_blk * 16 + 4) * 4 : 0;
+  return (size_t)nr * (n_blk * 16 + 2) * kPS * 2 + fb;
+}
 
-template <int R, int SH>
+template <int R, int SH, bool STEM = false>
 bool band_fits(const ConvGemmArgs& p) {
   const int nr = (R - 1) * SH + 3;
   const int nb = band_blocks(p.W);
   // (n_blk*16 + 2) > 128 keeps the loader's frame index wrapping at most once per step.
-  return nb >= 8 && band_lds<R, SH>(nb) <= 156 * 1024 && nr * (nb * 16 + 2) * 4 <= kBandVecPer * kBandThreads &&
+  return nb >= 8 && nb <= kBandMaxBlk && band_lds<R, SH, STEM>(nb) <= 156 * 1024 &&
+         nr * (nb * 16 + 2) * 4 <= kBandVecPer * kBandThreads &&
+         (!STEM || (nr + 2) * (nb * 16 + 4) <= 5 * kBandThreads) &&
          (int64_t)p.B * p.H * p.W * p.lda * 2 < (int64_t)kFcmOOB &&
          (!p.res || (p.res_ld % 8 == 0)) && (p.o_sn != 1 || p.o_sw % 8 == 0);
 }
 
 int g_fcm_cu = 0;
 
-template <int R, int SH>
-void launch_band(const ConvGemmArgs& p, hipStream_t st) {
+template <int R, int SH, bool STEM = false, bool SC = false>
+void launch_band(const ConvGemmArgs& p, hipStream_t st, const FcmFuse& f = FcmFuse{}) {
   const int nb = band_blocks(p.W);
   const int64_t bands = (int64_t)p.B * cdiv(p.Ho, R) * cdiv(p.W, nb * 16);
   SD_CHECK(bands < (1ll << 31), kErrInvalid, "fcm conv: too many bands");
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, SH>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, SH, STEM, SC>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
-  const size_t smem = band_lds<R, SH>(nb);
-  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, SH>), dim3(grid), dim3(kBandThreads), smem, st, p, (int)bands, nb);
+  const size_t smem = band_lds<R, SH, STEM>(nb);
+  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, SH, STEM, SC>), dim3(grid), dim3(kBandThreads), smem, st, p, f,
+                     (int)bands, nb);
 }
 
 }  // namespace
@@ -394,6 +521,40 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
   SD_CHECK(tiles < (1ll << 31), kErrInvalid, "fcm conv: too many tiles");
   const int grid = (int)std::min<int64_t>(tiles, (int64_t)g_fcm_cu * 4);
   hipLaunchKernelGGL(fcm_conv3x3_kernel, dim3(grid), dim3(256), 0, st, p, (int)tiles);
+  SD_LAUNCH_CHECK();
+}
+
+bool fcm_fused_supported(const ConvGemmArgs& p, const FcmFuse& f) {
+  static const bool off = getenv("SDIAR_NO_FCM_FUSE") != nullptr;   // A/B switch
+  if (off || p.sh != 2 || !p.out_bf16 || p.res || p.o_sn != 1 || p.o_sw != 32) return false;
+  if (f.sc_w && !(f.sc_alpha && f.sc_beta && f.sc_out)) return false;
+  if (f.fbank) {
+    if (!(f.stem_w && f.stem_alpha && f.stem_beta && f.fb_F == p.H)) return false;
+    ConvGemmArgs q = p;
+    q.a_bf16 = true;
+    q.lda = 32;
+    return fcm_conv_supported(q) && band_fits<2, 2, true>(q);
+  }
+  return fcm_conv_supported(p) && band_fits<2, 2>(p);
+}
+
+void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st) {
+  SD_CHECK(fcm_fused_supported(p, f), kErrInvalid, "fcm fused conv: unsupported arguments");
+  if (!g_fcm_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&g_fcm_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const double px = (double)p.B * p.Ho * p.Wo;
+  const double in_px = f.fbank ? 0.0 : (double)p.B * p.H * p.W;
+  double flops = 2.0 * px * 32 * 288 + (f.sc_w ? 2.0 * px * 32 * 32 : 0.0);
+  if (f.fbank) flops += 2.0 * (double)p.B * p.H * p.W * 32 * 9;
+  const double bytes = in_px * 64 + (f.fbank ? 4.0 * p.B * p.W * f.fb_F : 0.0) + px * 64 * (f.sc_w ? 2 : 1);
+  ProfScope prof(f.fbank ? "fcm_stem" : "fcm_conv3x3_band", flops, bytes, st);
+  if (f.fbank && f.sc_w) launch_band<2, 2, true, true>(p, st, f);
+  else if (f.fbank) launch_band<2, 2, true, false>(p, st, f);
+  else if (f.sc_w) launch_band<2, 2, false, true>(p, st, f);
+  else launch_band<2, 2>(p, st);
   SD_LAUNCH_CHECK();
 }
 

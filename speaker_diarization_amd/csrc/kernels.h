@@ -66,6 +66,19 @@ bool gemm_stream_supported(const ConvGemmArgs& p);            // bf16 A linear, 
 void conv_gemm_stream(const ConvGemmArgs& p, hipStream_t st);
 bool fcm_conv_supported(const ConvGemmArgs& p);               // bf16 3x3 32->32, pad 1, freq stride 1|2
 void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st);
+// CAM++ BasicResBlock entry conv (3x3, freq stride 2, bf16 NHWC out) with the block's 1x1 shortcut as a
+// second output and/or the FCM stem (head.conv1 + BN + ReLU of the fbank) computed in LDS instead of
+// read from HBM (p.A unused then; p.H = fb_F = 80, p.W = frames).
+struct FcmFuse {
+  const void* sc_w = nullptr;                 // packed bf16 Wt[32][32]
+  const float *sc_alpha = nullptr, *sc_beta = nullptr;
+  void* sc_out = nullptr;                     // bf16 NHWC (B, Ho, Wo, 32)
+  const float* fbank = nullptr;               // (B, W, fb_F) fp32
+  int fb_F = 0;
+  const float *stem_w = nullptr, *stem_alpha = nullptr, *stem_beta = nullptr;   // 32x9 raw, folded BN
+};
+bool fcm_fused_supported(const ConvGemmArgs& p, const FcmFuse& f);
+void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st);
 void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st);     // LDS-DMA fed variant
 bool gemm_areg_supported(const ConvGemmArgs& p);             // bf16 A linear, K in {192,256,384}, N % 64 == 0, N >= 768
 void conv_gemm_areg(const ConvGemmArgs& p, hipStream_t st);
