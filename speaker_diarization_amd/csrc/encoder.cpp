@@ -284,11 +284,13 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     conv_gemm(p1, true, st);
     glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
                !glu_epi, true, st);
-    if (L.group_norm) groupnorm_silu(ao.p, S, T, E, w.partial, L.gn_g, L.gn_b, 1e-5f, true, st);
     {
       RowProgArgs r;
       r.X = X; r.Xo = X; r.M = rows;
       r.A = ao.p; r.w0 = L.rp_pw2; r.b0 = L.pw2_b;
+      if (L.group_norm) {   // GroupNorm + SiLU applied by the program as it loads A (no separate pass)
+        r.gn_partial = w.partial; r.gn_nblk = (E + 63) / 64; r.gn_T = T; r.gn_g = L.gn_g; r.gn_b = L.gn_b;
+      }
       r.n_ffn = 1; r.ffn[0] = ffn(L, true);
       if (li + 1 < Ls.size()) {
         const ConformerL& Ln = Ls[li + 1];

@@ -215,6 +215,11 @@ struct RowProgArgs {
   const float *y_g = nullptr, *y_b = nullptr;
   void* y = nullptr;
   float eps = 1e-5f;
+  // optional A transform of the pre-GEMM: A = silu(GroupNorm(A)) (one group per sequence of gn_T rows),
+  // statistics from glu_dwconv's partial sums (gn_nblk pairs per sequence)
+  const float* gn_partial = nullptr;
+  int gn_nblk = 0, gn_T = 0;
+  const float *gn_g = nullptr, *gn_b = nullptr;
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

@@ -50,7 +50,8 @@ constexpr int kRefillAt = 3;          // the DMA refill is issued after this man
 // LDS parameter block (floats): b0 | per FFN: post_g post_b b2 (D each) b1 (kMaxHidden) | y_g y_b
 constexpr int kPrmFfn = 3 * kD + kMaxHidden;
 constexpr int kPrmB0 = 0, kPrmFfn0 = kD, kPrmY = kD + 2 * kPrmFfn;
-constexpr int kPrmFloats = (kPrmY + 2 * kD + 255) / 256 * 256;   // padded to whole KiB
+constexpr int kPrmGn = kPrmY + 2 * kD;   // GroupNorm gamma | beta of the pre-GEMM's A transform
+constexpr int kPrmFloats = (kPrmGn + 2 * kD + 255) / 256 * 256;   // padded to whole KiB
 constexpr size_t kSmemBytes = sizeof(uint16_t) * (size_t)kNSlot * kPiece + sizeof(float) * kPrmFloats;
 static_assert((kPrmFloats * 4) % 1024 == 0, "ring slots stay 1-KiB aligned");
 static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
@@ -188,6 +189,8 @@ void rowprog_kernel(RowProgArgs a) {
   }
   cp(kPrmY, a.y_g, kD);
   cp(kPrmY + kD, a.y_b, kD);
+  cp(kPrmGn, a.gn_g, kD);
+  cp(kPrmGn + kD, a.gn_b, kD);
   __syncthreads();
 
   const int ntiles = (a.M + kRows - 1) / kRows;
@@ -244,6 +247,48 @@ void rowprog_kernel(RowProgArgs a) {
         for (int kk = 0; kk < kKK; ++kk)
           af[tt][kk] = __builtin_bit_cast(
               bf16x8, live[tt] ? *reinterpret_cast<const uint4*>(ar + 32 * kk) : make_uint4(0u, 0u, 0u, 0u));
+      }
+      if (a.gn_partial) {
+        // A = silu(GroupNorm(A)): the conformer conv module's GroupNorm(1 group) + SiLU, applied on load
+        // with groupnorm_silu_kernel's arithmetic (ops.hip: statistics in double from the dwconv partials)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+          const int64_t sq = live[tt] ? row[tt] / a.gn_T : 0;
+          double sum = 0.0, ssq = 0.0;
+          for (int i = 0; i < a.gn_nblk; ++i) {
+            sum += a.gn_partial[(sq * a.gn_nblk + i) * 2];
+            ssq += a.gn_partial[(sq * a.gn_nblk + i) * 2 + 1];
+          }
+          const double n = (double)a.gn_T * kD;
+          const double mean = sum / n;
+          double var = ssq / n - mean * mean;
+          if (var < 0) var = 0;
+          const float fm = (float)mean;
+          const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
+#pragma unroll
+          for (int kk = 0; kk < kKK; ++kk) {
+            const int c = 32 * kk + 2 * g4;
+            const float4 g0 = *reinterpret_cast<const float4*>(prm + kPrmGn + c);
+            const float4 g1 = *reinterpret_cast<const float4*>(prm + kPrmGn + c + 4);
+            const float4 b0 = *reinterpret_cast<const float4*>(prm + kPrmGn + kD + c);
+            const float4 b1 = *reinterpret_cast<const float4*>(prm + kPrmGn + kD + c + 4);
+            const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+            const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            const uint4 u = __builtin_bit_cast(uint4, af[tt][kk]);
+            const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+            uint32_t pk[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              float x0 = (__uint_as_float(w4[h] << 16) - fm) * rstd * gg[2 * h] + bb[2 * h];
+              float x1 = (__uint_as_float(w4[h] & 0xffff0000u) - fm) * rstd * gg[2 * h + 1] + bb[2 * h + 1];
+              x0 = x0 / (1.f + __expf(-x0));
+              x1 = x1 / (1.f + __expf(-x1));
+              pk[h] = pack_bf16x2(x0, x1);
+            }
+            af[tt][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+            asm volatile("" ::: "memory");
+          }
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < kKK; ++kk) {
