@@ -130,6 +130,11 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
       (f == 1 ? L.rp_f1_b1 : L.rp_f2_b1) = arena.upload(b1);
     }
     L.rp_out = put(rowprog_pack_pre(w32(p + ".self_attn.out_proj.weight", 1.f), E, E));
+    if (L.group_norm) {   // conv_block.hip takes the GroupNorm variant (its stats feed the pw2 program)
+      int N, Cin, kh, kw;
+      const std::vector<float> w1 = ps.pack(p + ".conv_module.sequential.0.weight", N, Cin, kh, kw);
+      if (N == 2 * E && Cin == E && kh * kw == 1) L.cb_w1 = put(conv_block_pack_w1(w1, N, Cin));
+    }
     L.rp_pw2 = put(rowprog_pack_pre(w32(p + ".conv_module.sequential.5.weight", 1.f), E, E));
   }
   return L;
@@ -277,13 +282,20 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
       rowprog(r, "rowprog_out", st);
     }
-    ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
-    p1.glu = 1;
-    const bool glu_epi = gemm_stream_supported(p1);
-    if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
-    conv_gemm(p1, true, st);
-    glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
-               !glu_epi, true, st);
+    if (L.cb_w1 && conv_block_supported(E, T, kernel, true)) {
+      ConvBlockArgs c;   // pw1 + GLU + depthwise conv per sequence, h never leaves LDS
+      c.y = y.p; c.w1 = L.cb_w1; c.b1 = L.pw1_b; c.dw_w = L.dw_w; c.dw_b = L.dw_b; c.k = kernel;
+      c.out = ao.p; c.partial = w.partial; c.S = S; c.T = T;
+      conv_block(c, st);
+    } else {
+      ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
+      p1.glu = 1;
+      const bool glu_epi = gemm_stream_supported(p1);
+      if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
+      conv_gemm(p1, true, st);
+      glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
+                 !glu_epi, true, st);
+    }
     {
       RowProgArgs r;
       r.X = X; r.Xo = X; r.M = rows;

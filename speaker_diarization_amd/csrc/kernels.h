@@ -193,6 +193,25 @@ struct MhaBlockArgs {
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
 
+// ---------------------------------------------------------------- conv_block.hip
+// Conformer conv-module body per sequence (bf16, D 384, T <= 152): h = GLU(y · W1ᵀ + b1) kept in LDS,
+// out = depthwise_conv_k(h) + dw_b (bf16, (S*T, 384)), partial = GroupNorm sums per (sequence, 64 channels)
+// as glu_dwconv writes them.  w1 from conv_block_pack_w1 (original row order), b1 interleaved as the
+// GLU-epilogue GEMMs take it ([16 values | 16 gates] per 32-row group).
+struct ConvBlockArgs {
+  const void* y = nullptr;
+  const void* w1 = nullptr;
+  const float* b1 = nullptr;
+  const float *dw_w = nullptr, *dw_b = nullptr;
+  int k = 0;
+  void* out = nullptr;
+  float* partial = nullptr;
+  int S = 0, T = 0;
+};
+bool conv_block_supported(int D, int T, int k, bool bf16);
+std::vector<uint16_t> conv_block_pack_w1(const std::vector<float>& W, int N, int K);
+void conv_block(const ConvBlockArgs& a, hipStream_t st);
+
 // ---------------------------------------------------------------- rowprog.hip
 // Conformer per-token row program (bf16 weights, D 384): acc = X; [acc += A·W0ᵀ + b0];
 // per FFN i: acc += W2·silu(W1·LN_i(acc) + b1) + b2 (the ½ folded into W2 / b2), [acc = LN_post_i(acc)];
