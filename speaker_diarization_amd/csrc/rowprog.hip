@@ -158,7 +158,10 @@ __device__ __forceinline__ void add_bias(floatx4 (&acc)[kFT][TT], const float* b
   }
 }
 
-template <int TT, int PROBE>
+// PROG >= 0 fixes the program's structure at compile time (bit 0: pre-GEMM, bits 1-2: FFN count) so each
+// program is its own symbol in rocprof traces / PMC passes and carries no structure branches; -1 reads it
+// from the arguments (probe and 2-tile variants).
+template <int TT, int PROBE, int PROG = -1>
 __global__ __launch_bounds__(512 / TT) __attribute__((amdgpu_waves_per_eu(2 / TT, 2 / TT)))
 void rowprog_kernel(RowProgArgs a) {
   constexpr int kWaves = 8 / TT, kThreads = 64 * kWaves;
@@ -170,6 +173,8 @@ void rowprog_kernel(RowProgArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g4 = (lane >> 4) * 4;
   constexpr bool do_mfma = !(PROBE & 1), do_lds = !(PROBE & 4);
+  const bool has_pre = PROG >= 0 ? (PROG & 1) != 0 : a.w0 != nullptr;
+  const int nffn = PROG >= 0 ? (PROG >> 1) : a.n_ffn;
 
   // parameters -> LDS (before the first DMA, so the compiler's waits for these loads do not drain the ring)
   auto cp = [&](int off, const float* p, int n) {
@@ -179,7 +184,7 @@ void rowprog_kernel(RowProgArgs a) {
   cp(kPrmB0, a.b0, kD);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    if (i >= a.n_ffn) break;
+    if (i >= nffn) break;
     const RowFfnArgs& f = a.ffn[i];
     const int o = kPrmFfn0 + i * kPrmFfn;
     cp(o, f.post_g, kD);
@@ -200,9 +205,9 @@ void rowprog_kernel(RowProgArgs a) {
   R.wf0 = static_cast<const uint16_t*>(a.ffn[0].w);
   R.wf1 = static_cast<const uint16_t*>(a.ffn[1].w);
   R.ring = ring;
-  R.n_pre = a.w0 ? kKK : 0;
-  R.n_f0 = a.n_ffn > 0 ? 2 * (a.ffn[0].hidden / 32) : 0;
-  R.P = R.n_pre + R.n_f0 + (a.n_ffn > 1 ? 2 * (a.ffn[1].hidden / 32) : 0);
+  R.n_pre = has_pre ? kKK : 0;
+  R.n_f0 = nffn > 0 ? 2 * (a.ffn[0].hidden / 32) : 0;
+  R.P = R.n_pre + R.n_f0 + (nffn > 1 ? 2 * (a.ffn[1].hidden / 32) : 0);
   R.total = my_tiles * R.P;
   R.w = w;
   R.lane = lane;
@@ -238,7 +243,7 @@ void rowprog_kernel(RowProgArgs a) {
     }
 
     // ---- pre-GEMM: acc += A · W0ᵀ + b0 (A rows in natural k order, 16 B per lane and k-step)
-    if (a.w0) {
+    if (has_pre) {
       bf16x8 af[TT][kKK];
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
@@ -313,7 +318,7 @@ void rowprog_kernel(RowProgArgs a) {
     // ---- FFN modules (torchaudio _FeedForwardModule, residual x * 0.5 folded into W2 / b2)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      if (i >= a.n_ffn) break;
+      if (i >= nffn) break;
       const float* pf = prm + kPrmFfn0 + i * kPrmFfn;
       bf16x8 af[TT][kKK];
 #pragma unroll
@@ -519,7 +524,9 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
     int dev = 0, cus = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const void* ks[] = {reinterpret_cast<const void*>(rowprog_kernel<1, 0>), reinterpret_cast<const void*>(rowprog_kernel<2, 0>),
+    const void* ks[] = {reinterpret_cast<const void*>(rowprog_kernel<1, 0, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 2>),
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 0, 3>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 5>),
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 0>), reinterpret_cast<const void*>(rowprog_kernel<2, 0>),
                         reinterpret_cast<const void*>(rowprog_kernel<1, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 2>),
                         reinterpret_cast<const void*>(rowprog_kernel<1, 4>), reinterpret_cast<const void*>(rowprog_kernel<1, 3>)};
     for (const void* k : ks)
@@ -543,7 +550,14 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   else if (probe == 2) hipLaunchKernelGGL((rowprog_kernel<1, 2>), g3, dim3(512), kSmemBytes, st, a);
   else if (probe == 3) hipLaunchKernelGGL((rowprog_kernel<1, 3>), g3, dim3(512), kSmemBytes, st, a);
   else if (probe == 4) hipLaunchKernelGGL((rowprog_kernel<1, 4>), g3, dim3(512), kSmemBytes, st, a);
-  else hipLaunchKernelGGL((rowprog_kernel<1, 0>), g3, dim3(512), kSmemBytes, st, a);
+  else {
+    const int prog = (a.w0 ? 1 : 0) | (a.n_ffn << 1);
+    if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, a);
+    else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, a);
+    else if (prog == 3) hipLaunchKernelGGL((rowprog_kernel<1, 0, 3>), g3, dim3(512), kSmemBytes, st, a);
+    else if (prog == 5) hipLaunchKernelGGL((rowprog_kernel<1, 0, 5>), g3, dim3(512), kSmemBytes, st, a);
+    else hipLaunchKernelGGL((rowprog_kernel<1, 0>), g3, dim3(512), kSmemBytes, st, a);
+  }
   SD_LAUNCH_CHECK();
 }
 

@@ -19,12 +19,18 @@ from collections import defaultdict
 
 # sd_prof category -> HIP kernel symbols dispatched under it.
 CATEGORIES = {
+    # rowprog.hip programs are separate instantiations: <TT, PROBE, PROG> (PROG: bit 0 pre-GEMM, bits 1-2 FFNs)
+    "rowprog_out": r"rowprog_kernel<1, 0, 1>",
+    "rowprog_ffn": r"rowprog_kernel<1, 0, 2>",
+    "rowprog_pw2_ffn": r"rowprog_kernel<1, 0, [35]>",
+    "mha_block": r"mha_block_kernel",
+    "fcm_stem": r"fcm_conv3x3_band_kernel<2, 2, true",
     "gemm_ring": r"gemm_ring_kernel",
     "gemm_stream": r"gemm_stream_kernel",
     "gemm_areg": r"gemm_areg_kernel",
     "gemm_dma": r"gemm_dma_kernel",
     "gemm_bf16_reg": r"gemm_bf16_kernel",
-    "fcm_conv3x3_band": r"fcm_conv3x3\w*kernel",
+    "fcm_conv3x3_band": r"fcm_conv3x3_kernel|fcm_conv3x3_band_kernel<(4, 1|2, 2), false",
     "attention_bf16": r"attn_\w*kernel|attention\w*kernel",
     "lstm_recurrence": r"lstm\w*kernel",
     "dwconv": r"glu_dwconv_kernel",
