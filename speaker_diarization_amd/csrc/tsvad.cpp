@@ -13,6 +13,7 @@
 // All activations are fp32 channel-last; every contraction is conv_gemm (bf16 or
 // exact-f32 MFMA), eval BatchNorms are folded into GEMM prologues/epilogues.
 #include "tsvad.h"
+#include "prof.h"
 
 #include <cmath>
 
@@ -102,11 +103,76 @@ void TsvadModel::alloc_workspace() {
   lstm_work_ = ws(lstm_work_floats((int)Bm, cfg_.lstm_hidden, 2));
 }
 
+TsvadModel::~TsvadModel() {
+  for (GraphEntry& e : graphs_) {
+    if (e.exec) (void)hipGraphExecDestroy(e.exec);
+    if (e.graph) (void)hipGraphDestroy(e.graph);
+  }
+  if (cap_st_) (void)hipStreamDestroy(cap_st_);
+}
+
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
                          hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
+  static const bool no_graph = getenv("SDIAR_NO_GRAPH") && atoi(getenv("SDIAR_NO_GRAPH")) == 1;
+  if (no_graph || prof_enabled()) {
+    forward_body(ref, ts, B, Tf, Tl, logits, st);
+    return;
+  }
+  // Host-side part of the persistent LSTM's deferred error report (lstm_recurrence does the same on a
+  // direct run; a replayed graph only repeats the stream-ordered copy of the err word).
+  {
+    const int prev = __atomic_load_n(lstm_err_.get(), __ATOMIC_ACQUIRE);
+    __atomic_store_n(lstm_err_.get(), 0, __ATOMIC_RELEASE);
+    SD_CHECK(prev == 0, kErrHip, "lstm: a previous persistent LSTM launch lost workgroup co-residency "
+                                 "(its outputs were poisoned with NaN)");
+  }
+  GraphEntry* e = nullptr;
+  for (GraphEntry& g : graphs_)
+    if (g.ref == ref && g.ts == ts && g.logits == logits && g.B == B && g.Tf == Tf && g.Tl == Tl) e = &g;
+  if (!e) {
+    if (graphs_.size() >= 8) {   // bounded: the oldest key is dropped
+      GraphEntry& o = graphs_.front();
+      if (o.exec) (void)hipGraphExecDestroy(o.exec);
+      if (o.graph) (void)hipGraphDestroy(o.graph);
+      graphs_.erase(graphs_.begin());
+    }
+    graphs_.push_back(GraphEntry{ref, ts, logits, B, Tf, Tl});
+    e = &graphs_.back();
+  }
+  if (e->failed || ++e->seen < 2) {   // first sight: direct launches (and the launchers' one-time setup)
+    forward_body(ref, ts, B, Tf, Tl, logits, st);
+    return;
+  }
+  if (!e->exec) {
+    if (!cap_st_) SD_HIP(hipStreamCreateWithFlags(&cap_st_, hipStreamNonBlocking));
+    SD_HIP(hipStreamBeginCapture(cap_st_, hipStreamCaptureModeThreadLocal));
+    bool ok = true;
+    try {
+      forward_body(ref, ts, B, Tf, Tl, logits, cap_st_);
+    } catch (...) {
+      ok = false;
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(cap_st_, &g);
+    if (ok && ec == hipSuccess && g && hipGraphInstantiate(&e->exec, g, nullptr, nullptr, 0) == hipSuccess) {
+      e->graph = g;
+    } else {   // not capturable (or failed): this key runs direct launches from now on
+      if (g) (void)hipGraphDestroy(g);
+      e->exec = nullptr;
+      e->failed = true;
+      (void)hipGetLastError();
+      forward_body(ref, ts, B, Tf, Tl, logits, st);
+      return;
+    }
+  }
+  SD_HIP(hipGraphLaunch(e->exec, st));
+}
+
+void TsvadModel::forward_body(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
+                              hipStream_t st) {
   const bool bf = cfg_.bf16;
   const Tens x4 = cam_.forward(ref, B, Tf, st);   // CAM++ up to transit3, (B, T2, 512)
   const int T2 = CamTrunk::out_frames(Tf);

@@ -112,6 +112,33 @@ def test_tsvad_v1_large_batch_uses_wide_gemm_paths(gpu):
     assert err < BF16_ATOL
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_tsvad_graph_replay_matches_direct(gpu, variant):
+    """The second forward with the same (pointers, shapes) captures the whole forward into a hipGraph and
+    later ones replay it (tsvad.cpp): every replay must give the direct-launch logits bit for bit, a new
+    output buffer must not reuse the old graph, and the fp32 golden still holds through the graph."""
+    name = "tsvad_v0_rs4" if variant == 0 else "tsvad_v1_rs6"
+    v, rs, B, T, nl, iseed, wseed = TSVAD_CASES[name]
+    cfg = _cfg(v, rs)
+    m = TSVADModel(cfg, device=gpu, precision="bf16", max_batch=B)
+    m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=wseed)))
+    x, ts = tsvad_inputs(B, T, nl, seed=iseed)
+    xd, tsd = torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu)
+    out = torch.empty(B, 4, nl, device=gpu)
+    outs = []
+    for _ in range(4):   # direct, capture + launch, replay, replay
+        out.fill_(float("nan"))
+        m.forward(xd, tsd, nl, out=out)
+        outs.append(out.cpu().numpy().copy())
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+    other = torch.empty_like(out)
+    m.forward(xd, tsd, nl, out=other)
+    np.testing.assert_array_equal(other.cpu().numpy(), outs[0])
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    assert np.abs(outs[-1] - g["logits"]).max() < BF16_ATOL
+
+
 def test_tsvad_infer_res_dict_matches_reference(gpu):
     """TSVADModel.infer (model.py:923-970) -> (result, res_dict) vs the reference's own infer on
     the same seeded batch (tests/golden/tsvad_infer.npz, make_postprocess_golden.py): partial
