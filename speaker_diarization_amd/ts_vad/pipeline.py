@@ -17,6 +17,23 @@ from .model import TSVADModel
 from .windows import WindowPlan, plan_windows, shard_batches
 
 
+_DEV_CACHE = {}
+
+
+def _plan_i32(plan: WindowPlan, name: str, arr, dev, w0: int = 0, w1: int = None):
+    """Device int32 copy of a plan array, cached per (plan, slice, device): a pageable H2D copy per step
+    would block the host until the GPU drains the stream and leave the GPU idle while Python re-enqueues."""
+    import torch
+    key = (plan.n_labels, plan.rs_len, plan.segment_shift, plan.label_rate, plan.sample_rate, name, w0, w1, str(dev))
+    t = _DEV_CACHE.get(key)
+    if t is None:
+        if len(_DEV_CACHE) > 256:
+            _DEV_CACHE.clear()
+        t = torch.from_numpy(np.ascontiguousarray(arr).astype(np.int32)).to(dev)
+        _DEV_CACHE[key] = t
+    return t
+
+
 class TSVADPipeline:
     def __init__(self, model: TSVADModel, segment_shift: int = 1, batch_size: int = 64):
         self.model = model
@@ -46,8 +63,8 @@ class TSVADPipeline:
         s1 = min(wav.numel(), int(plan.ends[w1 - 1]) * spl)
         feats = kaldi_fbank(wav[s0:s1])
         f0 = int(plan.fbank_start[w0])
-        fstart = torch.from_numpy((plan.fbank_start[w0:w1] - f0).astype(np.int32)).to(dev)
-        fn = torch.from_numpy(plan.fbank_n[w0:w1].astype(np.int32)).to(dev)
+        fstart = _plan_i32(plan, "fstart", plan.fbank_start[w0:w1] - f0, dev, w0, w1)
+        fn = _plan_i32(plan, "fn", plan.fbank_n[w0:w1], dev, w0, w1)
         ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
         for b0, b1, T_out, T_lab in self.device_batches(plan, w0, w1):
             ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
@@ -78,8 +95,8 @@ class TSVADPipeline:
         dev = probs.device
         NS = probs.shape[1]
         out = torch.empty(NS, plan.n_labels, device=dev, dtype=torch.float32)
-        st = torch.from_numpy(plan.starts.astype(np.int32)).to(dev)
-        ln = torch.from_numpy(plan.lens.astype(np.int32)).to(dev)
+        st = _plan_i32(plan, "starts", plan.starts, dev)
+        ln = _plan_i32(plan, "lens", plan.lens, dev)
         _lib.call("sd_overlap_mean", _lib.ptr(probs.contiguous()), plan.n_win, NS, probs.shape[2],
                   _lib.ptr(st), _lib.ptr(ln), plan.dis, plan.chunk, plan.n_labels, _lib.ptr(out),
                   _lib.stream_ptr(dev))
@@ -92,8 +109,8 @@ class TSVADPipeline:
         dev = logits.device
         NS = logits.shape[1]
         out = torch.empty(NS, plan.n_labels, device=dev, dtype=torch.float32)
-        st = torch.from_numpy(plan.starts.astype(np.int32)).to(dev)
-        ln = torch.from_numpy(plan.lens.astype(np.int32)).to(dev)
+        st = _plan_i32(plan, "starts", plan.starts, dev)
+        ln = _plan_i32(plan, "lens", plan.lens, dev)
         _lib.call("sd_overlap_average", _lib.ptr(logits.contiguous()), plan.n_win, NS, logits.shape[2],
                   _lib.ptr(st), _lib.ptr(ln), plan.dis, plan.chunk, plan.n_labels, _lib.ptr(out),
                   _lib.stream_ptr(dev))
