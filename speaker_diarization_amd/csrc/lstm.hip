@@ -210,7 +210,14 @@ constexpr int LS_H = 256;
 constexpr int LS_WS = LS_H + 16;     // bf16 LDS row stride of the W slice (conflict-free fragment reads)
 constexpr int LS_MAXMT = 6;
 
-template <int MT>
+// TAG (MT <= 2): the hand-off without counters.  Every exchanged word is (step tag << 16) | bf16 h, so a
+// consumer knows a value is current from the value itself: the producer's write-through stores go out with no
+// vmcnt drain, barrier or counter add, and each consumer wave re-loads (sc1) its h words until every tag
+// matches — one L2 round trip per step instead of store-ack + barrier + atomic + poll + barrier + load.
+// Double buffering by step parity keeps a fast producer from overwriting words a slow consumer still needs
+// (it cannot publish h_{s+1} before every quarter published h_s, i.e. finished reading h_{s-1}).  The tags
+// start at 1 and the exchange buffer is zeroed before each launch; T < 65535.
+template <int MT, bool TAG>
 __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
@@ -238,11 +245,12 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
           *reinterpret_cast<const uint4*>(wd + (int64_t)(gate * H + 64 * q + j) * H + k8);
     }
   }
-  // h exchange: hx[parity][d][Bp][H] bf16; h_t lives in parity (t + 1) & 1, h_{-1} in 0.
+  // h exchange: hx[parity][d][Bp][H] bf16 (TAG: uint32 words); h_t lives in parity (t + 1) & 1, h_{-1} in 0.
+  constexpr int EB = TAG ? 4 : 2;   // bytes per exchanged value
   const int64_t plane = (int64_t)ndir * Bp * H;
-  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * EB), 0x00020000);
   auto hx_off = [&](int parity, int b, int u) {   // byte offset
-    return (uint32_t)(((int64_t)parity * plane + ((int64_t)d * Bp + b) * H + u) * 2);
+    return (uint32_t)(((int64_t)parity * plane + ((int64_t)d * Bp + b) * H + u) * EB);
   };
   float c[MT][4], hr[MT][4];
   int len[MT];
@@ -261,7 +269,17 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   for (int b = b0; b < min(B, b0 + BB); ++b) max_len = max(max_len, lengths ? lengths[b] : T);
 
   // Publish this workgroup's slice of h (rows b0.., units ub..ub+3 per lane), then count.
-  auto publish = [&](int parity) {
+  auto publish = [&](int parity, unsigned tag) {
+    if constexpr (TAG) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        u32x4_t v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (tag << 16) | (pack_bf16x2(hr[mt][r], 0.f) & 0xffffu);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rh, hx_off(parity, b0 + mt * 16 + l15, ub), 0, 16);   // sc1
+      }
+      return;
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
@@ -289,7 +307,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the poll
   };
 
-  publish(0);   // h_{-1}
+  publish(0, 1u);   // h_{-1}
   for (int step = 0; step < max_len; ++step) {
     // gx of this step for the lane's rows: 4 gates x 4 units (float4), issued before the wait.
     float4 gxv[MT][4];
@@ -303,19 +321,92 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
       for (int gate = 0; gate < 4; ++gate)
         gxv[mt][gate] = live ? *reinterpret_cast<const float4*>(gr + gate * H) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
     const int pin = step & 1;
     floatx4 acc[MT][4];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // TAG: the wave's h words of h_{step-1} (tag step + 1), re-loaded until every tag is current
+    u32x4_t hw[TAG ? MT : 1][TAG ? H / 32 : 1][2];
+    if constexpr (TAG) {
+      const unsigned want = (unsigned)(step + 1) & 0xffffu;
+      unsigned spins = 0;
+      // cheap poll first: lane j < 16 watches one word of producer wave j (unit 16j of row b0); the full
+      // load + per-word check below then usually succeeds at once (polling all words congests L2)
+      for (;;) {
+        asm volatile("" ::: "memory");
+        bool seen = true;
+        if (lane < 16) {
+          const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rh, hx_off(pin, b0, 16 * lane), 0, 16);
+          seen = (x[0] >> 16) == want;
+        }
+        if (__all(seen)) break;
+        if ((++spins & 255) == 0 && (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      for (;;) {
+        asm volatile("" ::: "memory");   // the words change under us: no load may be hoisted out of the spin
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int kc = 0; kc < H / 32; ++kc)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+              hw[mt][kc][hh] = __builtin_amdgcn_raw_buffer_load_b128(
+                  rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g + 4 * hh), 0, 16);
+        bool ok = true;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int kc = 0; kc < H / 32; ++kc)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) ok = ok && (hw[mt][kc][hh][r] >> 16) == want;
+        if (__all(ok)) break;
+        if ((++spins & 255) == 0 && (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    } else {
+      wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
+    }
+    // counter mode: every h fragment of the step requested at once (one L2 round trip, not one per k-step;
+    // s_memtime stamps: 5.1 k of a 10 k-cycle C1 step went to eight serial load -> MFMA waits)
+    bf16x8 hfa[TAG ? 1 : MT][TAG ? 1 : H / 32];
+    if constexpr (!TAG) {
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g), 0, 16));
+    }
+#pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rh, hx_off(pin, b0 + mt * 16 + l15, k0 + 8 * g), 0, 16);
-        hf[mt] = __builtin_bit_cast(bf16x8, x);
+        if constexpr (TAG) {
+          const int kc = k0 / 32;
+          u32x4_t x;   // bf16 units k0 + 8g + 0..7 from the low halves (the shift drops the tag)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+              x[2 * hh + r] = (hw[mt][kc][hh][2 * r] & 0xffffu) | (hw[mt][kc][hh][2 * r + 1] << 16);
+          hf[mt] = __builtin_bit_cast(bf16x8, x);
+        } else {
+          hf[mt] = hfa[mt][k0 / 32];
+        }
       }
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) {
@@ -334,20 +425,24 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
       const float gf[4] = {gxv[mt][1].x, gxv[mt][1].y, gxv[mt][1].z, gxv[mt][1].w};
       const float gg[4] = {gxv[mt][2].x, gxv[mt][2].y, gxv[mt][2].z, gxv[mt][2].w};
       const float go[4] = {gxv[mt][3].x, gxv[mt][3].y, gxv[mt][3].z, gxv[mt][3].w};
+      // bf16-mode gates with the hardware exp / reciprocal (tanh x = 2 sigmoid(2x) - 1): libm expf/tanhf cost
+      // 2.6-6.5 k cycles per step here, on the recurrence's critical path
+      auto sig = [](float x) { return __frcp_rn(1.f + __expf(-x)); };
+      auto tnh = [&](float x) { return fmaf(2.f, sig(2.f * x), -1.f); };
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float ig = 1.f / (1.f + expf(-(acc[mt][0][r] + gi[r])));
-        const float fg = 1.f / (1.f + expf(-(acc[mt][1][r] + gf[r])));
-        const float cg = tanhf(acc[mt][2][r] + gg[r]);
-        const float og = 1.f / (1.f + expf(-(acc[mt][3][r] + go[r])));
+        const float ig = sig(acc[mt][0][r] + gi[r]);
+        const float fg = sig(acc[mt][1][r] + gf[r]);
+        const float cg = tnh(acc[mt][2][r] + gg[r]);
+        const float og = sig(acc[mt][3][r] + go[r]);
         c[mt][r] = fg * c[mt][r] + ig * cg;
-        hr[mt][r] = og * tanhf(c[mt][r]);
+        hr[mt][r] = og * tnh(c[mt][r]);
       }
       if (out)
         *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) =
             make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
     }
-    publish((step + 1) & 1);   // h_step
+    publish((step + 1) & 1, (unsigned)(step + 2) & 0xffffu);   // h_step
   }
   // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
   // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
@@ -370,19 +465,19 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   }
 }
 
-template <int MT>
+template <int MT, bool TAG = false>
 void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                        const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                        uint16_t* hx, int Bp, unsigned* counters, int* err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, TAG>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL(lstm_group_bf16_kernel<MT>, dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
+  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, TAG>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
                      counters, err);
 }
@@ -396,10 +491,17 @@ int lstm_group_blocks_per_cu() {
   static int nb = -1;
   if (nb < 0) {
     const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int v = 0;
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT>, 256, smem));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, false>, 256, smem));
+    if (MT <= 2) {   // the tagged variant must fit as well
+      SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT <= 2 ? MT : 1, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      int vt = 0;
+      SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&vt, lstm_group_bf16_kernel<MT <= 2 ? MT : 1, true>, 256, smem));
+      v = std::min(v, vt);
+    }
     nb = v;
   }
   return nb;
@@ -433,7 +535,8 @@ int lstm_group_mt(int B, int ndir) {
 
 // Layout of the persistent kernel's scratch inside the caller's `work`: the double-buffered bf16
 // h exchange, then (16-B aligned) one counter per group and the err word.
-size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
+// sized for the tagged exchange (4 B per value; the counter protocol uses the first half)
+size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 4 + 15) / 16 * 16; }
 
 }  // namespace
 
@@ -474,10 +577,16 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       uint16_t* hx = reinterpret_cast<uint16_t*>(work);
       unsigned* ctl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + hx_bytes);
       SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
+      // the tagged hand-off is opt-in (SDIAR_LSTM_TAG=1): measured slower than the counter (C1 11.0 vs 8.7 ms)
+      static const bool want_tag = getenv("SDIAR_LSTM_TAG") && atoi(getenv("SDIAR_LSTM_TAG")) == 1;
+      const bool tag = want_tag && mt <= 2 && T < 65000;
+      if (tag) SD_HIP(hipMemsetAsync(hx, 0, hx_bytes, st));   // no stale tag may match
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       int* err = reinterpret_cast<int*>(ctl + groups);
-      switch (mt) {
+      if (tag && mt == 1) launch_lstm_group<1, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
+      else if (tag) launch_lstm_group<2, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
+      else switch (mt) {
         case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         case 3: launch_lstm_group<3>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
