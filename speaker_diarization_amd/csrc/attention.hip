@@ -454,6 +454,185 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
   }
 }
 
+// Long-sequence bf16 flash attention (FS-EEND: causal T = 6000 encoder and the decoder's strided time
+// attention; fs_eend.py:163-171).  bf16 in / out, so K and V tiles of 64 keys are staged in LDS with 16-B
+// copies (no fp32 round trip, no scattered 2-B transposes): K row-major for the Sᵀ = K·Qᵀ A operand, V
+// row-major read back as the Vᵀ A operand of Oᵀ = Vᵀ·Pᵀ with ds_read_b64_tr_b16 (the attn_short scheme).
+// LDS is double-buffered and the next tile is fetched into registers during the current tile's MFMAs (one
+// barrier per tile).  Causal tiles wholly below the diagonal skip the mask; query blocks run heaviest first.
+constexpr int kLKT = 64;   // keys per tile
+template <int HD>
+__global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
+  constexpr int KS = HD + 8;                 // K row stride (bf16): conflict-free fragment reads
+  constexpr int VS = HD;                     // V row stride (bf16), ds_read_b64_tr_b16 rows
+  constexpr int KC = HD / 32;                // 32-wide d chunks of Q / K
+  constexpr int DT = HD / 16;                // 16-wide d tiles of O
+  constexpr int CPR = HD / 8;                // 16-B chunks per row
+  constexpr int CHK = kLKT * CPR / 256;      // 16-B chunks per thread per matrix and tile
+  static_assert(HD % 32 == 0 && CHK >= 1, "head dim");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kLKT * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kLKT * VS];
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, l15 = lane & 15;
+  const int sh = blockIdx.y, s = sh / a.nh, h = sh % a.nh;
+  const int T = a.T, D = a.D;
+  const int qb = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;   // heaviest first
+  const int qblk0 = qb * kQB;
+  const int myq = qblk0 + wid * 16 + l15;
+  const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
+                       (int64_t)(s % a.seq_inner) * a.seq_inner_stride;
+  const int64_t tstr = (int64_t)a.tok_stride * a.ld_qkv;
+  const uint16_t* base = reinterpret_cast<const uint16_t*>(a.qkv) + row0 * a.ld_qkv + h * HD;
+  const int klen = a.key_len ? min(a.key_len[s], T) : T;
+
+  bf16x8 qf[KC];
+  {
+    const uint16_t* qr = base + (int64_t)min(myq, T - 1) * tstr;
+    const bool qv = myq < T;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const uint4 u = *reinterpret_cast<const uint4*>(qr + kc * 32 + g * 8);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      uint32_t pk[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)   // the generic kernel's rounding: bf16(q * scale)
+        pk[j] = qv ? pack_bf16x2(__uint_as_float(w[j] << 16) * a.scale, __uint_as_float(w[j] & 0xffff0000u) * a.scale)
+                   : 0u;
+      qf[kc] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+    }
+  }
+
+  int k_end = klen;
+  if (a.causal) k_end = min(k_end, qblk0 + kQB + a.causal_delay);
+  const int ntile = k_end > 0 ? (k_end + kLKT - 1) / kLKT : 0;
+  // staging map: chunk c = tid + 256 i -> key row c / CPR, 16-B chunk c % CPR
+  uint4 kreg[CHK], vreg[CHK];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CHK; ++i) {
+      const int c = tid + 256 * i, kr = c / CPR, ch = c % CPR;
+      const int key = t * kLKT + kr;
+      const uint16_t* r = base + (int64_t)min(key, T - 1) * tstr + ch * 8;
+      kreg[i] = key < T ? *reinterpret_cast<const uint4*>(r + D) : make_uint4(0u, 0u, 0u, 0u);
+      vreg[i] = key < T ? *reinterpret_cast<const uint4*>(r + 2 * D) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CHK; ++i) {
+      const int c = tid + 256 * i, kr = c / CPR, ch = c % CPR;
+      *reinterpret_cast<uint4*>(&Ks[buf][kr * KS + ch * 8]) = kreg[i];
+      *reinterpret_cast<uint4*>(&Vs[buf][kr * VS + ch * 8]) = vreg[i];
+    }
+  };
+
+  floatx4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int tr_off = ((4 * g + (l15 >> 2)) * VS + 4 * (l15 & 3)) * 2;   // attn_short's Vᵀ lane offset (bytes)
+
+  if (ntile > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntile; ++t) {
+    const int buf = t & 1, k0 = t * kLKT;
+    if (t + 1 < ntile) fetch(t + 1);   // in flight during this tile's MFMAs
+    // Sᵀ: 4 subtiles of 16 keys; lane holds keys k0 + 16 st + 4g + r of query myq
+    floatx4 sc[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[buf][(st * 16 + l15) * KS + kc * 32 + g * 8]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], acc, 0, 0, 0);
+      }
+      sc[st] = acc;
+    }
+    // mask only where a key of the tile can be invisible to some query of the block (a uniform branch:
+    // the per-element `full || visible` select form gave wrong scores on masked tiles; not root-caused)
+    const bool full = k0 + kLKT <= klen && (!a.causal || k0 + kLKT - 1 <= qblk0 + a.causal_delay);
+    if (!full) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + st * 16 + g * 4 + r;
+          const bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
+          sc[st][r] = ok ? sc[st][r] : -INFINITY;
+        }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sc[st][r]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = (m_new == -INFINITY) ? 0.f : __expf(sc[st][r] - m_new);
+        sc[st][r] = pv;
+        psum += pv;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;   // Oᵀ: lane's column is its own query
+    // Oᵀ += Vᵀ·Pᵀ over the tile's two 32-key halves
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8 pb;   // Pᵀ operand: k-index 8g + j <-> key 32 kh + 4g + j (j < 4), 32 kh + 16 + 4g + j - 4
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sc[2 * kh + (j >> 2)][j & 3];
+      const uint32_t vbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)&Vs[buf][0]) +
+                             (uint32_t)(32 * kh * VS * 2) + (uint32_t)tr_off;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + 16 * VS * 2 + dt * 32));
+        const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntile) stage(buf ^ 1);
+    __syncthreads();
+  }
+  if (myq < T) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (row0 + (int64_t)myq * a.tok_stride) * a.ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) =
+          make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+  }
+}
+
+template <int HD>
+bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
+  static const bool off = getenv("SDIAR_NO_ATTN_LONG") != nullptr;   // A/B switch: the generic kernel
+  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || HD % 32 || a.T <= 256 ||
+      (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 4) || (a.tok_stride * a.ld_qkv) % 8)
+    return false;
+  hipLaunchKernelGGL(attn_long_kernel<HD>, dim3(cdiv(a.T, kQB), a.S * a.nh), dim3(256), 0, st, a);
+  return true;
+}
+
 template <int HD>
 bool launch_short(const AttnArgs& a, bool bf16, hipStream_t st) {
   constexpr int HDP = ((HD + 31) / 32) * 32;
@@ -493,6 +672,9 @@ bool launch_short(const AttnArgs& a, bool bf16, hipStream_t st) {
 template <int HD>
 void launch_hd(const AttnArgs& a, bool bf16, hipStream_t st) {
   if (launch_short<HD>(a, bf16, st)) return;
+  if constexpr (HD % 32 == 0) {
+    if (launch_long<HD>(a, bf16, st)) return;
+  }
   dim3 grid(cdiv(a.T, kQB), a.S * a.nh);
   if (bf16 && a.io_bf16)
     hipLaunchKernelGGL((attn_kernel<true, HD, true>), grid, dim3(256), 0, st, a);

@@ -166,6 +166,24 @@ def test_attention_key_len(gpu, precision):
         assert _rel_err(out.cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("S,T,D,nh,causal,delay,kl", [(1, 6000, 256, 4, 1, 0, None), (2, 1000, 256, 4, 1, 3, None),
+                                                       (3, 513, 128, 4, 0, 0, (513, 300, 257)),
+                                                       (2, 700, 512, 4, 1, 0, (650, 700)), (1, 2000, 256, 4, 0, 0, None)])
+def test_attention_long_bf16(gpu, S, T, D, nh, causal, delay, kl):
+    """attn_long_kernel (T > 256, bf16 in/out: FS-EEND's causal T = 6000 encoder, the EDA T = 2000 chunks),
+    incl. causal look-ahead, key lengths and head dims 32 / 64 / 128, vs the fp32 torch reference."""
+    g = torch.Generator().manual_seed(T + S)
+    qkv = torch.randn(S * T, 3 * D, generator=g)
+    klt = None if kl is None else torch.tensor(kl, dtype=torch.int32)
+    ref = _attn_ref(qkv, S, T, D, nh, causal, delay, key_len=klt)
+    out = torch.empty(S * T, D, device=gpu)
+    kld = None if klt is None else klt.to(gpu)
+    _lib.call("sd_op_attention", _d(qkv, gpu), S, T, D, nh, causal, delay, None if kld is None else kld.data_ptr(),
+              out.data_ptr(), 2, _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    assert _rel_err(out.cpu(), ref) < 2e-2
+
+
 def _chunk_mask(T, chunk, left):
     """Key visibility of forward_chunk_by_chunk's KV caches (ts_vad2_streaming/model.py:594-655,
     transformer_chunk_streaming.py:305-373): chunks max(0, c - left) .. c."""
