@@ -455,33 +455,65 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
 }
 
 // Long-sequence bf16 flash attention (FS-EEND: causal T = 6000 encoder and the decoder's strided time
-// attention; fs_eend.py:163-171).  bf16 in / out, so K and V tiles of 64 keys are staged in LDS with 16-B
-// copies (no fp32 round trip, no scattered 2-B transposes): K row-major for the Sᵀ = K·Qᵀ A operand, V
-// row-major read back as the Vᵀ A operand of Oᵀ = Vᵀ·Pᵀ with ds_read_b64_tr_b16 (the attn_short scheme).
-// LDS is double-buffered and the next tile is fetched into registers during the current tile's MFMAs (one
-// barrier per tile).  Causal tiles wholly below the diagonal skip the mask; query blocks run heaviest first.
-constexpr int kLKT = 64;   // keys per tile
+// attention; fs_eend.py:163-171).  bf16 in / out, so K and V tiles are staged in LDS with 16-B copies (no
+// fp32 round trip, no scattered 2-B transposes): K row-major for the Sᵀ = K·Qᵀ A operand, V row-major read
+// back as the Vᵀ A operand of Oᵀ = Vᵀ·Pᵀ with ds_read_b64_tr_b16 (the attn_short scheme).
+//
+// A workgroup is 8 waves over 64 queries: waves w and w + 4 own the same 16 queries and split the keys by
+// 64-key tile parity (each 128-key pair of tiles is staged once; the even tile feeds waves 0-3, the odd one
+// waves 4-7), which doubles the waves in flight over the 1.5 per SIMD a T = 6000, 4-head causal launch
+// gives with one wave per 16 queries.  The two halves' (max, sum, O) are merged through LDS at the end.
+// Per tile: row max by 15 fmax + permlane16/32_swap (VALU, no LDS round trip), p = exp2(s·log2e - m·log2e)
+// as one FMA + v_exp, the row sum kept per lane and reduced once at the end.  Pairs are double-buffered in
+// LDS and fetched two pairs ahead into registers (one barrier per pair).  Tiles wholly visible skip the
+// mask; causal query blocks run heaviest first.
+constexpr int kLKT = 64;   // keys per tile (per wave); a pair of tiles per staging step
+__device__ __forceinline__ float vmax(float x, float y) {   // v_max_f32 without the canonicalising pre-ops
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ float xor16_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor16_add(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_add(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int HD>
-__global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
+__global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   constexpr int KS = HD + 8;                 // K row stride (bf16): conflict-free fragment reads
   constexpr int VS = HD;                     // V row stride (bf16), ds_read_b64_tr_b16 rows
   constexpr int KC = HD / 32;                // 32-wide d chunks of Q / K
   constexpr int DT = HD / 16;                // 16-wide d tiles of O
   constexpr int CPR = HD / 8;                // 16-B chunks per row
-  constexpr int CHK = kLKT * CPR / 256;      // 16-B chunks per thread per matrix and tile
+  constexpr int PK = 2 * kLKT;               // keys per staged pair
+  constexpr int CHK = PK * CPR / 512;        // 16-B chunks per thread per matrix and pair
+  constexpr float kL2E = 1.4426950408889634f;
   static_assert(HD % 32 == 0 && CHK >= 1, "head dim");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kLKT * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kLKT * VS];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][PK * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][PK * VS];
   typedef short v4s __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wid >> 2, qw = wid & 3;   // key-tile parity, query group (wave-uniform: SGPR branches)
   const int g = lane >> 4, l15 = lane & 15;
   const int sh = blockIdx.y, s = sh / a.nh, h = sh % a.nh;
   const int T = a.T, D = a.D;
   const int qb = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;   // heaviest first
   const int qblk0 = qb * kQB;
-  const int myq = qblk0 + wid * 16 + l15;
+  const int myq = qblk0 + qw * 16 + l15;
   const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
                        (int64_t)(s % a.seq_inner) * a.seq_inner_stride;
   const int64_t tstr = (int64_t)a.tok_stride * a.ld_qkv;
@@ -508,41 +540,41 @@ __global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
   int k_end = klen;
   if (a.causal) k_end = min(k_end, qblk0 + kQB + a.causal_delay);
   const int ntile = k_end > 0 ? (k_end + kLKT - 1) / kLKT : 0;
-  // staging map: chunk c = tid + 256 i -> key row c / CPR, 16-B chunk c % CPR
-  uint4 kreg[CHK], vreg[CHK];
-  auto fetch = [&](int t) {
+  const int npair = (ntile + 1) / 2;
+  // staging map: chunk c = tid + 512 i -> pair row c / CPR, 16-B chunk c % CPR.  Two register sets: pair
+  // p + 1 is staged from one at the end of pair p while pair p + 2 is in flight in the other.
+  struct KV { u32x4_t k[CHK], v[CHK]; };   // native vectors: HIP's uint4 wrapper kept the sets in scratch
+  KV ra, rb;
+  auto fetch = [&](int p, KV& r) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < CHK; ++i) {
-      const int c = tid + 256 * i, kr = c / CPR, ch = c % CPR;
-      const int key = t * kLKT + kr;
-      const uint16_t* r = base + (int64_t)min(key, T - 1) * tstr + ch * 8;
-      kreg[i] = key < T ? *reinterpret_cast<const uint4*>(r + D) : make_uint4(0u, 0u, 0u, 0u);
-      vreg[i] = key < T ? *reinterpret_cast<const uint4*>(r + 2 * D) : make_uint4(0u, 0u, 0u, 0u);
+      const int c = tid + 512 * i, kr = c / CPR, ch = c % CPR;
+      const int key = p * PK + kr;
+      const uint16_t* src = base + (int64_t)min(key, T - 1) * tstr + ch * 8;
+      // rows past T re-read row T - 1 (finite data; those keys are masked, p = 0): no branch around the load
+      r.k[i] = *reinterpret_cast<const u32x4_t*>(src + D);
+      r.v[i] = *reinterpret_cast<const u32x4_t*>(src + 2 * D);
     }
   };
-  auto stage = [&](int buf) {
+  auto stage = [&](int buf, const KV& r) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < CHK; ++i) {
-      const int c = tid + 256 * i, kr = c / CPR, ch = c % CPR;
-      *reinterpret_cast<uint4*>(&Ks[buf][kr * KS + ch * 8]) = kreg[i];
-      *reinterpret_cast<uint4*>(&Vs[buf][kr * VS + ch * 8]) = vreg[i];
+      const int c = tid + 512 * i, kr = c / CPR, ch = c % CPR;
+      *reinterpret_cast<u32x4_t*>(&Ks[buf][kr * KS + ch * 8]) = r.k[i];
+      *reinterpret_cast<u32x4_t*>(&Vs[buf][kr * VS + ch * 8]) = r.v[i];
     }
   };
 
   floatx4 o[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;   // l_run: this lane's partial row sum (its 16 keys per tile)
   const int tr_off = ((4 * g + (l15 >> 2)) * VS + 4 * (l15 & 3)) * 2;   // attn_short's Vᵀ lane offset (bytes)
+  const int krow0 = half * kLKT;                                        // this half's tile inside a pair
 
-  if (ntile > 0) {
-    fetch(0);
-    stage(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < ntile; ++t) {
-    const int buf = t & 1, k0 = t * kLKT;
-    if (t + 1 < ntile) fetch(t + 1);   // in flight during this tile's MFMAs
+  auto tile = [&](int t, int buf) __attribute__((always_inline)) {
+    const int k0 = t * kLKT;
+    const uint16_t* kb = &Ks[buf][krow0 * KS];
     // Sᵀ: 4 subtiles of 16 keys; lane holds keys k0 + 16 st + 4g + r of query myq
     floatx4 sc[4];
 #pragma unroll
@@ -550,7 +582,7 @@ __global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[buf][(st * 16 + l15) * KS + kc * 32 + g * 8]);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&kb[(st * 16 + l15) * KS + kc * 32 + g * 8]);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], acc, 0, 0, 0);
       }
       sc[st] = acc;
@@ -568,27 +600,26 @@ __global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
           sc[st][r] = ok ? sc[st][r] : -INFINITY;
         }
     }
-    float tmax = -INFINITY;
+    float tmax = sc[0][0];
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sc[st][r]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+      for (int r = (st == 0 ? 1 : 0); r < 4; ++r) tmax = vmax(tmax, sc[st][r]);
+    tmax = xor32_max(xor16_max(tmax));
+    const float m_new = vmax(m_run, tmax);
+    const bool dead = m_new == -INFINITY;   // no visible key yet for this query
+    const float ml = dead ? 0.f : m_new * kL2E;
+    const float alpha = dead ? 1.f : __builtin_amdgcn_exp2f(fmaf(m_run, kL2E, -ml));
     float psum = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = (m_new == -INFINITY) ? 0.f : __expf(sc[st][r] - m_new);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sc[st][r], kL2E, -ml));   // exp2(-inf) = 0
         sc[st][r] = pv;
         psum += pv;
       }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
-    l_run = l_run * alpha + psum;
+    l_run = fmaf(l_run, alpha, psum);
     m_run = m_new;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -601,7 +632,7 @@ __global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sc[2 * kh + (j >> 2)][j & 3];
       const uint32_t vbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)&Vs[buf][0]) +
-                             (uint32_t)(32 * kh * VS * 2) + (uint32_t)tr_off;
+                             (uint32_t)((krow0 + 32 * kh) * VS * 2) + (uint32_t)tr_off;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
@@ -610,8 +641,59 @@ __global__ __launch_bounds__(256) void attn_long_kernel(AttnArgs a) {
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
       }
     }
-    if (t + 1 < ntile) stage(buf ^ 1);
+  };
+  // buf as a compile-time constant: the two unrolled copies differ, so they are not merged into one body
+  // selecting between the register sets (which put the sets in scratch)
+  auto pair = [&](int p, KV& r, auto bufc) __attribute__((always_inline)) {
+    constexpr int buf = decltype(bufc)::value;
+    const int t = 2 * p + half;
+    tile(t, buf);   // t >= ntile (odd half, last pair): every key masked, no-op; no branch (see below)
+    // unconditional (a pair past the end lands in the idle buffer, clamped rows): a skipped path makes
+    // the compiler's vmcnt tracking assume the younger set is the one staged next, draining both sets
+    stage(buf ^ 1, r);
+    fetch(p + 3, r);
     __syncthreads();
+  };
+  if (npair > 0) {
+    fetch(0, ra);
+    stage(0, ra);
+    fetch(1, ra);
+    fetch(2, rb);
+  }
+  __syncthreads();
+  int p = 0;
+  for (; p + 1 < npair; p += 2) {
+    pair(p, ra, std::integral_constant<int, 0>{});
+    pair(p + 1, rb, std::integral_constant<int, 1>{});
+  }
+  if (p < npair) pair(p, ra, std::integral_constant<int, 0>{});
+
+  // merge the odd-tile half into the even-tile half (LDS reuse: every wave passed the last barrier)
+  constexpr int MW = 2 + 4 * DT;   // floats per lane: m, l, O
+  static_assert(4 * 64 * MW * 4 <= (int)sizeof(Ks), "merge scratch");
+  float* mg = reinterpret_cast<float*>(&Ks[0][0]) + (qw * 64 + lane);
+  if (half) {
+    mg[0] = m_run;
+    mg[256] = l_run;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mg[256 * (2 + 4 * dt + r)] = o[dt][r];
+  }
+  __syncthreads();
+  if (half) return;
+  {
+    const float m1 = mg[0], l1 = mg[256];
+    const float m = vmax(m_run, m1);
+    const float f0 = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m_run - m) * kL2E);
+    const float f1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m1 - m) * kL2E);
+    float l = l_run * f0 + l1 * f1;
+    l = xor32_add(xor16_add(l));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] = o[dt][r] * f0 + mg[256 * (2 + 4 * dt + r)] * f1;
+    l_run = l;
   }
   if (myq < T) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -629,7 +711,7 @@ bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
   if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || HD % 32 || a.T <= 256 ||
       (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 4) || (a.tok_stride * a.ld_qkv) % 8)
     return false;
-  hipLaunchKernelGGL(attn_long_kernel<HD>, dim3(cdiv(a.T, kQB), a.S * a.nh), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_long_kernel<HD>, dim3(cdiv(a.T, kQB), a.S * a.nh), dim3(512), 0, st, a);
   return true;
 }
 
