@@ -473,6 +473,11 @@ __device__ __forceinline__ float vmax(float x, float y) {   // v_max_f32 without
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
   return r;
 }
+__device__ __forceinline__ float vmax3(float x, float y, float z) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
 __device__ __forceinline__ float xor16_max(float x) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -481,19 +486,14 @@ __device__ __forceinline__ float xor32_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-__device__ __forceinline__ float xor16_add(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xor32_add(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
 
 template <int HD>
 __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
-  constexpr int KS = HD + 8;                 // K row stride (bf16): conflict-free fragment reads
-  constexpr int VS = HD;                     // V row stride (bf16), ds_read_b64_tr_b16 rows
+  // row strides (bf16) HD + 16: the only padding up to 32 with conflict-free ds_read_b128 K fragments
+  // (16-lane groups) AND ds_read_b64_tr_b16 V reads (32-lane groups) for HD = 32, 64, 128 (pad 8 / 0 cost
+  // 2x / 4x: SQ_LDS_BANK_CONFLICT was 4.5 extra cycles per LDS instruction)
+  constexpr int KS = HD + 16;
+  constexpr int VS = HD + 16;
   constexpr int KC = HD / 32;                // 32-wide d chunks of Q / K
   constexpr int DT = HD / 16;                // 16-wide d tiles of O
   constexpr int CPR = HD / 8;                // 16-B chunks per row
@@ -522,6 +522,7 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
 
   bf16x8 qf[KC];
   {
+    const float qs = a.scale * kL2E;
     const uint16_t* qr = base + (int64_t)min(myq, T - 1) * tstr;
     const bool qv = myq < T;
 #pragma unroll
@@ -530,9 +531,8 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
       uint32_t pk[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)   // the generic kernel's rounding: bf16(q * scale)
-        pk[j] = qv ? pack_bf16x2(__uint_as_float(w[j] << 16) * a.scale, __uint_as_float(w[j] & 0xffff0000u) * a.scale)
-                   : 0u;
+      for (int j = 0; j < 4; ++j)   // bf16(q * scale * log2 e): scores arrive in log2 units
+        pk[j] = qv ? pack_bf16x2(__uint_as_float(w[j] << 16) * qs, __uint_as_float(w[j] & 0xffff0000u) * qs) : 0u;
       qf[kc] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     }
   }
@@ -565,21 +565,31 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
     }
   };
 
-  floatx4 o[DT];
+  // Softmax against a per-query REFERENCE m (log2 units) that is raised only when a tile's max exceeds it
+  // by more than kTau (or the query sees its first key): the MFMA accumulators start at -m, so on the
+  // common path p = exp2(acc) with no subtraction and O is not rescaled.  The row sum l comes from the
+  // MFMA too (a ones A operand against Pᵀ: every accumulator row is the column sum), so it needs no
+  // VALU adds and no cross-lane reduction.  p <= 2^kTau keeps f32 sums and bf16 P exact enough.
+  constexpr float kTau = 8.f;
+  floatx4 o[DT], ls = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < DT; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;   // l_run: this lane's partial row sum (its 16 keys per tile)
+  float m_run = -INFINITY;   // reference (log2 units); -inf: no visible key yet
   const int tr_off = ((4 * g + (l15 >> 2)) * VS + 4 * (l15 & 3)) * 2;   // attn_short's Vᵀ lane offset (bytes)
   const int krow0 = half * kLKT;                                        // this half's tile inside a pair
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
   auto tile = [&](int t, int buf) __attribute__((always_inline)) {
     const int k0 = t * kLKT;
     const uint16_t* kb = &Ks[buf][krow0 * KS];
-    // Sᵀ: 4 subtiles of 16 keys; lane holds keys k0 + 16 st + 4g + r of query myq
+    const float mb = m_run == -INFINITY ? 0.f : m_run;   // accumulator origin
+    // Sᵀ - m: 4 subtiles of 16 keys; lane holds keys k0 + 16 st + 4g + r of query myq
     floatx4 sc[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      floatx4 acc = {-mb, -mb, -mb, -mb};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&kb[(st * 16 + l15) * KS + kc * 32 + g * 8]);
@@ -600,32 +610,38 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
           sc[st][r] = ok ? sc[st][r] : -INFINITY;
         }
     }
-    float tmax = sc[0][0];
+    float tmax = vmax3(sc[0][0], sc[0][1], sc[0][2]);
+    tmax = vmax3(tmax, sc[0][3], sc[1][0]);
+    tmax = vmax3(tmax, sc[1][1], sc[1][2]);
+    tmax = vmax3(tmax, sc[1][3], sc[2][0]);
+    tmax = vmax3(tmax, sc[2][1], sc[2][2]);
+    tmax = vmax3(tmax, sc[2][3], sc[3][0]);
+    tmax = vmax3(tmax, sc[3][1], sc[3][2]);
+    tmax = vmax(tmax, sc[3][3]);
+    tmax = xor32_max(xor16_max(tmax));   // relative to mb; -inf: every key of the tile masked
+    const bool dead = m_run == -INFINITY;
+    const bool raise = dead ? tmax != -INFINITY : tmax > kTau;
+    if (__ballot(raise)) {   // rare, wave-uniform: move the reference to this tile's max where raised
+      const float m_new = raise ? mb + tmax : m_run;
+      const float shift = raise ? tmax : 0.f;
+      const float alpha = raise && !dead ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[st][r] -= shift;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;   // Oᵀ: lane's column is its own query
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ls[r] *= alpha;
+      m_run = m_new;
+    }
 #pragma unroll
     for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int r = (st == 0 ? 1 : 0); r < 4; ++r) tmax = vmax(tmax, sc[st][r]);
-    tmax = xor32_max(xor16_max(tmax));
-    const float m_new = vmax(m_run, tmax);
-    const bool dead = m_new == -INFINITY;   // no visible key yet for this query
-    const float ml = dead ? 0.f : m_new * kL2E;
-    const float alpha = dead ? 1.f : __builtin_amdgcn_exp2f(fmaf(m_run, kL2E, -ml));
-    float psum = 0.f;
-#pragma unroll
-    for (int st = 0; st < 4; ++st)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sc[st][r], kL2E, -ml));   // exp2(-inf) = 0
-        sc[st][r] = pv;
-        psum += pv;
-      }
-    l_run = fmaf(l_run, alpha, psum);
-    m_run = m_new;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;   // Oᵀ: lane's column is its own query
-    // Oᵀ += Vᵀ·Pᵀ over the tile's two 32-key halves
+      for (int r = 0; r < 4; ++r) sc[st][r] = __builtin_amdgcn_exp2f(sc[st][r]);   // exp2(-inf) = 0
+    // Oᵀ += Vᵀ·Pᵀ, l += 1ᵀ·Pᵀ over the tile's two 32-key halves
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       bf16x8 pb;   // Pᵀ operand: k-index 8g + j <-> key 32 kh + 4g + j (j < 4), 32 kh + 16 + 4g + j - 4
@@ -640,6 +656,7 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
         const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
       }
+      ls = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, ls, 0, 0, 0);
     }
   };
   // buf as a compile-time constant: the two unrolled copies differ, so they are not merged into one body
@@ -674,7 +691,7 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   float* mg = reinterpret_cast<float*>(&Ks[0][0]) + (qw * 64 + lane);
   if (half) {
     mg[0] = m_run;
-    mg[256] = l_run;
+    mg[256] = ls[0];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -682,18 +699,17 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   }
   __syncthreads();
   if (half) return;
+  float l_run;
   {
     const float m1 = mg[0], l1 = mg[256];
     const float m = vmax(m_run, m1);
-    const float f0 = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m_run - m) * kL2E);
-    const float f1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m1 - m) * kL2E);
-    float l = l_run * f0 + l1 * f1;
-    l = xor32_add(xor16_add(l));
+    const float f0 = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - m);
+    const float f1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - m);
+    l_run = ls[0] * f0 + l1 * f1;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[dt][r] = o[dt][r] * f0 + mg[256 * (2 + 4 * dt + r)] * f1;
-    l_run = l;
   }
   if (myq < T) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
