@@ -721,6 +721,104 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   }
 }
 
+// Tiny-sequence attention (T <= 16: FS-EEND's per-frame attention across its C speaker slots,
+// fs_eend.py:456-478 self_attn2 over the slot axis; S = frames x batch sequences).  The work is a few
+// kFLOP per sequence, so the kernel is a bf16 stream (read q, k, v once, write o once): one thread per
+// (sequence, head, query) computes its T scores, softmax and output row in f32 registers; the T threads of
+// a (sequence, head) sit in adjacent lanes, so their k / v rows are one cache-line fetch per wave.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_tiny_kernel(AttnArgs a) {
+  constexpr int C8 = HD / 8;   // 16-B chunks per head row
+  const int T = a.T, D = a.D;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)a.S * a.nh * T) return;
+  const int i = (int)(gid % T);
+  const int64_t sh = gid / T;
+  const int h = (int)(sh % a.nh), s = (int)(sh / a.nh);
+  const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
+                       (int64_t)(s % a.seq_inner) * a.seq_inner_stride;
+  const int64_t tstr = (int64_t)a.tok_stride * a.ld_qkv;
+  const uint16_t* base = reinterpret_cast<const uint16_t*>(a.qkv) + row0 * a.ld_qkv + h * HD;
+  const int klen = a.key_len ? min(a.key_len[s], T) : T;
+  float q[HD];
+  {
+    const uint16_t* qr = base + (int64_t)i * tstr;
+#pragma unroll
+    for (int c = 0; c < C8; ++c) {
+      const uint4 u = *reinterpret_cast<const uint4*>(qr + 8 * c);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // the MFMA kernels' rounding: bf16(q * scale)
+        const uint32_t pk = pack_bf16x2(__uint_as_float(w[j] << 16) * a.scale, __uint_as_float(w[j] & 0xffff0000u) * a.scale);
+        q[8 * c + 2 * j] = __uint_as_float(pk << 16);
+        q[8 * c + 2 * j + 1] = __uint_as_float(pk & 0xffff0000u);
+      }
+    }
+  }
+  float sc[16];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    sc[j] = -INFINITY;
+    if (j < T && j < klen && (!a.causal || j <= i + a.causal_delay)) {
+      const uint16_t* kr = base + (int64_t)j * tstr + D;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < C8; ++c) {
+        const uint4 u = *reinterpret_cast<const uint4*>(kr + 8 * c);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc = fmaf(q[8 * c + 2 * e], __uint_as_float(w[e] << 16), acc);
+          acc = fmaf(q[8 * c + 2 * e + 1], __uint_as_float(w[e] & 0xffff0000u), acc);
+        }
+      }
+      sc[j] = acc;
+      m = fmaxf(m, acc);
+    }
+  }
+  float o[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) o[d] = 0.f;
+  float l = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (sc[j] != -INFINITY) {
+      const float p = __expf(sc[j] - m);
+      l += p;
+      const uint16_t* vr = base + (int64_t)j * tstr + 2 * D;
+#pragma unroll
+      for (int c = 0; c < C8; ++c) {
+        const uint4 u = *reinterpret_cast<const uint4*>(vr + 8 * c);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[8 * c + 2 * e] = fmaf(p, __uint_as_float(w[e] << 16), o[8 * c + 2 * e]);
+          o[8 * c + 2 * e + 1] = fmaf(p, __uint_as_float(w[e] & 0xffff0000u), o[8 * c + 2 * e + 1]);
+        }
+      }
+    }
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (row0 + (int64_t)i * a.tok_stride) * a.ldo + h * HD;
+#pragma unroll
+  for (int c = 0; c < C8; ++c)
+    *reinterpret_cast<uint4*>(orow + 8 * c) =
+        make_uint4(pack_bf16x2(o[8 * c] * inv, o[8 * c + 1] * inv), pack_bf16x2(o[8 * c + 2] * inv, o[8 * c + 3] * inv),
+                   pack_bf16x2(o[8 * c + 4] * inv, o[8 * c + 5] * inv), pack_bf16x2(o[8 * c + 6] * inv, o[8 * c + 7] * inv));
+}
+
+template <int HD>
+bool launch_tiny(const AttnArgs& a, bool bf16, hipStream_t st) {
+  static const bool off = getenv("SDIAR_NO_ATTN_TINY") != nullptr;   // A/B switch: attn_short
+  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || a.T > 16 || HD % 8 || HD > 128 ||
+      (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 8) || (a.tok_stride * a.ld_qkv) % 8)
+    return false;
+  const int64_t n = (int64_t)a.S * a.nh * a.T;
+  hipLaunchKernelGGL(attn_tiny_kernel<HD>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  return true;
+}
+
 template <int HD>
 bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
   static const bool off = getenv("SDIAR_NO_ATTN_LONG") != nullptr;   // A/B switch: the generic kernel
@@ -769,6 +867,7 @@ bool launch_short(const AttnArgs& a, bool bf16, hipStream_t st) {
 
 template <int HD>
 void launch_hd(const AttnArgs& a, bool bf16, hipStream_t st) {
+  if (launch_tiny<HD>(a, bf16, st)) return;
   if (launch_short<HD>(a, bf16, st)) return;
   if constexpr (HD % 32 == 0) {
     if (launch_long<HD>(a, bf16, st)) return;

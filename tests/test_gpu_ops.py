@@ -133,7 +133,8 @@ def _attn_ref(qkv, S, T, D, nh, causal=0, delay=0, key_len=None):
 @pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("S,T,D,nh,causal", [(8, 100, 384, 4, 0), (6, 150, 384, 8, 0), (1, 777, 256, 4, 0),
                                              (2, 300, 256, 4, 1), (3, 33, 512, 4, 0), (5, 256, 256, 4, 1),
-                                             (40, 6, 256, 4, 0), (2, 129, 1024, 8, 0)])
+                                             (40, 6, 256, 4, 0), (2, 129, 1024, 8, 0), (7, 3, 128, 2, 1),
+                                             (33, 16, 256, 4, 1), (9, 11, 512, 4, 0)])
 def test_attention(gpu, precision, S, T, D, nh, causal):
     g = torch.Generator().manual_seed(S * T)
     qkv = torch.randn(S * T, 3 * D, generator=g)
@@ -149,11 +150,12 @@ def test_attention(gpu, precision, S, T, D, nh, causal):
 
 
 @pytest.mark.parametrize("precision", [0, 2])
-def test_attention_key_len(gpu, precision):
-    S, T, D, nh = 3, 70, 384, 8
+@pytest.mark.parametrize("T,kls", [(70, (70, 41, 1)), (9, (9, 4, 1))])   # T <= 16: the tiny-sequence kernel
+def test_attention_key_len(gpu, precision, T, kls):
+    S, D, nh = 3, 384, 8
     g = torch.Generator().manual_seed(5)
     qkv = torch.randn(S * T, 3 * D, generator=g)
-    kl = torch.tensor([70, 41, 1], dtype=torch.int32)
+    kl = torch.tensor(kls, dtype=torch.int32)
     ref = _attn_ref(qkv, S, T, D, nh, key_len=kl)
     out = torch.empty(S * T, D, device=gpu)
     kld = kl.to(gpu)
