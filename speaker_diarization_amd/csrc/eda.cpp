@@ -107,7 +107,7 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   // Linear + LayerNorm
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, E), bf, st);
   layernorm(Y_, rows, E, E, norm_g_, norm_b_, 1e-5f, X_, E, false, st);
-  for (const auto& L : tfm_) run_transformer(L, X_, S, T, E, cfg_.n_heads, key_len, w, st);
+  for (size_t i = 0; i < tfm_.size(); ++i) run_transformer(tfm_[i], X_, S, T, E, cfg_.n_heads, key_len, w, st, 0, 0, i > 0);
   run_conformer_stack(conf_, X_, S, T, E, cfg_.n_heads, 31, key_len, w, st);
   if (plain) {   // eend/models.py:97-99: decoder Linear, activation=sigmoid (eend_infer.py:69)
     ConvGemmArgs p = lin(Tens{X_, false}, rows, E, dec_.w, dec_.beta, Tens{act, false}, cfg_.n_speakers);

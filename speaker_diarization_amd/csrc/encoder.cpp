@@ -141,14 +141,19 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
 }
 
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
-                     const EncoderWork& w, hipStream_t st, int causal, int causal_delay) {
+                     const EncoderWork& w, hipStream_t st, int causal, int causal_delay, bool xb_in) {
   // nn.TransformerEncoderLayer, post-LN: X = LN1(X + SA(X)); X = LN2(X + FFN(X)).
   // X is the fp32 residual stream; the sub-block outputs t (bf16 in bf16 mode) are added
-  // inside the LayerNorm kernel, so every GEMM epilogue only stores.
+  // inside the LayerNorm kernel, so every GEMM epilogue only stores.  In bf16 mode both LNs also
+  // write bf16(X) into AO (dead between the out-projection and the next attention), the A operand
+  // of the GEMMs that read X: the bf16 GEMM paths take bf16 A (an fp32 A is rounded the same way
+  // inside the slow register-staged kernel).  xb_in: AO already holds bf16(X) (the previous layer).
   const int rows = S * T;
   const bool bf = w.bf16;
   const Tens x{X, false}, t{w.Y, bf}, qkv{w.QKV, bf}, ao{w.AO, bf}, h{w.H, bf};
-  conv_gemm(lin(x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
+  uint16_t* xb = bf ? reinterpret_cast<uint16_t*>(w.AO) : nullptr;
+  const Tens xa = bf ? Tens{xb, true} : x;
+  conv_gemm(lin(bf && xb_in ? xa : x, rows, E, L.in_proj, L.in_b, qkv, 3 * E), bf, st);
   AttnArgs a;
   a.qkv = qkv.p; a.io_bf16 = bf; a.S = S; a.T = T; a.D = E; a.nh = nh; a.ld_qkv = 3 * E;
   a.out = ao.p; a.ldo = E; a.scale = 1.f / std::sqrt((float)(E / nh));
@@ -157,12 +162,12 @@ void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int n
   a.causal_delay = causal_delay;
   attention(a, bf, st);
   conv_gemm(lin(ao, rows, E, L.out_proj, L.out_b, t, E), bf, st);
-  add_layernorm(X, t.p, bf, rows, E, L.n1g, L.n1b, 1e-5f, false, X, false, st);
-  ConvGemmArgs p = lin(x, rows, E, L.l1, L.b1, h, L.l1.N);
+  add_layernorm(X, t.p, bf, rows, E, L.n1g, L.n1b, 1e-5f, false, X, false, st, xb);
+  ConvGemmArgs p = lin(xa, rows, E, L.l1, L.b1, h, L.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
   conv_gemm(lin(h, rows, L.l1.N, L.l2, L.b2, t, E), bf, st);
-  add_layernorm(X, t.p, bf, rows, E, L.n2g, L.n2b, 1e-5f, false, X, false, st);
+  add_layernorm(X, t.p, bf, rows, E, L.n2g, L.n2b, 1e-5f, false, X, false, st, xb);
 }
 
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,

@@ -78,8 +78,10 @@ struct EncoderWork {
 
 // X: (S*T, E) fp32, updated in place.  key_len: device int32 (S) or nullptr.
 // causal: key j visible to query i iff j <= i + causal_delay (fs_eend.py:168-171 mask).
+// bf16 mode leaves bf16(X) in w.AO on return; xb_in: it is there on entry too (consecutive layers).
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
-                     const EncoderWork& w, hipStream_t st, int causal = 0, int causal_delay = 0);
+                     const EncoderWork& w, hipStream_t st, int causal = 0, int causal_delay = 0,
+                     bool xb_in = false);
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,
                    const int* key_len, const EncoderWork& w, hipStream_t st);
 // All layers of a torchaudio Conformer; runs the per-token parts as rowprog.hip programs when every

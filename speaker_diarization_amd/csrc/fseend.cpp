@@ -131,7 +131,11 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
   const int D = cfg_.n_units, nh = cfg_.n_heads;
   const int64_t n = (int64_t)S * T * C;
   const bool bf = cfg_.bf16;
-  const Tens a{A, false}, t{A2_, bf}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
+  const Tens t{A2_, bf}, qkv{QKV_, bf}, ao{AO_, bf}, h{H_, bf};
+  // bf16 mode: the GEMMs read bf16(A), which every LayerNorm also writes into AO (dead between the
+  // out-projection and the next attention); the caller leaves it there before the first layer.
+  uint16_t* ab = bf ? reinterpret_cast<uint16_t*>(AO_) : nullptr;
+  const Tens a = bf ? Tens{ab, true} : Tens{A, false};
   const float scale = 1.f / std::sqrt((float)(D / nh));
   // (1) attention over time within each slot, causal
   conv_gemm(lin(a, (int)n, D, fus_.in1, fus_.in1_b, qkv, 3 * D), bf, st);
@@ -144,7 +148,7 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
     attention(t, bf, st);
   }
   conv_gemm(lin(ao, (int)n, D, fus_.out1, fus_.out1_b, t, D), bf, st);
-  add_layernorm(A, t.p, bf, (int)n, D, fus_.n11g, fus_.n11b, 1e-5f, false, A, false, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n11g, fus_.n11b, 1e-5f, false, A, false, st, ab);
   // (2) attention over the C slots of each frame, no mask
   conv_gemm(lin(a, (int)n, D, fus_.in2, fus_.in2_b, qkv, 3 * D), bf, st);
   {
@@ -154,13 +158,13 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
     attention(s, bf, st);
   }
   conv_gemm(lin(ao, (int)n, D, fus_.out2, fus_.out2_b, t, D), bf, st);
-  add_layernorm(A, t.p, bf, (int)n, D, fus_.n21g, fus_.n21b, 1e-5f, false, A, false, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n21g, fus_.n21b, 1e-5f, false, A, false, st, ab);
   // (3) feed-forward
   ConvGemmArgs p = lin(a, (int)n, D, fus_.l1, fus_.b1, h, fus_.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
   conv_gemm(lin(h, (int)n, fus_.l1.N, fus_.l2, fus_.b2, t, D), bf, st);
-  add_layernorm(A, t.p, bf, (int)n, D, fus_.n22g, fus_.n22b, 1e-5f, false, A, false, st);
+  add_layernorm(A, t.p, bf, (int)n, D, fus_.n22g, fus_.n22b, 1e-5f, false, A, false, st, ab);
 }
 
 void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int* lengths, int C, float* preds,
@@ -175,9 +179,9 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
   const EncoderWork w{Y_, QKV_, AO_, H_, nullptr, bf};
   // Encoder
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, D), bf, st);
-  layernorm(Y_, rows, D, D, norm_g_, norm_b_, 1e-5f, X_, D, false, st);
+  layernorm(Y_, rows, D, D, norm_g_, norm_b_, 1e-5f, X_, D, false, st, bf ? reinterpret_cast<uint16_t*>(AO_) : nullptr);
   for (const auto& L : enc_)
-    run_transformer(L, X_, S, T, D, cfg_.n_heads, nullptr, w, st, cfg_.has_mask, cfg_.mask_delay);
+    run_transformer(L, X_, S, T, D, cfg_.n_heads, nullptr, w, st, cfg_.has_mask, cfg_.mask_delay, true);
   // emb[:ilen] re-padded with zeros (:83-84), then the look-ahead conv (:85)
   for (int s = 0; s < S; ++s) {
     const int len = lengths ? lengths[s] : T;
@@ -203,6 +207,7 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
   conv_gemm(lin(Tens{emb, false}, rows, D, conv_emb_, nullptr, Tens{G_, false}, D), bf, st);
   float* A = att_out ? att_out : A_;
   slot_init(G_, rows, C, D, slot_bias_, A, st);
+  if (bf) f32_to_bf16(A, (int64_t)rows * C * D, AO_, st);   // run_fusion's bf16(A) operand
   for (int i = 0; i < cfg_.dec_n_layers; ++i) run_fusion(A, S, T, C, st);
   slot_scores(emb, A, rows, C, D, preds, att_out != nullptr, st);
 }

@@ -128,12 +128,13 @@ void stats_pool(const void* x, bool x_bf16, int B, int T, int C, const float* s,
 // ---------------------------------------------------------------- norms
 // y = LN(x) * g + b over the last dim D; rows of x at stride ldx, y at ldy.
 // y may be bf16 (y_bf16); x is fp32 (the residual stream).
+// y2 (optional, fp32 y only): a bf16 copy of y, the A operand of the GEMMs that read it.
 void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
-               float eps, void* y, int ldy, bool y_bf16, hipStream_t st);
+               float eps, void* y, int ldy, bool y_bf16, hipStream_t st, uint16_t* y2 = nullptr);
 // Residual add fused into LayerNorm: v = x + t (t fp32 or bf16, rows of D); write_x: x = v;
 // y = LN(v) (y may alias x or t: each row is read completely before it is written).
 void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
-                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st);
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2 = nullptr);
 
 // ---------------------------------------------------------------- attention
 // Multi-head self-attention core on a packed in-projection output.

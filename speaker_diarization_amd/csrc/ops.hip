@@ -358,7 +358,8 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
                                                             const void* __restrict__ t, float* __restrict__ xo,
                                                             const float* __restrict__ g,
                                                             const float* __restrict__ bb, float eps,
-                                                            act_t<YBF>* __restrict__ y, int ldy) {
+                                                            act_t<YBF>* __restrict__ y, int ldy,
+                                                            uint16_t* __restrict__ y2) {
   const int hl = threadIdx.x & 31;
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
   if (row >= rows) return;   // whole 32-lane halves leave together
@@ -406,27 +407,30 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
       *reinterpret_cast<uint2*>(yr + c) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
     else
       *reinterpret_cast<float4*>(yr + c) = make_float4(o0, o1, o2, o3);
+    if (y2)   // bf16 shadow of an fp32 y (the next GEMM's A operand; the bf16 GEMMs round A the same way)
+      *reinterpret_cast<uint2*>(y2 + (int64_t)row * ldy + c) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
   }
 }
 
 template <int NV, int TM>
 static void lnv_launch2(const float* x, int rows, int D, int ldx, const void* t, float* xo, const float* g,
-                        const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
+                        const float* b, float eps, void* y, int ldy, bool ybf, uint16_t* y2, hipStream_t st) {
   dim3 grid(cdiv(rows, 8));
   if (ybf)
     hipLaunchKernelGGL((layernorm_vec_kernel<NV, true, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
-                       eps, reinterpret_cast<uint16_t*>(y), ldy);
+                       eps, reinterpret_cast<uint16_t*>(y), ldy, y2);
   else
     hipLaunchKernelGGL((layernorm_vec_kernel<NV, false, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
-                       eps, reinterpret_cast<float*>(y), ldy);
+                       eps, reinterpret_cast<float*>(y), ldy, y2);
 }
 
 template <int NV>
 static void lnv_launch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
-                       const float* g, const float* b, float eps, void* y, int ldy, bool ybf, hipStream_t st) {
-  if (tm == 0) lnv_launch2<NV, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
-  else if (tm == 1) lnv_launch2<NV, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
-  else lnv_launch2<NV, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, st);
+                       const float* g, const float* b, float eps, void* y, int ldy, bool ybf, uint16_t* y2,
+                       hipStream_t st) {
+  if (tm == 0) lnv_launch2<NV, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
+  else if (tm == 1) lnv_launch2<NV, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
+  else lnv_launch2<NV, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
 }
 
 static bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -452,21 +456,29 @@ static void ln_launch(const float* x, int rows, int D, int ldx, const void* t, i
 }
 
 static void ln_dispatch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
-                        const float* g, const float* b, float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
+                        const float* g, const float* b, float eps, void* y, int ldy, bool y_bf16, hipStream_t st,
+                        uint16_t* y2 = nullptr) {
+  SD_CHECK(!y2 || !y_bf16, kErrInvalid, "layernorm: the bf16 shadow output needs an fp32 y");
   const bool vec = D % 128 == 0 && D <= 1024 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(xo) &&
                    aligned16(g) && aligned16(b) && (reinterpret_cast<uintptr_t>(y) & (y_bf16 ? 7 : 15)) == 0 &&
-                   (reinterpret_cast<uintptr_t>(t) & (tm == 2 ? 7 : 15)) == 0;
+                   (reinterpret_cast<uintptr_t>(t) & (tm == 2 ? 7 : 15)) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y2) & 7) == 0;
   if (vec) {
     switch (D / 128) {
-      case 1: lnv_launch<1>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 2: lnv_launch<2>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 3: lnv_launch<3>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 4: lnv_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 5: lnv_launch<5>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 6: lnv_launch<6>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      case 7: lnv_launch<7>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
-      default: lnv_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st); break;
+      case 1: lnv_launch<1>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 2: lnv_launch<2>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 3: lnv_launch<3>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 4: lnv_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 5: lnv_launch<5>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 6: lnv_launch<6>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 7: lnv_launch<7>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      default: lnv_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
     }
+  } else if (y2) {
+    ln_dispatch(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, false, st);
+    SD_CHECK(ldy == D, kErrInvalid, "layernorm: bf16 shadow needs ldy == D");
+    f32_to_bf16(reinterpret_cast<const float*>(y), (int64_t)rows * D, y2, st);
+    return;
   } else if (D <= 256) ln_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
   else if (D <= 512) ln_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
   else if (D <= 1024) ln_launch<16>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, st);
@@ -475,16 +487,17 @@ static void ln_dispatch(const float* x, int rows, int D, int ldx, const void* t,
 }
 
 void layernorm(const float* x, int rows, int D, int ldx, const float* g, const float* b,
-               float eps, void* y, int ldy, bool y_bf16, hipStream_t st) {
-  ProfScope prof("layernorm", 0.0, (4.0 + (y_bf16 ? 2.0 : 4.0)) * rows * D, st);
-  ln_dispatch(x, rows, D, ldx, nullptr, 0, nullptr, g, b, eps, y, ldy, y_bf16, st);
+               float eps, void* y, int ldy, bool y_bf16, hipStream_t st, uint16_t* y2) {
+  ProfScope prof("layernorm", 0.0, (4.0 + (y_bf16 ? 2.0 : 4.0) + (y2 ? 2.0 : 0.0)) * rows * D, st);
+  ln_dispatch(x, rows, D, ldx, nullptr, 0, nullptr, g, b, eps, y, ldy, y_bf16, st, y2);
 }
 
 void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
-                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st) {
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2) {
   ProfScope prof("add_layernorm", 0.0,
-                 (4.0 + (t_bf16 ? 2.0 : 4.0) + (write_x ? 4.0 : 0.0) + (y_bf16 ? 2.0 : 4.0)) * rows * D, st);
-  ln_dispatch(x, rows, D, D, t, t_bf16 ? 2 : 1, write_x ? x : nullptr, g, b, eps, y, D, y_bf16, st);
+                 (4.0 + (t_bf16 ? 2.0 : 4.0) + (write_x ? 4.0 : 0.0) + (y_bf16 ? 2.0 : 4.0) + (y2 ? 2.0 : 0.0)) *
+                     rows * D, st);
+  ln_dispatch(x, rows, D, D, t, t_bf16 ? 2 : 1, write_x ? x : nullptr, g, b, eps, y, D, y_bf16, st, y2);
 }
 
 // ------------------------------------------------------------------ TS-VAD glue
