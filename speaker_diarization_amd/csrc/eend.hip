@@ -27,17 +27,23 @@ namespace {
 
 constexpr int kMaxMels = 64;
 
+// One wave per frame, 8 frames per workgroup.  Everything a frame needs besides its samples is built
+// once per workgroup in LDS: the twiddles, the Hann window (the same sincospi values the per-sample form
+// computed) and each mel filter's nonzero bin range, so the projection runs over ~20 bins instead of
+// BINS (the skipped terms are exact zeros: same sums, same order).  The butterfly stages of a frame
+// belong to its wave alone, so they are ordered by a wave barrier, not a workgroup barrier.
 template <int LOG2N>
-__global__ __launch_bounds__(256) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
+__global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                           int n_frames, int hop, int win_len,
                                                           const float* __restrict__ mel_fb, int n_mels,
                                                           double* __restrict__ out) {
   constexpr int N = 1 << LOG2N;
   constexpr int BINS = N / 2 + 1;
-  constexpr int FPB = 4;
+  constexpr int FPB = 8;
   __shared__ double2 buf[FPB][N];
   __shared__ double2 tw[N / 2];
-  __shared__ double pw[FPB][BINS + 1];
+  __shared__ double win[N];
+  __shared__ int mlo[kMaxMels], mhi[kMaxMels];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int f = blockIdx.x * FPB + w;
@@ -47,26 +53,42 @@ __global__ __launch_bounds__(256) void stft_logmel_kernel(const float* __restric
     sincospi(-2.0 * (double)k / (double)N, &s, &c);
     tw[k] = make_double2(c, s);
   }
+  for (int j = threadIdx.x; j < win_len; j += blockDim.x) {
+    double s, c;
+    sincospi(2.0 * (double)j / (double)win_len, &s, &c);
+    win[j] = 0.5 - 0.5 * c;
+  }
+  for (int m = threadIdx.x; m < n_mels; m += blockDim.x) {
+    mlo[m] = BINS;
+    mhi[m] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_mels * BINS; i += blockDim.x) {
+    const int m = i / BINS, k = i - m * BINS;
+    if (mel_fb[i] != 0.f) {
+      atomicMin(&mlo[m], k);
+      atomicMax(&mhi[m], k + 1);
+    }
+  }
   // Frame f covers padded samples [f*hop, f*hop + N) of the wav zero-padded by N/2;
   // the periodic Hann window of win_len sits at offset (N - win_len)/2.
   const int lpad = (N - win_len) / 2;
   const int64_t base = (int64_t)f * hop - N / 2 + lpad;
+  __syncthreads();   // window table
   for (int n = lane; n < N; n += 64) {
     double v = 0.0;
     const int j = n - lpad;
     if (active && j >= 0 && j < win_len) {
       const int64_t gi = base + j;
-      if (gi >= 0 && gi < n_samples) {
-        double s, c;
-        sincospi(2.0 * (double)j / (double)win_len, &s, &c);
-        v = (double)wav[gi] * (0.5 - 0.5 * c);
-      }
+      if (gi >= 0 && gi < n_samples) v = (double)wav[gi] * win[j];
     }
     const int r = (int)(__brev((unsigned)n) >> (32 - LOG2N));
     buf[w][r] = make_double2(v, 0.0);
   }
-  __syncthreads();
   for (int half = 1; half < N; half <<= 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int tstride = N / (2 * half);
     for (int bfly = lane; bfly < N / 2; bfly += 64) {
       const int grp = bfly / half, pos = bfly % half;
@@ -77,18 +99,18 @@ __global__ __launch_bounds__(256) void stft_logmel_kernel(const float* __restric
       buf[w][i0] = make_double2(a.x + t.x, a.y + t.y);
       buf[w][i1] = make_double2(a.x - t.x, a.y - t.y);
     }
-    __syncthreads();
   }
-  for (int k = lane; k < BINS; k += 64) {
-    const double2 c = buf[w][k];
-    pw[w][k] = c.x * c.x + c.y * c.y;
-  }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (!active) return;
   for (int m = lane; m < n_mels; m += 64) {
     const float* fr = mel_fb + (int64_t)m * BINS;
     double acc = 0.0;
-    for (int k = 0; k < BINS; ++k) acc = fma((double)fr[k], pw[w][k], acc);
+    for (int k = mlo[m]; k < mhi[m]; ++k) {
+      const double2 c = buf[w][k];
+      acc = fma((double)fr[k], c.x * c.x + c.y * c.y, acc);
+    }
     out[(int64_t)f * n_mels + m] = log10(fmax(acc, 1e-10));
   }
 }
@@ -193,12 +215,12 @@ void stft_logmel(const float* wav, int64_t n_samples, int n_frames, int n_fft, i
   if (n_frames <= 0) return;
   ProfScope prof("stft_logmel", 5.0 * n_fft * std::log2((double)n_fft) * n_frames,
                  4.0 * (double)n_frames * hop + 8.0 * n_frames * n_mels, st);
-  const dim3 grid(cdiv(n_frames, 4));
+  const dim3 grid(cdiv(n_frames, 8));
   if (n_fft == 512)
-    hipLaunchKernelGGL(stft_logmel_kernel<9>, grid, dim3(256), 0, st, wav, n_samples, n_frames, hop, win_len,
+    hipLaunchKernelGGL(stft_logmel_kernel<9>, grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
                        mel_fb, n_mels, out);
   else
-    hipLaunchKernelGGL(stft_logmel_kernel<8>, grid, dim3(256), 0, st, wav, n_samples, n_frames, hop, win_len,
+    hipLaunchKernelGGL(stft_logmel_kernel<8>, grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
                        mel_fb, n_mels, out);
   SD_LAUNCH_CHECK();
 }
