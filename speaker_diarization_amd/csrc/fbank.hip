@@ -24,22 +24,55 @@ constexpr int kFrameLen = 400;
 constexpr int kShift = 160;
 constexpr int kNfft = 512;
 constexpr int kBins = kNfft / 2 + 1;
-constexpr int kFramesPerBlock = 4;
+constexpr int kFramesPerBlock = 8;
+constexpr int kMaxFbMels = 128;
 
 __device__ __forceinline__ int bitrev9(int x) { return __brev((unsigned)x) >> (32 - 9); }
+__device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses (no workgroup barrier)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
-__global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
+// One wave per frame, 8 frames per workgroup.  Built once per workgroup in LDS: the twiddles, the
+// window (the same cospif / powf values the per-sample form computed) and each mel filter's nonzero bin
+// range, so the projection runs over a filter's ~10 bins instead of all 257 (the skipped terms are exact
+// zeros: same sums, same order).  A frame's FFT stages belong to its wave alone: wave barriers only.
+__global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                     float in_scale, int n_frames,
                                                     const float* __restrict__ mel_fb, int n_mels,
                                                     const float2* __restrict__ twiddle, int window,
                                                     float* __restrict__ out) {
   __shared__ float2 buf[kFramesPerBlock][kNfft];
   __shared__ float pw[kFramesPerBlock][kBins + 3];
+  __shared__ float2 tw[kNfft / 2];
+  __shared__ float win[kFrameLen];
+  __shared__ int mlo[kMaxFbMels], mhi[kMaxFbMels];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int f = blockIdx.x * kFramesPerBlock + w;
   const bool active = f < n_frames;
   const float* x = wav + (int64_t)(active ? f : 0) * kShift;
+
+  for (int k = threadIdx.x; k < kNfft / 2; k += blockDim.x) tw[k] = twiddle[k];
+  for (int n = threadIdx.x; n < kFrameLen; n += blockDim.x) {
+    const float cw = cospif(2.f * (float)n / (float)(kFrameLen - 1));
+    // hamming (ts_vad_dataset.py:50) or povey = hann^0.85 (kaldi default, used by the
+    // embedding extractor, generate_chunk_speaker_embedding_...py:326-327).
+    win[n] = window == 0 ? 0.54f - 0.46f * cw : powf(0.5f - 0.5f * cw, 0.85f);
+  }
+  for (int m = threadIdx.x; m < n_mels; m += blockDim.x) {
+    mlo[m] = kBins;
+    mhi[m] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_mels * kBins; i += blockDim.x) {
+    const int m = i / kBins, k = i - m * kBins;
+    if (mel_fb[i] != 0.f) {
+      atomicMin(&mlo[m], k);
+      atomicMax(&mhi[m], k + 1);
+    }
+  }
 
   // Load, DC removal.
   float v[7];
@@ -58,8 +91,8 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
     int n = lane + i * 64;
     if (n < kFrameLen) buf[w][n].x = v[i] - mean;   // scratch (real part)
   }
-  __syncthreads();
-  // Pre-emphasis + Hamming, written bit-reversed for the DIT FFT.
+  __syncthreads();   // window table, mel ranges, this frame's scratch
+  // Pre-emphasis + window, written bit-reversed for the DIT FFT.
   float y[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -68,48 +101,44 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
     if (n < kFrameLen) {
       float cur = buf[w][n].x;
       float prev = n > 0 ? buf[w][n - 1].x : cur;
-      const float cw = cospif(2.f * (float)n / (float)(kFrameLen - 1));
-      // hamming (ts_vad_dataset.py:50) or povey = hann^0.85 (kaldi default, used by the
-      // embedding extractor, generate_chunk_speaker_embedding_...py:326-327).
-      float win = window == 0 ? 0.54f - 0.46f * cw : powf(0.5f - 0.5f * cw, 0.85f);
-      val = (cur - 0.97f * prev) * win;
+      val = (cur - 0.97f * prev) * win[n];
     }
     y[i] = val;
   }
-  __syncthreads();
+  wave_sync();
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     int n = lane + i * 64;
     buf[w][bitrev9(n)] = make_float2(y[i], 0.f);
   }
-  __syncthreads();
   // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
   for (int half = 1; half < kNfft; half <<= 1) {
+    wave_sync();
     const int tstride = kNfft / (2 * half);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int bfly = lane + i * 64;
       int grp = bfly / half, pos = bfly % half;
       int i0 = grp * 2 * half + pos, i1 = i0 + half;
-      float2 tw = twiddle[pos * tstride];
+      float2 t0 = tw[pos * tstride];
       float2 a = buf[w][i0], b = buf[w][i1];
-      float2 t = make_float2(b.x * tw.x - b.y * tw.y, b.x * tw.y + b.y * tw.x);
+      float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
       buf[w][i0] = make_float2(a.x + t.x, a.y + t.y);
       buf[w][i1] = make_float2(a.x - t.x, a.y - t.y);
     }
-    __syncthreads();
   }
+  wave_sync();
   for (int k = lane; k < kBins; k += 64) {
     float2 c = buf[w][k];
     pw[w][k] = c.x * c.x + c.y * c.y;
   }
-  __syncthreads();
+  wave_sync();
   if (!active) return;
   const float eps = 1.1920928955078125e-07f;
   for (int m = lane; m < n_mels; m += 64) {
     const float* fr = mel_fb + (int64_t)m * kBins;
     float acc = 0.f;
-    for (int k = 0; k < kBins; ++k) acc = fmaf(fr[k], pw[w][k], acc);
+    for (int k = mlo[m]; k < mhi[m]; ++k) acc = fmaf(fr[k], pw[w][k], acc);
     out[(int64_t)f * n_mels + m] = logf(fmaxf(acc, eps));
   }
 }
@@ -132,7 +161,8 @@ void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fram
   }
   if (n_frames <= 0) return;
   ProfScope prof("fbank_kaldi", 0.0, 4.0 * ((double)n_frames * kShift + (double)n_frames * n_mels), st);
-  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(n_frames, kFramesPerBlock)), dim3(256), 0, st, wav,
+  SD_CHECK(n_mels > 0 && n_mels <= kMaxFbMels, kErrInvalid, "fbank: n_mels out of range");
+  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(n_frames, kFramesPerBlock)), dim3(512), 0, st, wav,
                      n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, window, out);
   SD_LAUNCH_CHECK();
 }
