@@ -13,6 +13,8 @@
 // (+ dil halo rows each side) in LDS while doing so, evaluates the gate, and runs the
 // conv for its <= 100 output rows on MFMA from LDS (transposed: 4 consecutive output
 // channels per lane -> 8-B stores into the dense block's channel slice).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -38,23 +40,19 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
     const uint16_t* __restrict__ x, int T, int dil, const uint16_t* __restrict__ wt /*[32][3*128] bf16*/,
     const float* __restrict__ bias, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gate_in,
-    uint16_t* __restrict__ out, int ldo, int nseg) {
+    uint16_t* __restrict__ out, int ldo, int nseg, int ntask) {
   __shared__ __attribute__((aligned(16))) uint16_t xs[kRows * kC];   // rows s0 - dil .. s0 + 100 + dil
   __shared__ float4 red_t[kP][kL];
   __shared__ float4 red_s[kP][kL];
   __shared__ float ctx[kC];
   __shared__ float h1[kC1];
   __shared__ float gate[kC2];
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);   // the nseg workgroups of an item share an XCD
-  const int b = lid / nseg, s = lid - b * nseg;
   const int tid = threadIdx.x;
   const int part = tid / kL, l = tid % kL;
-  const int t0 = s * kSeg, t1 = min(T, t0 + kSeg);
-  const int r_lo = t0 - dil, r_hi = t1 + dil;          // staged window [r_lo, r_hi)
-  const uint16_t* xb = x + (int64_t)b * T * kC;
-
   // The conv's weight fragments (rows n = nt*16 + l15, k = kk*32 + lk*8; L2-resident) are
-  // requested first so their latency hides behind the row pass.
+  // requested first so their latency hides behind the row pass, and kept for every task of this
+  // persistent workgroup (they are as many bytes as a task's rows: one load per task doubled the
+  // L2 -> CU traffic).
   const int lane = tid & 63, wv = tid >> 6;
   const int l15 = lane & 15, lk = lane >> 4;
   bf16x8 wf[2][12];
@@ -63,6 +61,13 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk)
       wf[nt][kk] = *reinterpret_cast<const bf16x8*>(wt + (nt * 16 + l15) * (3 * kC) + kk * 32 + lk * 8);
+  for (int task = blockIdx.x; task < ntask; task += gridDim.x) {
+  if (task != (int)blockIdx.x) __syncthreads();   // the previous task's LDS reads are done
+  const int lid = xcd_remap(task, ntask);        // the nseg tasks of an item share an XCD
+  const int b = lid / nseg, s = lid - b * nseg;
+  const int t0 = s * kSeg, t1 = min(T, t0 + kSeg);
+  const int r_lo = t0 - dil, r_hi = t1 + dil;          // staged window [r_lo, r_hi)
+  const uint16_t* xb = x + (int64_t)b * T * kC;
 
   // ---- pass over all rows: whole-sequence sum, segment sum, stage the window rows
   float4 at = make_float4(0.f, 0.f, 0.f, 0.f), as = at;
@@ -167,6 +172,19 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
       }
     }
   }
+  }   // task
+}
+
+// Persistent grid: tasks (item, segment) are dealt to at most kCamWgPerCu workgroups per CU.
+constexpr int kCamWgPerCu = 4;
+dim3 cam_grid(int B, int nseg) {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return dim3((unsigned)std::min(B * nseg, kCamWgPerCu * n_cu));
 }
 
 }  // namespace
@@ -184,9 +202,9 @@ void cam_local_fused(const void* x, int B, int T, int dil, const void* wt, const
   const int nseg = cdiv(T, kSeg);
   ProfScope prof("cam_local_fused", 2.0 * B * T * kC2 * 3 * kC + 2.0 * B * nseg * (kC * kC1 + kC1 * kC2),
                  2.0 * B * T * (kC + kC2), st);
-  hipLaunchKernelGGL(cam_local_fused_kernel<true>, dim3(B * nseg), dim3(256), 0, st, static_cast<const uint16_t*>(x),
+  hipLaunchKernelGGL(cam_local_fused_kernel<true>, cam_grid(B, nseg), dim3(256), 0, st, static_cast<const uint16_t*>(x),
                      T, dil, static_cast<const uint16_t*>(wt), bias, w1, b1, w2, b2, nullptr,
-                     static_cast<uint16_t*>(out), ldo, nseg);
+                     static_cast<uint16_t*>(out), ldo, nseg, B * nseg);
   SD_LAUNCH_CHECK();
 }
 
@@ -196,9 +214,9 @@ void cam_local_conv(const void* x, int B, int T, int dil, const void* wt, const 
   SD_CHECK((reinterpret_cast<uintptr_t>(out) & 7) == 0, kErrInvalid, "cam_local_conv: output must be 8-B aligned");
   const int nseg = cdiv(T, kSeg);
   ProfScope prof("cam_local_conv", 2.0 * B * T * kC2 * 3 * kC, 2.0 * B * T * (kC + kC2), st);
-  hipLaunchKernelGGL(cam_local_fused_kernel<false>, dim3(B * nseg), dim3(256), 0, st,
+  hipLaunchKernelGGL(cam_local_fused_kernel<false>, cam_grid(B, nseg), dim3(256), 0, st,
                      static_cast<const uint16_t*>(x), T, dil, static_cast<const uint16_t*>(wt), bias, nullptr, nullptr,
-                     nullptr, nullptr, gate, static_cast<uint16_t*>(out), ldo, nseg);
+                     nullptr, nullptr, gate, static_cast<uint16_t*>(out), ldo, nseg, B * nseg);
   SD_LAUNCH_CHECK();
 }
 
