@@ -103,7 +103,7 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   SD_CHECK(plain || (lengths && perm), kErrInvalid, "lengths and perm are required");
   const int E = cfg_.n_units, rows = S * T, NA = cfg_.max_n_speakers;
   const bool bf = cfg_.bf16;
-  const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf};
+  const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf, true};   // replicas only: split-K allowed
   // Linear + LayerNorm
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, E), bf, st);
   layernorm(Y_, rows, E, E, norm_g_, norm_b_, 1e-5f, X_, E, false, st);

@@ -140,6 +140,23 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
   return L;
 }
 
+void ffn_down_add_ln(const ConvGemmArgs& pd, void* hbuf, float* X, const float* g, const float* b, bool bf,
+                     uint16_t* xb, hipStream_t st, bool split_k) {
+  // X = LN(X + FFN-down(h)).  Short-M, long-K shapes (M 6000, K 2048) run split-K into fp32 slabs that the
+  // LayerNorm sums; the slabs live in the hidden buffer's unused upper half (the bf16 hidden layer takes
+  // rows * K * 2 of its rows * K * 4 bytes).
+  const int rows = pd.B * pd.Ho * pd.Wo, E = pd.N;
+  const int ks = bf && split_k ? gemm_splitk_count(pd) : 1;
+  if (ks > 1 && (int64_t)ks * E * 4 <= (int64_t)pd.K * 2 && pd.K % 8 == 0) {
+    float* slabs = reinterpret_cast<float*>(static_cast<uint16_t*>(hbuf) + (int64_t)rows * pd.K);
+    conv_gemm_splitk(pd, ks, slabs, st);
+    add_layernorm(X, slabs, false, rows, E, g, b, 1e-5f, false, X, false, st, xb, ks);
+    return;
+  }
+  conv_gemm(pd, bf, st);
+  add_layernorm(X, pd.out, bf, rows, E, g, b, 1e-5f, false, X, false, st, xb);
+}
+
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
                      const EncoderWork& w, hipStream_t st, int causal, int causal_delay, bool xb_in) {
   // nn.TransformerEncoderLayer, post-LN: X = LN1(X + SA(X)); X = LN2(X + FFN(X)).
@@ -166,8 +183,7 @@ void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int n
   ConvGemmArgs p = lin(xa, rows, E, L.l1, L.b1, h, L.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
-  conv_gemm(lin(h, rows, L.l1.N, L.l2, L.b2, t, E), bf, st);
-  add_layernorm(X, t.p, bf, rows, E, L.n2g, L.n2b, 1e-5f, false, X, false, st, xb);
+  ffn_down_add_ln(lin(h, rows, L.l1.N, L.l2, L.b2, t, E), w.H, X, L.n2g, L.n2b, bf, xb, st, w.split_k);
 }
 
 void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, int kernel,

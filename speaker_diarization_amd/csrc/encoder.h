@@ -74,10 +74,16 @@ struct EncoderWork {
   float* H;        // rows * max(ffn, 2E)
   float* partial;  // S * cdiv(E, 64) * 2
   bool bf16;
+  // Split-K FFN down-projections allowed (their split count depends on the row count, so a model whose
+  // rows are sharded over ranks — TS-VAD windows, bit-identical for any world size — leaves this off).
+  bool split_k = false;
 };
 
 // X: (S*T, E) fp32, updated in place.  key_len: device int32 (S) or nullptr.
 // causal: key j visible to query i iff j <= i + causal_delay (fs_eend.py:168-171 mask).
+// X = LN(X + pd) for the FFN down-projection pd (split-K into slabs in hbuf's upper half when that pays).
+void ffn_down_add_ln(const ConvGemmArgs& pd, void* hbuf, float* X, const float* g, const float* b, bool bf,
+                     uint16_t* xb, hipStream_t st, bool split_k);
 // bf16 mode leaves bf16(X) in w.AO on return; xb_in: it is there on entry too (consecutive layers).
 void run_transformer(const TransformerL& L, float* X, int S, int T, int E, int nh, const int* key_len,
                      const EncoderWork& w, hipStream_t st, int causal = 0, int causal_delay = 0,

@@ -163,8 +163,7 @@ void FsEendModel::run_fusion(float* A, int S, int T, int C, hipStream_t st) {
   ConvGemmArgs p = lin(a, (int)n, D, fus_.l1, fus_.b1, h, fus_.l1.N);
   p.act = kActRelu;
   conv_gemm(p, bf, st);
-  conv_gemm(lin(h, (int)n, fus_.l1.N, fus_.l2, fus_.b2, t, D), bf, st);
-  add_layernorm(A, t.p, bf, (int)n, D, fus_.n22g, fus_.n22b, 1e-5f, false, A, false, st, ab);
+  ffn_down_add_ln(lin(h, (int)n, fus_.l1.N, fus_.l2, fus_.b2, t, D), H_, A, fus_.n22g, fus_.n22b, bf, ab, st, true);
 }
 
 void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int* lengths, int C, float* preds,
@@ -176,7 +175,7 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
   SD_CHECK(ld_in >= in_ld_ && ld_in % 4 == 0, kErrInvalid, "feature row stride must be >= in_ld and % 4");
   const int D = cfg_.n_units, rows = S * T;
   const bool bf = cfg_.bf16;
-  const EncoderWork w{Y_, QKV_, AO_, H_, nullptr, bf};
+  const EncoderWork w{Y_, QKV_, AO_, H_, nullptr, bf, true};   // replicas only: split-K allowed
   // Encoder
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, D), bf, st);
   layernorm(Y_, rows, D, D, norm_g_, norm_b_, 1e-5f, X_, D, false, st, bf ? reinterpret_cast<uint16_t*>(AO_) : nullptr);

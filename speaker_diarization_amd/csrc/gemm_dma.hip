@@ -50,6 +50,14 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   const int m0 = (tile / n_nt) * BM;
   const int n0 = (tile % n_nt) * BN;
   const int taps = p.kh * p.kw;
+  // split-K share [kb, ke) of this workgroup (blockIdx.y); whole K without a split
+  const int z = blockIdx.y;
+  int kb = 0, ke = p.K;
+  if (p.ksplit > 1) {
+    const int kc = ((p.K + BK - 1) / BK + p.ksplit - 1) / p.ksplit * BK;
+    kb = min(p.K, z * kc);
+    ke = min(p.K, kb + kc);
+  }
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), (short)0,
                                                                       (int)kOOB, 0x00020000);
@@ -86,7 +94,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   }
 
   auto issue = [&](int kt, int stg) {
-    const int k0 = kt * BK;
+    const int k0 = kb + kt * BK;
     int tap = 0, c0 = k0;
     if (taps > 1) {
       tap = k0 / p.Cin;
@@ -100,7 +108,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
     for (int j = 0; j < AI; ++j) {
       const int hi = a_h[j] + dho, wi = a_w[j] + dwo;
       const int c = c0 + a_lc[j] * 8;
-      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && (k0 + a_lc[j] * 8) < p.K;
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && (k0 + a_lc[j] * 8) < ke;
       const uint32_t off = ok ? (uint32_t)((((int64_t)(a_bh[j] + hi) * p.W + wi) * p.lda + p.a_coff + c) * 2)
                               : kOOB;
       lds_ptr_t dst = (lds_ptr_t)(As + (wid * (BM / 4) + j * 8) * BK);
@@ -109,7 +117,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       const int k = k0 + b_lc[j] * 8;
-      const bool ok = b_row[j] < p.N && k < p.K;
+      const bool ok = b_row[j] < p.N && k < ke;
       const uint32_t off = ok ? (uint32_t)(((int64_t)b_row[j] * p.K + k) * 2) : kOOB;
       lds_ptr_t dst = (lds_ptr_t)(Bs + (wid * (BN / 4) + j * 8) * BK);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, dst, 16, off, 0, 0, 0);
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = (p.K + BK - 1) / BK;
+  const int KT = (ke - kb + BK - 1) / BK;
   const int l15 = lane & 15, lk = lane >> 4;
   // Optional BN-ReLU prologue (CAM dense layers: nonlinear1 before linear1): applied
   // in place on the landed A stage, 16 B per thread-step, before the MFMAs read it.
@@ -225,8 +233,9 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
     for (int u = 0; u < 4; ++u) {
       const bool ok = full || n + u < p.N;
       al[u] = (p.alpha && ok) ? p.alpha[n + u] : 1.f;
-      be[u] = (p.beta && ok) ? p.beta[n + u] : 0.f;
+      be[u] = (p.beta && ok && z == 0) ? p.beta[n + u] : 0.f;   // split-K: bias once, in slab 0
     }
+    void* const outp = p.ksplit > 1 ? static_cast<void*>(reinterpret_cast<float*>(p.out) + z * p.split_stride) : p.out;
     float4 rv[ITER];
     if (p.res) {
       const float* rbase = reinterpret_cast<const float*>(p.res);
@@ -259,14 +268,14 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
       const int64_t o = (int64_t)m * p.o_sw + n;
       if (full) {
         if (p.out_bf16)
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.out) + o) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(outp) + o) =
               make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         else
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(outp) + o) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         for (int u = 0; u < 4 && n + u < p.N; ++u) {
-          if (p.out_bf16) reinterpret_cast<uint16_t*>(p.out)[o + u] = f2bf_bits(v[u]);
-          else reinterpret_cast<float*>(p.out)[o + u] = v[u];
+          if (p.out_bf16) reinterpret_cast<uint16_t*>(outp)[o + u] = f2bf_bits(v[u]);
+          else reinterpret_cast<float*>(outp)[o + u] = v[u];
         }
       }
     }
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
 template <int BM, int BN>
 void launch(const ConvGemmArgs& p, hipStream_t st) {
   const int M = p.B * p.Ho * p.Wo;
-  dim3 grid(cdiv(p.N, BN) * cdiv(M, BM));
+  dim3 grid(cdiv(p.N, BN) * cdiv(M, BM), p.ksplit > 1 ? p.ksplit : 1);
   hipLaunchKernelGGL((gemm_dma_kernel<BM, BN>), grid, dim3(256), 0, st, p);
 }
 
@@ -369,6 +378,36 @@ void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st) {
     if (big) launch<128, 32>(p, st); else launch<64, 32>(p, st);
   }
   SD_LAUNCH_CHECK();
+}
+
+// Split-K for the short-M, long-K GEMMs (the post-LN FFN down-projections: M 6000, K 2048, N 256 is 188
+// 64x128 tiles, one per CU, each walking 32 k-tiles at one DMA latency apiece): ksplit workgroups per tile.
+int gemm_splitk_count(const ConvGemmArgs& p) {
+  static const bool off = getenv("SDIAR_NO_SPLITK") != nullptr;   // A/B switch
+  const int M = p.B * p.Ho * p.Wo;
+  if (off || !gemm_dma_supported(p) || p.kh * p.kw != 1 || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
+      p.act != kActNone || p.o_sn != 1 || p.K < 1024 || p.N % 4)
+    return 1;
+  const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
+  const int64_t tiles = (int64_t)cdiv(M, 128) * cdiv(p.N, bn);
+  const int64_t tiles_launched = tiles >= 512 ? tiles : (int64_t)cdiv(M, 64) * cdiv(p.N, bn);
+  int ks = 1;
+  while (ks < 4 && tiles_launched * ks < 768 && p.K / (2 * ks) >= 512) ks *= 2;
+  return ks;
+}
+
+void conv_gemm_splitk(const ConvGemmArgs& p_in, int ksplit, float* slabs, hipStream_t st) {
+  SD_CHECK(ksplit >= 1 && ksplit <= 8, kErrInvalid, "splitk: bad split count");
+  ConvGemmArgs p = p_in;
+  const int M = p.B * p.Ho * p.Wo;
+  p.ksplit = ksplit;
+  p.split_stride = (int64_t)M * p.N;
+  p.out = slabs;
+  p.out_bf16 = false;
+  p.o_sb = (int64_t)p.Ho * p.Wo * p.N; p.o_sh = (int64_t)p.Wo * p.N; p.o_sw = p.N; p.o_sn = 1;
+  ProfScope prof("gemm_dma_splitk", 2.0 * M * p.N * (double)p.K,
+                 2.0 * M * (double)p.K + 2.0 * p.N * p.K + 4.0 * ksplit * M * p.N, st);
+  conv_gemm_dma(p, st);
 }
 
 }  // namespace sd

@@ -50,6 +50,10 @@ struct ConvGemmArgs {
   const int* kv_cursor = nullptr;
   int kv_mult = 1, kv_col0 = 0;
   int64_t kv_ld = 0;
+  // Split-K (gemm_dma path only, via conv_gemm_splitk): blockIdx.y = split z sums k-tiles of its share of
+  // K into fp32 slab z at out + z * split_stride (bias in slab 0 only; no act / alpha / residual).
+  int ksplit = 1;
+  int64_t split_stride = 0;
 };
 // Row order of a GLU projection (2C, K) -> groups of [16 value rows | their 16 gate rows].
 inline int glu_interleave_row(int r, int C) {   // new row index of original row r
@@ -60,6 +64,10 @@ inline int glu_interleave_row(int r, int C) {   // new row index of original row
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
 void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
+// Split-K: the split count worth using for p on the gemm_dma path (1 = none), and the launch writing
+// ksplit fp32 row-major (M x N) slabs to `slabs` (the consumer sums them, e.g. add_layernorm's t_slabs).
+int gemm_splitk_count(const ConvGemmArgs& p);
+void conv_gemm_splitk(const ConvGemmArgs& p, int ksplit, float* slabs, hipStream_t st);
 bool gemm_ring_supported(const ConvGemmArgs& p);             // bf16 A/out, taps==1, K<=1024, N>=96, tall M
 void conv_gemm_ring(const ConvGemmArgs& p, hipStream_t st);
 bool gemm_stream_supported(const ConvGemmArgs& p);            // bf16 A linear, K%64==0, K<=768, no res
@@ -133,8 +141,10 @@ void layernorm(const float* x, int rows, int D, int ldx, const float* g, const f
                float eps, void* y, int ldy, bool y_bf16, hipStream_t st, uint16_t* y2 = nullptr);
 // Residual add fused into LayerNorm: v = x + t (t fp32 or bf16, rows of D); write_x: x = v;
 // y = LN(v) (y may alias x or t: each row is read completely before it is written).
+// t_slabs > 1 (fp32 t only): t is the sum of t_slabs slabs t + i * rows * D (a split-K GEMM's partials).
 void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
-                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2 = nullptr);
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2 = nullptr,
+                   int t_slabs = 1);
 
 // ---------------------------------------------------------------- attention
 // Multi-head self-attention core on a packed in-projection output.

@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
                                                             const float* __restrict__ g,
                                                             const float* __restrict__ bb, float eps,
                                                             act_t<YBF>* __restrict__ y, int ldy,
-                                                            uint16_t* __restrict__ y2) {
+                                                            uint16_t* __restrict__ y2, int t_slabs) {
   const int hl = threadIdx.x & 31;
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
   if (row >= rows) return;   // whole 32-lane halves leave together
@@ -371,8 +371,11 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
     const int c = (hl + i * 32) * 4;
     float4 a = *reinterpret_cast<const float4*>(xr + c);
     if constexpr (TM == 1) {
-      const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(t) + (int64_t)row * D + c);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      for (int sl = 0; sl < t_slabs; ++sl) {   // split-K partial slabs, summed in slab order
+        const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(t) +
+                                                           ((int64_t)sl * rows + row) * D + c);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
     }
     if constexpr (TM == 2) {
       const uint2 b = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(t) + (int64_t)row * D + c);
@@ -414,23 +417,24 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
 
 template <int NV, int TM>
 static void lnv_launch2(const float* x, int rows, int D, int ldx, const void* t, float* xo, const float* g,
-                        const float* b, float eps, void* y, int ldy, bool ybf, uint16_t* y2, hipStream_t st) {
+                        const float* b, float eps, void* y, int ldy, bool ybf, uint16_t* y2, int t_slabs,
+                        hipStream_t st) {
   dim3 grid(cdiv(rows, 8));
   if (ybf)
     hipLaunchKernelGGL((layernorm_vec_kernel<NV, true, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
-                       eps, reinterpret_cast<uint16_t*>(y), ldy, y2);
+                       eps, reinterpret_cast<uint16_t*>(y), ldy, y2, t_slabs);
   else
     hipLaunchKernelGGL((layernorm_vec_kernel<NV, false, TM>), grid, dim3(256), 0, st, x, rows, D, ldx, t, xo, g, b,
-                       eps, reinterpret_cast<float*>(y), ldy, y2);
+                       eps, reinterpret_cast<float*>(y), ldy, y2, t_slabs);
 }
 
 template <int NV>
 static void lnv_launch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
                        const float* g, const float* b, float eps, void* y, int ldy, bool ybf, uint16_t* y2,
-                       hipStream_t st) {
-  if (tm == 0) lnv_launch2<NV, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
-  else if (tm == 1) lnv_launch2<NV, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
-  else lnv_launch2<NV, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, st);
+                       int t_slabs, hipStream_t st) {
+  if (tm == 0) lnv_launch2<NV, 0>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, t_slabs, st);
+  else if (tm == 1) lnv_launch2<NV, 1>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, t_slabs, st);
+  else lnv_launch2<NV, 2>(x, rows, D, ldx, t, xo, g, b, eps, y, ldy, ybf, y2, t_slabs, st);
 }
 
 static bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -457,23 +461,26 @@ static void ln_launch(const float* x, int rows, int D, int ldx, const void* t, i
 
 static void ln_dispatch(const float* x, int rows, int D, int ldx, const void* t, int tm, float* xo,
                         const float* g, const float* b, float eps, void* y, int ldy, bool y_bf16, hipStream_t st,
-                        uint16_t* y2 = nullptr) {
+                        uint16_t* y2 = nullptr, int t_slabs = 1) {
   SD_CHECK(!y2 || !y_bf16, kErrInvalid, "layernorm: the bf16 shadow output needs an fp32 y");
+  SD_CHECK(t_slabs == 1 || tm == 1, kErrInvalid, "layernorm: t slabs need an fp32 t");
   const bool vec = D % 128 == 0 && D <= 1024 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(xo) &&
                    aligned16(g) && aligned16(b) && (reinterpret_cast<uintptr_t>(y) & (y_bf16 ? 7 : 15)) == 0 &&
                    (reinterpret_cast<uintptr_t>(t) & (tm == 2 ? 7 : 15)) == 0 &&
                    (reinterpret_cast<uintptr_t>(y2) & 7) == 0;
   if (vec) {
     switch (D / 128) {
-      case 1: lnv_launch<1>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 2: lnv_launch<2>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 3: lnv_launch<3>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 4: lnv_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 5: lnv_launch<5>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 6: lnv_launch<6>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      case 7: lnv_launch<7>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
-      default: lnv_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, st); break;
+      case 1: lnv_launch<1>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 2: lnv_launch<2>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 3: lnv_launch<3>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 4: lnv_launch<4>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 5: lnv_launch<5>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 6: lnv_launch<6>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      case 7: lnv_launch<7>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
+      default: lnv_launch<8>(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, y_bf16, y2, t_slabs, st); break;
     }
+  } else if (t_slabs > 1) {
+    SD_CHECK(false, kErrInvalid, "layernorm: t slabs need D % 128 == 0 and 16-B aligned rows");
   } else if (y2) {
     ln_dispatch(x, rows, D, ldx, t, tm, xo, g, b, eps, y, ldy, false, st);
     SD_CHECK(ldy == D, kErrInvalid, "layernorm: bf16 shadow needs ldy == D");
@@ -493,11 +500,11 @@ void layernorm(const float* x, int rows, int D, int ldx, const float* g, const f
 }
 
 void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const float* g, const float* b,
-                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2) {
+                   float eps, bool write_x, void* y, bool y_bf16, hipStream_t st, uint16_t* y2, int t_slabs) {
   ProfScope prof("add_layernorm", 0.0,
-                 (4.0 + (t_bf16 ? 2.0 : 4.0) + (write_x ? 4.0 : 0.0) + (y_bf16 ? 2.0 : 4.0) + (y2 ? 2.0 : 0.0)) *
-                     rows * D, st);
-  ln_dispatch(x, rows, D, D, t, t_bf16 ? 2 : 1, write_x ? x : nullptr, g, b, eps, y, D, y_bf16, st, y2);
+                 (4.0 + (t_bf16 ? 2.0 : 4.0 * t_slabs) + (write_x ? 4.0 : 0.0) + (y_bf16 ? 2.0 : 4.0) +
+                  (y2 ? 2.0 : 0.0)) * rows * D, st);
+  ln_dispatch(x, rows, D, D, t, t_bf16 ? 2 : 1, write_x ? x : nullptr, g, b, eps, y, D, y_bf16, st, y2, t_slabs);
 }
 
 // ------------------------------------------------------------------ TS-VAD glue
