@@ -487,7 +487,7 @@ __device__ __forceinline__ float xor32_max(float x) {
   return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-template <int HD>
+template <int HD, bool HOIST>
 __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   // row strides (bf16) HD + 16: the only padding up to 32 with conflict-free ds_read_b128 K fragments
   // (16-lane groups) AND ds_read_b64_tr_b16 V reads (32-lane groups) for HD = 32, 64, 128 (pad 8 / 0 cost
@@ -585,6 +585,33 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
     const int k0 = t * kLKT;
     const uint16_t* kb = &Ks[buf][krow0 * KS];
     const float mb = m_run == -INFINITY ? 0.f : m_run;   // accumulator origin
+    // Every LDS fragment of the tile is requested up front, in source order ahead of the softmax's rare
+    // branch (a block boundary the scheduler does not hoist loads across): the Vᵀ reads' latency then hides
+    // behind the S MFMAs and the softmax instead of stalling the P·V MFMAs (the waves of a workgroup run
+    // phase-locked between barriers, so other waves do not cover it).
+    // HOIST (small grids, latency-bound: ILP over occupancy) — large grids keep the reads next to their
+    // MFMAs, which leaves 114 instead of 142 VGPRs (4 waves per SIMD instead of 3) at HD 64.
+    bf16x8 kf[4][KC];
+    bf16x8 vf[HOIST ? 2 : 1][HOIST ? DT : 1];
+    const uint32_t vb0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)&Vs[buf][0]) +
+                         (uint32_t)(krow0 * VS * 2) + (uint32_t)tr_off;
+    auto vfrag = [&](int kh, int dt) __attribute__((always_inline)) {
+      const uint32_t vbase = vb0 + (uint32_t)(32 * kh * VS * 2);
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + 16 * VS * 2 + dt * 32));
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+          kf[st][kc] = *reinterpret_cast<const bf16x8*>(&kb[(st * 16 + l15) * KS + kc * 32 + g * 8]);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) vf[kh][dt] = vfrag(kh, dt);
+    }
     // Sᵀ - m: 4 subtiles of 16 keys; lane holds keys k0 + 16 st + 4g + r of query myq
     floatx4 sc[4];
 #pragma unroll
@@ -592,8 +619,8 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
       floatx4 acc = {-mb, -mb, -mb, -mb};
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&kb[(st * 16 + l15) * KS + kc * 32 + g * 8]);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], acc, 0, 0, 0);
+        if constexpr (!HOIST) kf[st][kc] = *reinterpret_cast<const bf16x8*>(&kb[(st * 16 + l15) * KS + kc * 32 + g * 8]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][kc], qf[kc], acc, 0, 0, 0);
       }
       sc[st] = acc;
     }
@@ -647,13 +674,11 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
       bf16x8 pb;   // Pᵀ operand: k-index 8g + j <-> key 32 kh + 4g + j (j < 4), 32 kh + 16 + 4g + j - 4
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sc[2 * kh + (j >> 2)][j & 3];
-      const uint32_t vbase = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)&Vs[buf][0]) +
-                             (uint32_t)((krow0 + 32 * kh) * VS * 2) + (uint32_t)tr_off;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + dt * 32));
-        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(uintptr_t)(vbase + 16 * VS * 2 + dt * 32));
-        const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        bf16x8 va;
+        if constexpr (HOIST) va = vf[kh][dt];
+        else va = vfrag(kh, dt);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[dt], 0, 0, 0);
       }
       ls = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, ls, 0, 0, 0);
@@ -825,7 +850,19 @@ bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
   if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || HD % 32 || a.T <= 256 ||
       (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 4) || (a.tok_stride * a.ld_qkv) % 8)
     return false;
-  hipLaunchKernelGGL(attn_long_kernel<HD>, dim3(cdiv(a.T, kQB), a.S * a.nh), dim3(512), 0, st, a);
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const dim3 grid(cdiv(a.T, kQB), a.S * a.nh);
+  // fewer than 2 workgroups per CU: latency-bound, hoist the fragment reads (measured: T 6000 with 4
+  // heads 67 -> 57 us; with 24 sequence-heads the occupancy loss made it 215 -> 244 us)
+  if ((int64_t)grid.x * grid.y < 2LL * n_cu)
+    hipLaunchKernelGGL((attn_long_kernel<HD, true>), grid, dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_long_kernel<HD, false>), grid, dim3(512), 0, st, a);
   return true;
 }
 
