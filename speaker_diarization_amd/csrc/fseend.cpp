@@ -185,12 +185,16 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
   for (int s = 0; s < S; ++s) {
     const int len = lengths ? lengths[s] : T;
     SD_CHECK(len >= 1 && len <= T, kErrInvalid, "sequence length out of range");
-    if (len < T)
+    if (len < T) {
       SD_HIP(hipMemsetAsync(X_ + ((int64_t)s * T + len) * D, 0, (size_t)(T - len) * D * sizeof(float), st));
+      if (bf)   // the encoder's last LayerNorm left bf16(X) in AO_: the conv reads that copy
+        SD_HIP(hipMemsetAsync(reinterpret_cast<uint16_t*>(AO_) + ((int64_t)s * T + len) * D, 0,
+                              (size_t)(T - len) * D * sizeof(uint16_t), st));
+    }
   }
   {
     ConvGemmArgs p;
-    p.A = X_; p.a_bf16 = false; p.B = S; p.H = 1; p.W = T; p.Cin = D; p.lda = D; p.a_coff = 0;
+    p.A = bf ? static_cast<const void*>(AO_) : X_; p.a_bf16 = bf; p.B = S; p.H = 1; p.W = T; p.Cin = D; p.lda = D; p.a_coff = 0;
     p.kh = 1; p.kw = cnn_.w.kw; p.sh = 1; p.sw = 1; p.ph = 0; p.pw = 9; p.dh = 1; p.dw = 1;
     p.Ho = 1; p.Wo = T + 18 - (cnn_.w.kw - 1);
     SD_CHECK(p.Wo == T, kErrInvalid, "cnn padding 9 requires conv_delay 9 (fs_eend.py:41)");
