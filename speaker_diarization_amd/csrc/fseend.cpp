@@ -192,6 +192,7 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
                               (size_t)(T - len) * D * sizeof(uint16_t), st));
     }
   }
+  int ks = 1;
   {
     ConvGemmArgs p;
     p.A = bf ? static_cast<const void*>(AO_) : X_; p.a_bf16 = bf; p.B = S; p.H = 1; p.W = T; p.Cin = D; p.lda = D; p.a_coff = 0;
@@ -202,10 +203,17 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
     p.beta = cnn_.beta;
     p.out = Y_; p.out_bf16 = false;
     p.o_sb = (int64_t)T * D; p.o_sh = 0; p.o_sw = D; p.o_sn = 1;
-    conv_gemm(p, bf, st);
+    // 19 taps x 256 = K 4864 over M = frames: split-K into fp32 slabs in the (now idle) hidden buffer,
+    // summed by the L2 normalisation that consumes the conv output
+    ks = bf ? gemm_splitk_count(p) : 1;
+    if (ks > 1 && ks * D <= cfg_.enc_ffn) conv_gemm_splitk(p, ks, H_, st);
+    else {
+      ks = 1;
+      conv_gemm(p, bf, st);
+    }
   }
   float* emb = emb_out ? emb_out : EMB_;
-  row_l2norm(Y_, rows, D, emb, st);
+  row_l2norm(ks > 1 ? H_ : Y_, rows, D, emb, st, ks);
   // Decoder
   conv_gemm(lin(Tens{emb, false}, rows, D, conv_emb_, nullptr, Tens{G_, false}, D), bf, st);
   float* A = att_out ? att_out : A_;

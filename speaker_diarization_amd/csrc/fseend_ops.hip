@@ -11,17 +11,34 @@
 namespace sd {
 namespace {
 
+// slabs > 1: x is the sum of `slabs` split-K partial slabs x + k * rows * D (summed in slab order).
 __global__ __launch_bounds__(256) void row_l2norm_kernel(const float* __restrict__ x, int rows, int D,
-                                                         float* __restrict__ y) {
+                                                         float* __restrict__ y, int slabs) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= rows) return;
   const float* xr = x + (int64_t)r * D;
+  constexpr int kMaxPer = 8;   // D <= 512
+  float v[kMaxPer];
   float s = 0.f;
-  for (int i = lane; i < D; i += 64) s = fmaf(xr[i], xr[i], s);
+#pragma unroll
+  for (int j = 0; j < kMaxPer; ++j) {
+    const int i = lane + 64 * j;
+    float a = 0.f;
+    if (i < D) {
+      a = xr[i];
+      for (int k = 1; k < slabs; ++k) a += xr[(int64_t)k * rows * D + i];
+    }
+    v[j] = a;
+    s = fmaf(a, a, s);
+  }
   s = warp_sum(s);
   const float n = sqrtf(s);
-  for (int i = lane; i < D; i += 64) y[(int64_t)r * D + i] = xr[i] / n;
+#pragma unroll
+  for (int j = 0; j < kMaxPer; ++j) {
+    const int i = lane + 64 * j;
+    if (i < D) y[(int64_t)r * D + i] = v[j] / n;
+  }
 }
 
 // out[(t*C + c), :] = g[t, :] + p[c, :]
@@ -64,10 +81,11 @@ __global__ __launch_bounds__(256) void slot_scores_kernel(const float* __restric
 
 }  // namespace
 
-void row_l2norm(const float* x, int rows, int D, float* y, hipStream_t st) {
+void row_l2norm(const float* x, int rows, int D, float* y, hipStream_t st, int slabs) {
   if (rows <= 0) return;
-  ProfScope prof("row_l2norm", 3.0 * rows * D, 8.0 * rows * D, st);
-  hipLaunchKernelGGL(row_l2norm_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, D, y);
+  SD_CHECK(D <= 512 && slabs >= 1, kErrInvalid, "row_l2norm: D > 512");
+  ProfScope prof("row_l2norm", 3.0 * rows * D, 4.0 * (slabs + 1) * rows * D, st);
+  hipLaunchKernelGGL(row_l2norm_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, D, y, slabs);
   SD_LAUNCH_CHECK();
 }
 

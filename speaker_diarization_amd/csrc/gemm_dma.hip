@@ -385,7 +385,7 @@ void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st) {
 int gemm_splitk_count(const ConvGemmArgs& p) {
   static const bool off = getenv("SDIAR_NO_SPLITK") != nullptr;   // A/B switch
   const int M = p.B * p.Ho * p.Wo;
-  if (off || !gemm_dma_supported(p) || p.kh * p.kw != 1 || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
+  if (off || !gemm_dma_supported(p) || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
       p.act != kActNone || p.o_sn != 1 || p.K < 1024 || p.N % 4)
     return 1;
   const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);

@@ -396,7 +396,8 @@ void attractor_scores(const float* emb, int S, int T, int E, const float* att, i
                       const float* lb, float* probs, float* act, hipStream_t st);
 
 // ---------------------------------------------------------------- fs-eend glue (fseend_ops.hip)
-void row_l2norm(const float* x, int rows, int D, float* y, hipStream_t st);   // y = x / |x| per row
+// y = x / |x| per row (D <= 512); slabs > 1: x is the sum of split-K slabs x + k * rows * D
+void row_l2norm(const float* x, int rows, int D, float* y, hipStream_t st, int slabs = 1);
 // out (T*C, D): out[t*C + c] = g[t] + p[c]
 void slot_init(const float* g, int T, int C, int D, const float* p, float* out, hipStream_t st);
 // scores (T, C) = emb[t]·att[t,c]/|att[t,c]|; write_norm: att normalised in place.
