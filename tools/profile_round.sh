@@ -12,5 +12,6 @@ for WL in "$@"; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$WL" -o run -- python3 $BENCH \
     > "$OUT/trace_$WL.log" 2>&1
   cp "$(find "$OUT/trace_$WL" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats_$WL.csv"
+  rm -rf "$OUT/trace_$WL"   # the full traces exceed what gpurun copies back
   echo "$WL ok"
 done
