@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) void lstm_step_bf16_kernel(
 constexpr int LS_H = 256;
 constexpr int LS_WS = LS_H + 16;     // bf16 LDS row stride of the W slice (conflict-free fragment reads)
 constexpr int LS_MAXMT = 6;
+constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (256 B: own L2 line)
 
 // TAG (MT <= 2): the hand-off without counters.  Every exchanged word is (step tag << 16) | bf16 h, so a
 // consumer knows a value is current from the value itself: the producer's write-through stores go out with no
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   const int n_bb = (B + BB - 1) / BB;
   const int d = grp / n_bb, b0 = (grp % n_bb) * BB;
   const int G4 = ndir * 4 * H;
-  unsigned* cnt = counters + grp;
+  unsigned* cnt = counters + grp * LS_CNT_STRIDE;   // one cache line per group (no false sharing)
   const int ub = 64 * q + 16 * w + 4 * g;       // first of this lane's 4 units
 
   // W slice -> LDS: slice row (gate, j) = W_hh row gate*H + 64q + j.
@@ -546,7 +547,7 @@ int64_t lstm_work_floats(int B, int H, int ndir) {
   // persistent path at the largest row block it may pick (Bp <= B + 16 * LS_MAXMT)
   const int Bp = (B + 16 * LS_MAXMT);
   const int64_t grp = (int64_t)ndir * cdiv(B, 16) + 2;
-  const int64_t bytes = (int64_t)lstm_group_hx_bytes(Bp, ndir) + 4 * grp + 16;
+  const int64_t bytes = (int64_t)lstm_group_hx_bytes(Bp, ndir) + 4LL * LS_CNT_STRIDE * grp + 16;
   return std::max<int64_t>(step_path, (bytes + 3) / 4);
 }
 
@@ -571,7 +572,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       // Exchange buffers + counters live in the caller's per-handle `work` (lstm_work_floats), so
       // recurrences of different handles / streams / devices never share scratch.
       const size_t hx_bytes = lstm_group_hx_bytes(Bp, ndir);
-      const size_t ctl_bytes = ((size_t)(groups + 1) * 4 + 15) / 16 * 16;
+      const size_t ctl_bytes = ((size_t)(groups + 1) * 4 * LS_CNT_STRIDE + 15) / 16 * 16;
       SD_CHECK((int64_t)((hx_bytes + ctl_bytes + 3) / 4) <= lstm_work_floats(B, H, ndir), kErrInvalid,
                "lstm: work buffer too small");
       uint16_t* hx = reinterpret_cast<uint16_t*>(work);
@@ -583,7 +584,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       if (tag) SD_HIP(hipMemsetAsync(hx, 0, hx_bytes, st));   // no stale tag may match
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
-      int* err = reinterpret_cast<int*>(ctl + groups);
+      int* err = reinterpret_cast<int*>(ctl + (size_t)groups * LS_CNT_STRIDE);
       if (tag && mt == 1) launch_lstm_group<1, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
       else if (tag) launch_lstm_group<2, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
       else switch (mt) {
