@@ -69,6 +69,28 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
   const int r_lo = t0 - dil, r_hi = t1 + dil;          // staged window [r_lo, r_hi)
   const uint16_t* xb = x + (int64_t)b * T * kC;
 
+  if constexpr (!FUSED) {
+    // Only the window rows: every 16-B chunk of them requested at once (one HBM round trip per task,
+    // the row pass below keeps four in flight per lane), halo rows outside [0, T) zero-filled.
+    constexpr int CH = kC / 8;                        // 16-B chunks per row
+    constexpr int NL = (kRows * CH + 255) / 256;      // chunks per thread
+    const int nr = r_hi - r_lo;
+    uint4 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 256 * i, r = c / CH, q = c - r * CH;
+      const int t = r_lo + r;
+      v[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (r < nr && t >= 0 && t < T) v[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)t * kC + q * 8);
+    }
+    if (tid < kC2) gate[tid] = gate_in[((int64_t)b * nseg + s) * kC2 + tid];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + 256 * i, r = c / CH, q = c - r * CH;
+      if (r < nr) *reinterpret_cast<uint4*>(xs + xs_off(r, q * 8)) = v[i];
+    }
+    __syncthreads();
+  } else {
   // ---- pass over all rows: whole-sequence sum, segment sum, stage the window rows
   float4 at = make_float4(0.f, 0.f, 0.f, 0.f), as = at;
   auto take = [&](int t, const uint2& u) {
@@ -91,10 +113,7 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
     const int t = r_lo + r;
     if (t < 0 || t >= T) *reinterpret_cast<uint2*>(xs + xs_off(r, 4 * l)) = make_uint2(0u, 0u);
   }
-  if constexpr (!FUSED) {
-    if (tid < kC2) gate[tid] = gate_in[((int64_t)b * nseg + s) * kC2 + tid];
-    __syncthreads();
-  } else {
+  {
   red_t[part][l] = at;
   red_s[part][l] = as;
   __syncthreads();
@@ -133,6 +152,7 @@ __global__ __launch_bounds__(256) void cam_local_fused_kernel(
   }
   __syncthreads();
   }
+  }   // FUSED
 
   // ---- conv rows t0..t1-1 on MFMA: C'[n][t] = sum_k W[n][k] X[t][k], k = tap*128 + c
   const int nrows = t1 - t0;
