@@ -509,9 +509,17 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wid >> 2, qw = wid & 3;   // key-tile parity, query group (wave-uniform: SGPR branches)
   const int g = lane >> 4, l15 = lane & 15;
-  const int sh = blockIdx.y, s = sh / a.nh, h = sh % a.nh;
+  // XCD-aware order: the query blocks of one (sequence, head) are consecutive logical ids on one XCD, so
+  // its K/V prefix (1.5 MB at T 6000, d 64) is fetched into that XCD's L2 once instead of into all eight
+  // (FETCH_SIZE: 150 MB per decoder launch for 37 MB of K/V)
+  const int nqb = (int)gridDim.x;
+  // (large grids only: a small grid's heads would land whole on few XCDs, heavy query blocks together)
+  const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int lid = HOIST ? lin : xcd_remap(lin, (int)(gridDim.x * gridDim.y));
+  const int sh = lid / nqb, s = sh / a.nh, h = sh % a.nh;
   const int T = a.T, D = a.D;
-  const int qb = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;   // heaviest first
+  const int qbi = lid - sh * nqb;
+  const int qb = a.causal ? nqb - 1 - qbi : qbi;   // heaviest first
   const int qblk0 = qb * kQB;
   const int myq = qblk0 + qw * 16 + l15;
   const int64_t row0 = (int64_t)(s / a.seq_inner) * (a.seq_outer ? a.seq_outer : (int64_t)T) +
