@@ -216,8 +216,10 @@ __global__ __launch_bounds__(kRingThreads) void gemm_ring_kernel(ConvGemmArgs p)
     }
   }
 
-  // ---- epilogue: lane holds rows m0 + wm*TM + mt*16 + l15, columns n .. n+3
-  const int64_t out_bytes = (int64_t)M * p.o_sw * 2;
+  // ---- epilogue: lane holds rows m0 + wm*TM + mt*16 + l15, columns n .. n+3 (bf16: 8-B stores; fp32 out,
+  // e.g. the TS-VAD LSTM input projection: 16-B stores)
+  const int eb = p.out_bf16 ? 2 : 4;
+  const int64_t out_bytes = (int64_t)M * p.o_sw * eb;
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, (int)(out_bytes < (int64_t)kOOB ? out_bytes : kOOB - 1),
                                         0x00020000);
@@ -235,9 +237,14 @@ __global__ __launch_bounds__(kRingThreads) void gemm_ring_kernel(ConvGemmArgs p)
       }
       const int m = m0 + wm * TM + mt * 16 + l15;
       const int n = n0 + wn * TN + nt * 16 + lk * 4;
-      const uint32_t off = (m < M && n < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + n) * 2) : kOOB;
-      const u32x2_t v = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
-      __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+      const uint32_t off = (m < M && n < p.N) ? (uint32_t)(((int64_t)m * p.o_sw + n) * eb) : kOOB;
+      if (p.out_bf16) {
+        const u32x2_t v = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+        __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+      } else {
+        const u32x4_t v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 0);
+      }
     }
 }
 
@@ -507,8 +514,10 @@ bool gemm_ring_supported(const ConvGemmArgs& p) {
   const int M = p.B * p.Ho * p.Wo;
   const bool row_major = p.o_sn == 1 && out_rows_linear(p) && a_rows_linear(p);
   const int64_t a_bytes = ((int64_t)p.B * p.H * p.W) * p.lda * 2;
-  return p.a_bf16 && p.out_bf16 && !p.gate && !p.res && !p.glu && p.kh * p.kw == 1 &&
-         (!p.pre_scale || p.pre_shift) && p.K <= kRingMaxK && p.K % 8 == 0 && p.lda % 8 == 0 &&
+  // fp32 output: the one-tile-per-workgroup kernel only (N > RBN); K > kRingMaxK: no prologue (the s/h
+  // staging in LDS is what bounds K)
+  return p.a_bf16 && (p.out_bf16 || p.N > RBN) && !p.gate && !p.res && !p.glu && p.kh * p.kw == 1 &&
+         (!p.pre_scale || p.pre_shift) && (!p.pre_scale || p.K <= kRingMaxK) && p.K % 8 == 0 && p.lda % 8 == 0 &&
          p.a_coff % 8 == 0 && p.N >= 96 && p.N % 4 == 0 && p.o_sw % 4 == 0 && row_major && M >= 8 * RBM &&
          a_bytes < (int64_t)kOOB && (int64_t)p.N * p.K * 2 < (int64_t)kOOB;
 }
