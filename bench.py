@@ -214,7 +214,7 @@ def kernel_report(kernels, workload, ms_per_step, precision):
                         "achieved_tflops": round(flops / s / 1e12, 1), "mfma_frac": round(flops / s / 1e12 / PEAKS[dt], 4),
                         "achieved_gbs": round(byts / s / 1e9, 1), "hbm_frac": round(byts / s / 1e9 / HBM_PEAK, 4)}
     tab = {}
-    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:14]:
+    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])[:24]:
         r = roofline_of(k, v)
         tab[k] = {"share": round(v["ms"] / kms, 3), "ms": round(v["ms"], 3), "launches": v["launches"],
                   "bound": r["bound"], "frac": r["frac"]}

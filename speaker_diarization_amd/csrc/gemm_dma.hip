@@ -139,23 +139,50 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   // its logical chunk, hence its 8 k columns, are fixed: 2 x 2 float4 loads per k-tile.
   const int pre_pc = tid & 7;
   const int pre_lc = pre_pc ^ ((tid >> 3) & 7);
+  // Multi-tap convs: a prologue row whose input position is conv zero padding for the k-tile's tap must
+  // stay 0 (BN-ReLU is applied before the padding); the rows a thread transforms are fixed (r = tid/8 + 32j),
+  // so their input offsets are computed once.
+  constexpr int PRJ = BM / 32;
+  int pr_h[PRJ], pr_w[PRJ];
+#pragma unroll
+  for (int j = 0; j < PRJ; ++j) {
+    const int m = m0 + (tid >> 3) + 32 * j;
+    if (m < M) {
+      const int wo = m % p.Wo, t = m / p.Wo;
+      pr_h[j] = (t % p.Ho) * p.sh - p.ph;
+      pr_w[j] = wo * p.sw - p.pw;
+    } else {
+      pr_h[j] = -(1 << 28);
+      pr_w[j] = 0;
+    }
+  }
   auto prologue = [&](int kt, int stg) {
     uint16_t* As = sm + stg * STAGE;
-    const int k = kt * BK + pre_lc * 8;
+    const int kg = kb + kt * BK;                    // first k of the tile (one tap: Cin % BK == 0)
+    const int tap = taps > 1 ? kg / p.Cin : 0;
+    const int ti = tap / p.kw, tj = tap - ti * p.kw;
+    const int k = kg + pre_lc * 8;                  // this thread's 8 k columns
+    const int c = k - tap * p.Cin;                  // their channel (k itself for one tap)
     float sc[8], sh[8];
-    if (k + 8 <= p.K) {
-      const float4 s0 = *reinterpret_cast<const float4*>(p.pre_scale + k);
-      const float4 s1 = *reinterpret_cast<const float4*>(p.pre_scale + k + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(p.pre_shift + k);
-      const float4 h1 = *reinterpret_cast<const float4*>(p.pre_shift + k + 4);
+    if (k + 8 <= ke) {
+      const float4 s0 = *reinterpret_cast<const float4*>(p.pre_scale + c);
+      const float4 s1 = *reinterpret_cast<const float4*>(p.pre_scale + c + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(p.pre_shift + c);
+      const float4 h1 = *reinterpret_cast<const float4*>(p.pre_shift + c + 4);
       sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
       sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
     } else {
 #pragma unroll
       for (int u = 0; u < 8; ++u) { sc[u] = 0.f; sh[u] = 0.f; }   // K tail: A*0 + 0 (weights are 0 too)
     }
-    for (int i = tid; i < BM * 8; i += 256) {
+#pragma unroll
+    for (int j = 0; j < PRJ; ++j) {
+      const int i = tid + 256 * j;
       uint4* ptr = reinterpret_cast<uint4*>(As + (i >> 3) * BK + pre_pc * 8);
+      if (taps > 1 && !((unsigned)(pr_h[j] + ti * p.dh) < (unsigned)p.H && (unsigned)(pr_w[j] + tj * p.dw) < (unsigned)p.W)) {
+        *ptr = make_uint4(0u, 0u, 0u, 0u);   // zero padding stays zero
+        continue;
+      }
       uint4 v = *ptr;
       uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -362,7 +389,7 @@ bool gemm_dma_supported(const ConvGemmArgs& p) {
   const int taps = p.kh * p.kw;
   const int64_t a_bytes = ((int64_t)p.B * p.H * p.W) * p.lda * 2;
   const int64_t w_bytes = (int64_t)p.N * p.K * 2;
-  return p.a_bf16 && (!p.pre_scale || (taps == 1 && p.pre_shift)) && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
+  return p.a_bf16 && (!p.pre_scale || (p.pre_shift && (taps == 1 || p.Cin % BK == 0))) && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
          p.a_coff % 8 == 0 && a_bytes < (int64_t)kOOB && w_bytes < (int64_t)kOOB;
 }
 
