@@ -177,6 +177,11 @@ struct AttnArgs {
   // mask_dump (T*T int32, zeroed) receives 1/2 = visible/masked for each visited pair of seq 0, head 0.
   int mask_form = 0;
   int* mask_dump = nullptr;
+  // Internal (attention.hip): split-KV of the long kernel's small grids — blockIdx.z halves of a query
+  // block's key pairs, partials merged by the later finisher through split_ws / split_cnt.
+  int nsplit = 1;
+  float* split_ws = nullptr;
+  int* split_cnt = nullptr;
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
