@@ -278,7 +278,8 @@ bool gemm_areg_supported(const ConvGemmArgs& p) {
   return p.a_bf16 && !p.pre_scale && !p.gate && !p.res && p.kh * p.kw == 1 &&
          // measured against gemm_stream on the C2 shapes (M = 360000, K = 384): faster from
          // N = 768 (GLU pw1 768: 318 vs 355 us; QKV 1152: 508 vs 586 us), slower at N = 384 / 512
-         (p.K == 384 || p.K == 256 || p.K == 192) && p.N % NB == 0 && p.N >= 768 && p.N <= kMaxN &&
+         // K 256 (FS-EEND decoder in-projections, M 36000, N 768): gemm_stream 132 vs 167 us, so not here
+         (p.K == 384 || p.K == 192) && p.N % NB == 0 && p.N >= 768 && p.N <= kMaxN &&
          p.lda % 8 == 0 && p.a_coff % 8 == 0 && p.o_sw % 4 == 0 && row_major && M >= 64 * RB &&
          (int64_t)M * p.lda * 2 < (int64_t)kOOB && (int64_t)p.N * p.K * 2 < (int64_t)kOOB &&
          (int64_t)M * p.o_sw * 4 < (int64_t)kOOB && (!p.glu || (p.out_bf16 && p.act == kActNone && p.N % 32 == 0));
