@@ -327,9 +327,11 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       const float* swb = f.stem_w;
       asm volatile("" : "+s"(swb));
       const float* swp = swb + (tid & 3) * 72;
-      float sw[8][9];
+      // channel pairs as packed f32 (v_pk_fma_f32: the same fmaf chain per channel, two per instruction)
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      f32x2 sw2[4][9];
 #pragma unroll
-      for (int k = 0; k < 72; ++k) sw[k / 9][k % 9] = swp[k];
+      for (int k = 0; k < 72; ++k) sw2[k / 18][k % 9][(k / 9) & 1] = swp[k];
       for (int i = tid; i < n_vec; i += kBandThreads) {
         const int pix = i >> 2, rr = pix / Wp, px = pix - rr * Wp;
         const bool ok = (unsigned)(hb + rr) < (unsigned)p.H && (unsigned)(w0 + px) < (unsigned)W;
@@ -340,11 +342,15 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
           for (int dw = 0; dw < 3; ++dw) x9[dh * 3 + dw] = fbs[(rr + dh) * (Wp + 2) + px + dw];
         float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          float acc = 0.f;
+        for (int u2 = 0; u2 < 4; ++u2) {
+          f32x2 acc = {0.f, 0.f};
 #pragma unroll
-          for (int k = 0; k < 9; ++k) acc = fmaf(sw[u][k], x9[k], acc);
-          v[u] = ok ? fmaxf(acc * s_al[u] + s_be[u], 0.f) : 0.f;
+          for (int k = 0; k < 9; ++k) acc = __builtin_elementwise_fma(sw2[u2][k], f32x2{x9[k], x9[k]}, acc);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int u = 2 * u2 + e;
+            v[u] = ok ? fmaxf(acc[e] * s_al[u] + s_be[u], 0.f) : 0.f;
+          }
         }
         *reinterpret_cast<uint4*>(xs + pix * kPS + (i & 3) * 8) =
             make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
