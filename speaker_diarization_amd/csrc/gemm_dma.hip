@@ -13,6 +13,8 @@
 //   one vmcnt(0) + barrier per k-tile.
 // * Epilogue identical to gemm_bf16.hip (LDS-staged, coalesced, bf16/fp32 out).
 // Handles taps == 1 (linear / 1x1 conv) and multi-tap convs with Cin % 64 == 0.
+#include <string>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -415,6 +417,15 @@ int gemm_splitk_count(const ConvGemmArgs& p) {
   if (off || !gemm_dma_supported(p) || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
       p.act != kActNone || p.o_sn != 1 || p.K < 1024 || p.N % 4)
     return 1;
+  // enough 256x128 tiles for one per CU: the ring GEMM (3-stage DMA ring) beats the split (FS-EEND decoder
+  // FFN-down, M 36000: 163 vs 243 us for 2 launches; at M 6000 the split wins, 96 vs 141 us for 4)
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  if (gemm_ring_supported(p) && (int64_t)cdiv(M, 256) * cdiv(p.N, 128) >= n_cu) return 1;
   const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
   const int64_t tiles = (int64_t)cdiv(M, 128) * cdiv(p.N, bn);
   const int64_t tiles_launched = tiles >= 512 ? tiles : (int64_t)cdiv(M, 64) * cdiv(p.N, bn);
@@ -432,7 +443,10 @@ void conv_gemm_splitk(const ConvGemmArgs& p_in, int ksplit, float* slabs, hipStr
   p.out = slabs;
   p.out_bf16 = false;
   p.o_sb = (int64_t)p.Ho * p.Wo * p.N; p.o_sh = (int64_t)p.Wo * p.N; p.o_sw = p.N; p.o_sn = 1;
-  ProfScope prof("gemm_dma_splitk", 2.0 * M * p.N * (double)p.K,
+  static const bool detail = getenv("SDIAR_PROF_DETAIL") != nullptr;
+  std::string key = "gemm_dma_splitk";
+  if (detail && prof_enabled()) key += " M=" + std::to_string(M) + " K=" + std::to_string(p.K) + " ks=" + std::to_string(ksplit);
+  ProfScope prof(key.c_str(), 2.0 * M * p.N * (double)p.K,
                  2.0 * M * (double)p.K + 2.0 * p.N * p.K + 4.0 * ksplit * M * p.N, st);
   conv_gemm_dma(p, st);
 }
