@@ -8,13 +8,15 @@ segment_shift 1 s, 64 windows per batch, bf16 MFMA.  One step = the whole hot
 path over one meeting: wav already in HBM -> kaldi fbank -> window CMN -> model
 -> sigmoid + overlap-average posteriors (NS, 25 Hz frames).
 
-N GPUs (torchrun, one process per GPU, RCCL): STRONG scaling by default — one
-fixed long meeting (60 min, the C4 long-form shape of BASELINE.json) with the
-headline model, its windows sharded by contiguous ranges of the global 64-window
-batch grid; each rank runs the sub-span fbank + its windows, and the per-window
-logits are all-gathered (the only exchange) before the ordered overlap average.
-`--scaling weak` restores N x 10-min meetings.  `--workload c4` runs the C4 model
-(CAM++ + transformer, rs_len 4) on the same 60-min strong-scaling meeting.
+N GPUs (`--gpus N`: bench.py starts N ranks itself, or runs under the driver's
+torchrun; one process per GPU, RCCL): BASELINE C4 — one fixed 60-min 4-speaker
+meeting, TS-VAD CAM++ + transformer, rs_len 4 — as STRONG scaling: its windows are
+sharded by contiguous ranges of the global 64-window batch grid, each rank runs the
+sub-span fbank + its windows, and the per-window logits are all-gathered (the only
+exchange) before the ordered overlap average.  The N=1 line carries the same
+meeting's 1-GPU time (`c4_60min_ms`), so every point of the series reads against
+one workload.  `--workload c2 --gpus N` runs the headline model on that meeting;
+`--scaling weak` gives N x 10-min meetings.
 """
 from __future__ import annotations
 
@@ -68,12 +70,17 @@ HBM_PEAK = 8000.0                        # GB/s
 ATTN_KERNELS = ("mha_block", "attention_bf16", "attention_f32")   # fused block first (C2 conformer)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without an external launcher bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS) + ["dist_check"],
+                    help="default: c2 on one GPU, c4 (the 60-min strong-scaling meeting) on N > 1; "
+                         "dist_check = CPU/gloo launcher self-test (no GPU)")
+    ap.add_argument("--no-c4-ref", action="store_true",
+                    help="N=1 C2 line: skip the 1-GPU time of the C4 60-min meeting the N>1 lines run")
     ap.add_argument("--minutes", type=float, default=None,
                     help="weak scaling: meeting minutes per GPU; strong scaling: total meeting minutes")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
@@ -86,7 +93,7 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--chunk", type=int, default=None, help="c5s: model frames per streaming push")
     ap.add_argument("--no-graph", action="store_true", help="c5s: direct launches instead of hipGraph replay")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # ----------------------------------------------------------------------------- host facts
@@ -223,17 +230,84 @@ def kernel_report(kernels, workload, ms_per_step, precision):
 
 
 # ----------------------------------------------------------------------------- distributed helpers
-def dist_setup():
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` with no external launcher: start N fresh child processes of this
+    script, one per GPU, with the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR/PORT) — the reference's own multi-process pattern is torchrun
+    --nproc_per_node (egs/magicdata-ramc/tests/test_ddp.sh:3).  This parent never touches
+    the GPU (no torch import), so nothing GPU-initialised is forked or exec'd.  If a rank
+    fails, the others are stopped (they would wait in a collective) and its code is returned."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:           # our own children, by handle
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dist_setup(backend="nccl"):
+    """One process per GPU from the torchrun environment (the driver's launcher or
+    launch_ranks); backend "nccl" is RCCL on ROCm.  backend "gloo" is the CPU self-test."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if backend == "gloo":
+        dev = torch.device("cpu")
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=dev)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, torch.device("cuda", local)
+        world = dist.get_world_size()
+    return world, rank, dev
+
+
+def ranks_joined(world, dev):
+    """Every rank's id, all-gathered over the job's backend (RCCL on the GPU path): the
+    line's proof that N ranks joined the collective the data path uses."""
+    if world == 1:
+        return [0]
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([dist.get_rank()], device=dev, dtype=torch.int64)
+    allr = torch.empty(world, device=dev, dtype=torch.int64)
+    dist.all_gather_into_tensor(allr, mine)
+    return [int(x) for x in allr.cpu()]
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
 
 
 def timed(step, warmup, steps, world, dev):
@@ -243,24 +317,57 @@ def timed(step, warmup, steps, world, dev):
     import torch.distributed as dist
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     out = None
     for _ in range(steps):
         out = step()
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, out
+
+
+def main_dist_check(a):
+    """CPU self-test of the launcher (tests/test_bench_launcher.py): the same rank setup,
+    timing and line as the TS-VAD strong-scaling path, with gloo instead of RCCL and the
+    device forward replaced by seeded window logits, so no GPU is needed.  Each rank takes its
+    contiguous share of the C4 60-min meeting's 64-window batch grid; the all-gather of
+    ts_vad/pipeline.py re-assembles the global window order, which every rank checks."""
+    import torch
+    from speaker_diarization_amd.ts_vad.pipeline import gather_windows
+    from speaker_diarization_amd.ts_vad.windows import plan_windows, shard_batches
+    world, rank, dev = dist_setup("gloo")
+    joined = ranks_joined(world, dev)
+    plan = plan_windows(60 * 60 * 25, 4, 1)
+    g = torch.Generator().manual_seed(777)
+    full = torch.randn(plan.n_win, 4, plan.chunk, generator=g)
+    w0, w1 = shard_batches(plan, a.batch, world, rank)
+
+    def step():
+        local = full[w0:w1].clone()
+        return gather_windows(local, plan, a.batch, world) if world > 1 else local
+    elapsed, got = timed(step, a.warmup, a.steps, world, dev)
+    ok = bool(torch.equal(got, full))
+    if rank == 0:
+        print(json.dumps({"metric": "launcher self-test (window-logit all-gather)", "value": round(
+            plan.n_win * a.steps / elapsed, 1), "unit": "windows/s", "n_gpus": world, "rccl_ranks": None,
+            "ranks_joined": joined, "backend": "gloo", "gather_matches_global_order": ok,
+            "shard": [w0, w1], "n_win": plan.n_win, "steps": a.steps, "warmup": a.warmup}))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
 
 
 # ----------------------------------------------------------------------------- TS-VAD (C2 / C4)
@@ -330,35 +437,74 @@ def der_parity(meeting, gpu_post, cpu_post, span_s, n_real=4, label_rate=25):
             "note": "seeded random weights: absolute DER is meaningless, the GPU-vs-reference difference is the check"}
 
 
-def main(a, wl):
+def tsvad_job(wl, a, world, dev, total_min):
+    """Model, pipeline and synthetic meeting of a TS-VAD workload (C2 / C4)."""
     import torch
     from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
     from speaker_diarization_amd.ts_vad.model import TSVADModel
     from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
-    from speaker_diarization_amd.ts_vad.postprocess import posteriors_to_rttm_gpu
     from speaker_diarization_amd.weights import TSVADConfig, to_torch, tsvad_state_dict
-
-    world, rank, dev = dist_setup()
-    scaling = a.scaling or ("strong" if (world > 1 or wl.get("strong")) else "weak")
-    if scaling == "strong":
-        total_min = a.minutes if a.minutes is not None else 60.0
-    else:
-        total_min = (a.minutes if a.minutes is not None else wl["minutes"]) * world
     cfg = TSVADConfig(rs_len=wl["rs_len"]) if wl["variant"] == 0 else TSVADConfig.ots_vad_v1(rs_len=wl["rs_len"])
     sd_np = tsvad_state_dict(cfg, seed=777)
     model = TSVADModel(cfg, device=dev, precision=a.precision, max_batch=max(a.batch, a.device_batch))
     model.load_state_dict(to_torch(sd_np))
     pipe = TSVADPipeline(model, segment_shift=1, batch_size=a.batch)
-
     meeting = make_meeting(total_min * 60.0, n_spk=4, seed=777)
     ts_np = speaker_embeddings(4, seed=777)
-    wav = torch.from_numpy(meeting.wav).to(dev)
-    ts = torch.from_numpy(ts_np).to(dev)
-    n_lab = meeting.labels.shape[1]
-    frames_per_step = meeting.wav.size // 160     # 10 ms frames of the whole meeting
+    job = dict(cfg=cfg, sd_np=sd_np, model=model, pipe=pipe, meeting=meeting, ts_np=ts_np,
+               wav=torch.from_numpy(meeting.wav).to(dev), ts=torch.from_numpy(ts_np).to(dev),
+               n_lab=meeting.labels.shape[1], frames=meeting.wav.size // 160)
+    job["step"] = lambda: pipe.posteriors(job["wav"], job["ts"], job["n_lab"])
+    return job
 
-    def step():
-        return pipe.posteriors(wav, ts, n_lab)
+
+def c4_reference(a, dev):
+    """The N>1 lines' workload (BASELINE C4: CAM++ + transformer, rs_len 4, one fixed 60-min
+    meeting) timed on this one GPU, so the scaling series reads against one workload."""
+    wl = WORKLOADS["c4"]
+    job = tsvad_job(wl, a, 1, dev, 60.0)
+    steps = max(1, min(a.steps, 3))
+    elapsed, _ = timed(job["step"], 1, steps, 1, dev)
+    out = {"workload": wl["desc"], "meeting_minutes": 60.0, "windows": job["pipe"].plan(job["n_lab"]).n_win,
+           "steps": steps, "warmup": 1, "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "value": round(job["frames"] * steps / elapsed, 1), "unit": "frames/s",
+           "note": "same meeting, model and window grid as the --gpus N > 1 lines (strong scaling)"}
+    del job
+    return out
+
+
+def posterior_parity(gpu_post, cpu_post, span_frames, n_real=4, med_filter=21):
+    """Posterior-level parity of the product path against the fp32 CPU oracle over the span
+    the CPU sample covers exactly: max / mean |diff| of the averaged posteriors, and per recipe
+    threshold the frames whose speech decision differs — on the raw posteriors and after the
+    reference's medfilt(21) (ts_vad2/infer.py:90-100, scipy.signal.medfilt as the reference)."""
+    from scipy.signal import medfilt
+    from speaker_diarization_amd.ts_vad.postprocess import THRESHOLDS
+    g = np.asarray(gpu_post[:n_real, :span_frames], np.float32)
+    c = np.asarray(cpu_post[:n_real, :span_frames], np.float32)
+    d = np.abs(g.astype(np.float64) - c)
+    gm = np.stack([medfilt(x, med_filter) for x in g])
+    cm = np.stack([medfilt(x, med_filter) for x in c])
+    return {"frames_compared": int(g.size), "tracks": n_real, "span_label_frames": int(span_frames),
+            "max_abs_diff": float(d.max()), "mean_abs_diff": float(d.mean()),
+            "decision_flips_raw": {str(t): int(((g > t) != (c > t)).sum()) for t in THRESHOLDS},
+            "decision_flips_medfilt": {str(t): int(((gm > t) != (cm > t)).sum()) for t in THRESHOLDS},
+            "reference": "oracle/pipeline_ref.py (ts_vad2/infer.py:216-285 restated, fp32 torch-CPU)"}
+
+
+def main(a, wl):
+    from speaker_diarization_amd.ts_vad.postprocess import posteriors_to_rttm_gpu
+
+    world, rank, dev = dist_setup()
+    joined = ranks_joined(world, dev)
+    scaling = a.scaling or ("strong" if (world > 1 or wl.get("strong")) else "weak")
+    if scaling == "strong":
+        total_min = a.minutes if a.minutes is not None else 60.0
+    else:
+        total_min = (a.minutes if a.minutes is not None else wl["minutes"]) * world
+    job = tsvad_job(wl, a, world, dev, total_min)
+    pipe, meeting, step = job["pipe"], job["meeting"], job["step"]
+    frames_per_step = job["frames"]     # 10 ms frames of the whole meeting
 
     elapsed, post = timed(step, a.warmup, a.steps, world, dev)
     ms_per_step = elapsed / a.steps * 1000.0
@@ -368,25 +514,30 @@ def main(a, wl):
     keys = [f"{meeting.name}-{i + 1}" for i in range(4)]
 
     def e2e():
-        p = pipe.posteriors(wav, ts, n_lab)
+        p = pipe.posteriors(job["wav"], job["ts"], job["n_lab"])
         return posteriors_to_rttm_gpu(keys, p) if rank == 0 else None
     e2e()
     t_e2e, _, _ = median3(e2e)
 
     kernels = None if a.no_kernel_timing else live_kernels(step)
 
-    cpu, der = None, None
+    cpu, der, parity = None, None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu, cpu_post, n_cpu = cpu_baseline(cfg, sd_np, meeting, ts_np, a.cpu_seconds)
+        cpu, cpu_post, n_cpu = cpu_baseline(job["cfg"], job["sd_np"], meeting, job["ts_np"], a.cpu_seconds)
         der = der_parity(meeting, post, cpu_post, float(n_cpu))
+        parity = posterior_parity(post.cpu().numpy(), cpu_post, n_cpu * 25)
+    c4 = None
+    if world == 1 and a.workload == "c2" and not a.no_c4_ref:
+        c4 = c4_reference(a, dev)
 
     if rank == 0:
-        plan = pipe.plan(n_lab)
+        plan = pipe.plan(job["n_lab"])
         line = {
             "metric": "diarized frames/sec (10 ms hop)",
             "value": round(value, 1),
             "unit": "frames/s",
             "n_gpus": world,
+            "rccl_ranks": joined if world > 1 else None,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -405,8 +556,12 @@ def main(a, wl):
                            "what": "wav in HBM -> posteriors -> GPU medfilt/threshold/run-length -> RTTM lines "
                                    "(10 thresholds), median of 3"},
         }
+        if c4 is not None:
+            line["c4_60min_ms"] = c4["ms_per_step"]
+            line["c4_60min"] = c4
         line.update(kernel_report(kernels, a.workload, ms_per_step, a.precision))
         line["cpu_baseline"] = cpu
+        line["parity"] = parity
         line["der"] = der
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
@@ -748,6 +903,17 @@ def main_stream(a, wl):
 
 if __name__ == "__main__":
     _a = parse()
+    if _a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: start the N ranks here (this process never touches the GPU)
+        sys.exit(launch_ranks(_a.gpus, sys.argv[1:]))
+    _world = int(os.environ.get("WORLD_SIZE", "1"))
+    if _world != _a.gpus:
+        print(f"[bench] --gpus {_a.gpus} but the launcher started {_world} ranks; using {_world}", file=sys.stderr)
+    if _a.workload is None:
+        _a.workload = "c4" if _world > 1 else "c2"
+    if _a.workload == "dist_check":
+        main_dist_check(_a)
+        sys.exit(0)
     _wl = WORKLOADS[_a.workload]
     if _wl.get("kind") == "fseend_stream":
         main_stream(_a, _wl)

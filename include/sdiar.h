@@ -74,6 +74,11 @@ int sd_tsvad_finalize(sd_tsvad* h);
  * logits: device (B, max_num_speaker, T_label) — pre-sigmoid, like forward(). */
 int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_speech, int B,
                      int T_fbank, int T_label, float* logits, void* stream);
+/* Waits for `stream` and returns SD_ERR_HIP if the ots_vad BiLSTM's persistent recurrence of a
+ * forward enqueued on it lost workgroup co-residency (its logits are NaN).  The Python mirror
+ * calls it after forward(), so the failing forward itself raises (RuntimeError); an
+ * uncollected report is raised by the handle's next forward at the latest. */
+int sd_tsvad_status(sd_tsvad* h, void* stream);
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 int sd_tsvad_destroy(sd_tsvad* h);
 
@@ -225,6 +230,8 @@ int sd_eda_input_stride(const sd_eda* h);
  * act: device (S, T, max_n_speakers - 1) = sigmoid(emb · attractors[:-1]ᵀ). */
 int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S, int T, const int* lengths,
                    const int* key_len, const int* perm, float* probs, float* act, void* stream);
+/* As sd_tsvad_status for the EDA encoder / decoder LSTMs (encoder_decoder_attractor.py:19-59). */
+int sd_eda_status(sd_eda* h, void* stream);
 int64_t sd_eda_device_bytes(const sd_eda* h);
 int sd_eda_destroy(sd_eda* h);
 

@@ -117,6 +117,7 @@ _SIGS = {
     "sd_tsvad_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_tsvad_finalize": (c_int, [c_void_p]),
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sd_tsvad_status": (c_int, [c_void_p, c_void_p]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
     "sd_tsvad_stream_create": (c_int, [POINTER(TsvadStreamConfig), POINTER(c_void_p)]),
@@ -145,6 +146,7 @@ _SIGS = {
     "sd_eda_input_stride": (c_int, [c_void_p]),
     "sd_eda_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
+    "sd_eda_status": (c_int, [c_void_p, c_void_p]),
     "sd_eda_device_bytes": (c_int64, [c_void_p]),
     "sd_eda_destroy": (c_int, [c_void_p]),
     "sd_fseend_create": (c_int, [POINTER(FseendConfig), POINTER(c_void_p)]),

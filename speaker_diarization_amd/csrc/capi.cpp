@@ -159,6 +159,13 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref, const float* ts, int B, int 
   });
 }
 
+int sd_tsvad_status(sd_tsvad* h, void* stream) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null argument");
+    h->model->status(S(stream));
+  });
+}
+
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h) { return h ? (int64_t)h->model->device_bytes() : 0; }
 
 int sd_tsvad_destroy(sd_tsvad* h) {
@@ -215,6 +222,13 @@ int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S_, int T, c
   return guard([&] {
     SD_CHECK(h && feats && act, sd::kErrInvalid, "null argument");
     h->model->forward(feats, ld_feats, S_, T, lengths, key_len, perm, probs, act, S(stream));
+  });
+}
+
+int sd_eda_status(sd_eda* h, void* stream) {
+  return guard([&] {
+    SD_CHECK(h, sd::kErrInvalid, "null argument");
+    h->model->status(S(stream));
   });
 }
 
@@ -552,6 +566,8 @@ int sd_overlap_average(const float* logits, int n_win, int NS, int Tw, const int
                        const int* len, int dis, int chunk, int n_frames, float* out, void* stream) {
   return guard([&] {
     SD_CHECK(dis > 0 && chunk > 0, sd::kErrInvalid, "overlap_average: bad window geometry");
+    SD_CHECK((chunk + dis - 1) / dis <= sd::kOverlapMaxWindows, sd::kErrInvalid,
+             "overlap_average: more covering windows per frame than the pairwise mean supports");
     sd::overlap_average(logits, n_win, NS, Tw, start, len, dis, chunk, n_frames, out, S(stream));
   });
 }
@@ -560,6 +576,8 @@ int sd_overlap_mean(const float* probs, int n_win, int NS, int Tw, const int* st
                     int chunk, int n_frames, float* out, void* stream) {
   return guard([&] {
     SD_CHECK(dis > 0 && chunk > 0, sd::kErrInvalid, "overlap_mean: bad window geometry");
+    SD_CHECK((chunk + dis - 1) / dis <= sd::kOverlapMaxWindows, sd::kErrInvalid,
+             "overlap_mean: more covering windows per frame than the pairwise mean supports");
     sd::overlap_average(probs, n_win, NS, Tw, start, len, dis, chunk, n_frames, out, S(stream), false);
   });
 }

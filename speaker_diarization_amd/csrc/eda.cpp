@@ -96,6 +96,7 @@ void EdaModel::finalize() {
 void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* lengths, const int* key_len,
                        const int* perm, float* probs, float* act, hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
+  lstm_err_.raise_if_set();   // an earlier forward's report nobody collected with sd_eda_status
   SD_CHECK(S >= 1 && S <= cfg_.max_seqs, kErrInvalid, "sequences exceed max_seqs");
   SD_CHECK(T >= 1 && T <= cfg_.max_frames, kErrInvalid, "frames exceed max_frames");
   SD_CHECK(ld_in >= in_ld_ && ld_in % 4 == 0, kErrInvalid, "feature row stride must be >= in_ld and % 4");
@@ -103,7 +104,9 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   SD_CHECK(plain || (lengths && perm), kErrInvalid, "lengths and perm are required");
   const int E = cfg_.n_units, rows = S * T, NA = cfg_.max_n_speakers;
   const bool bf = cfg_.bf16;
-  const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf, true};   // replicas only: split-K allowed
+  // No split-K: its split count depends on the batched M (chunks per forward x T), and EDA chunks are
+  // sharded over ranks with activities bit-identical for any world size (test_eda_chunk_shards_bit_identical).
+  const EncoderWork w{Y_, QKV_, AO_, H_, partial_, bf, false};
   // Linear + LayerNorm
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, E), bf, st);
   layernorm(Y_, rows, E, E, norm_g_, norm_b_, 1e-5f, X_, E, false, st);
@@ -119,10 +122,10 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   gather_rows(X_, S, T, E, perm, lengths, Y_, st);
   conv_gemm(lin(Tens{Y_, false}, rows, E, enc_ih_, enc_b_, Tens{G_, false}, 4 * E), bf, st);
   lstm_recurrence(G_, S, T, E, 1, enc_hh_, lengths, nullptr, nullptr, nullptr, 0, hT_, cT_, lstm_work_, st,
-                  enc_hh_bf_, lstm_err_.get());
+                  enc_hh_bf_, lstm_err_.get(0));
   fill_rows(dec_b_, 4 * E, S * NA, Gd_, st);
   lstm_recurrence(Gd_, S, NA, E, 1, dec_hh_, nullptr, hT_, cT_, att_, E, nullptr, nullptr, lstm_work_, st,
-                  dec_hh_bf_, lstm_err_.get());
+                  dec_hh_bf_, lstm_err_.get(1));
   attractor_scores(X_, S, T, E, att_, NA, lin_w_, lin_b_, probs, act, st);
 }
 

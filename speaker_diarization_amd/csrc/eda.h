@@ -37,6 +37,8 @@ class EdaModel {
                const int* perm, float* probs, float* act, hipStream_t st);
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
+  // waits for `st` and raises kErrHip if a persistent LSTM of the forwards enqueued on it timed out
+  void status(hipStream_t st) { SD_HIP(hipStreamSynchronize(st)); lstm_err_.raise_if_set(); }
 
  private:
   float* ws(size_t n) { return static_cast<float*>(arena_.alloc(n * sizeof(float))); }
@@ -44,7 +46,7 @@ class EdaModel {
   EdaConfig cfg_;
   ParamStore ps_;
   DeviceArena arena_;
-  PinnedFlag lstm_err_;   // deferred poll-timeout report of the persistent LSTM (lstm.hip)
+  PinnedFlags lstm_err_;   // poll-timeout reports of the persistent LSTMs (lstm.hip), one slot each
   bool finalized_ = false;
   int in_ld_ = 352;
 

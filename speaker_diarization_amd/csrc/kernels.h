@@ -330,9 +330,10 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 // whh_bf16 (optional, same layout in bf16 bits): bf16-MFMA recurrence (bf16 mode); the
 // cell state, gates and h stay fp32, h is rounded to bf16 only as the MFMA operand.
 // work: per-handle device scratch of lstm_work_floats(B, H, ndir) floats (the persistent bf16
-// kernel keeps its h exchange and counters there).  host_err (optional, pinned, per handle):
-// receives a stream-ordered copy of the persistent kernel's poll-timeout flag; a set flag is
-// reported (kErrHip) by the next call on that handle.
+// kernel keeps its h exchange and counters there).  host_err (optional, a pinned slot of the handle's
+// PinnedFlags, one per recurrence of a forward): receives a stream-ordered copy of the persistent
+// kernel's poll-timeout flag; the handle raises kErrHip for a set slot once the stream has completed
+// (sd_tsvad_status / sd_eda_status after the forward), or at the latest on its next call.
 int64_t lstm_work_floats(int B, int H, int ndir);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
@@ -360,7 +361,10 @@ void pack_weight(const float* w, int N, int Cin, int taps, void* out, bool bf16,
 }  // namespace sd
 
 namespace sd {
-// sigmoid=false: inputs are probabilities already (sd_overlap_mean).
+// sigmoid=false: inputs are probabilities already (sd_overlap_mean).  numpy's pairwise
+// summation is reproduced for up to kOverlapMaxWindows covering windows per frame.
+constexpr int kOverlapMaxDepth = 6;
+constexpr int kOverlapMaxWindows = (128 << kOverlapMaxDepth) / 2;
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,
                      int dis, int chunk, int n_frames, float* out, hipStream_t st, bool sigmoid = true);
 

@@ -211,19 +211,13 @@ constexpr int LS_WS = LS_H + 16;     // bf16 LDS row stride of the W slice (conf
 constexpr int LS_MAXMT = 6;
 constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (256 B: own L2 line)
 
-// TAG (MT <= 2): the hand-off without counters.  Every exchanged word is (step tag << 16) | bf16 h, so a
-// consumer knows a value is current from the value itself: the producer's write-through stores go out with no
-// vmcnt drain, barrier or counter add, and each consumer wave re-loads (sc1) its h words until every tag
-// matches — one L2 round trip per step instead of store-ack + barrier + atomic + poll + barrier + load.
-// Double buffering by step parity keeps a fast producer from overwriting words a slow consumer still needs
-// (it cannot publish h_{s+1} before every quarter published h_s, i.e. finished reading h_{s-1}).  The tags
-// start at 1 and the exchange buffer is zeroed before each launch; T < 65535.
-template <int MT, bool TAG>
+template <int MT>
 __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
     float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
-    uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err) {
+    uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err,
+    unsigned spin_limit) {
   constexpr int H = LS_H, BB = 16 * MT;
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -246,8 +240,8 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
           *reinterpret_cast<const uint4*>(wd + (int64_t)(gate * H + 64 * q + j) * H + k8);
     }
   }
-  // h exchange: hx[parity][d][Bp][H] bf16 (TAG: uint32 words); h_t lives in parity (t + 1) & 1, h_{-1} in 0.
-  constexpr int EB = TAG ? 4 : 2;   // bytes per exchanged value
+  // h exchange: hx[parity][d][Bp][H] bf16; h_t lives in parity (t + 1) & 1, h_{-1} in 0.
+  constexpr int EB = 2;   // bytes per exchanged value
   const int64_t plane = (int64_t)ndir * Bp * H;
   const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * EB), 0x00020000);
   auto hx_off = [&](int parity, int b, int u) {   // byte offset
@@ -270,17 +264,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   for (int b = b0; b < min(B, b0 + BB); ++b) max_len = max(max_len, lengths ? lengths[b] : T);
 
   // Publish this workgroup's slice of h (rows b0.., units ub..ub+3 per lane), then count.
-  auto publish = [&](int parity, unsigned tag) {
-    if constexpr (TAG) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        u32x4_t v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (tag << 16) | (pack_bf16x2(hr[mt][r], 0.f) & 0xffffu);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rh, hx_off(parity, b0 + mt * 16 + l15, ub), 0, 16);   // sc1
-      }
-      return;
-    }
+  auto publish = [&](int parity) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
@@ -294,21 +278,23 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     if (tid == 0) {
       unsigned spins = 0;
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        // A peer that never arrives (broken co-residency) must not hang the GPU: give up
-        // after ~0.1 s, and once any workgroup gave up, every later wait returns at once.
-        if ((++spins & 1023) == 0 && (spins > (1u << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+        // A peer that never arrives (broken co-residency) must not hang the GPU: give up after
+        // spin_limit polls (default 2^22, ~0.1 s), and once any workgroup gave up, every later wait
+        // returns at once.
+        if (spins >= spin_limit ||
+            ((spins & 1023) == 1023 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
+        ++spins;
+        __builtin_amdgcn_s_sleep(1);
       }
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the poll
   };
 
-  publish(0, 1u);   // h_{-1}
+  publish(0);   // h_{-1}
   for (int step = 0; step < max_len; ++step) {
     // gx of this step for the lane's rows: 4 gates x 4 units (float4), issued before the wait.
     float4 gxv[MT][4];
@@ -328,87 +314,21 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // TAG: the wave's h words of h_{step-1} (tag step + 1), re-loaded until every tag is current
-    u32x4_t hw[TAG ? MT : 1][TAG ? H / 32 : 1][2];
-    if constexpr (TAG) {
-      const unsigned want = (unsigned)(step + 1) & 0xffffu;
-      unsigned spins = 0;
-      // cheap poll first: lane j < 16 watches one word of producer wave j (unit 16j of row b0); the full
-      // load + per-word check below then usually succeeds at once (polling all words congests L2)
-      for (;;) {
-        asm volatile("" ::: "memory");
-        bool seen = true;
-        if (lane < 16) {
-          const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rh, hx_off(pin, b0, 16 * lane), 0, 16);
-          seen = (x[0] >> 16) == want;
-        }
-        if (__all(seen)) break;
-        if ((++spins & 255) == 0 && (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_AGENT))) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      for (;;) {
-        asm volatile("" ::: "memory");   // the words change under us: no load may be hoisted out of the spin
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int kc = 0; kc < H / 32; ++kc)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh)
-              hw[mt][kc][hh] = __builtin_amdgcn_raw_buffer_load_b128(
-                  rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g + 4 * hh), 0, 16);
-        bool ok = true;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int kc = 0; kc < H / 32; ++kc)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ok = ok && (hw[mt][kc][hh][r] >> 16) == want;
-        if (__all(ok)) break;
-        if ((++spins & 255) == 0 && (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_AGENT))) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    } else {
-      wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
-    }
-    // counter mode: every h fragment of the step requested at once (one L2 round trip, not one per k-step;
+    wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
+    // every h fragment of the step requested at once (one L2 round trip, not one per k-step;
     // s_memtime stamps: 5.1 k of a 10 k-cycle C1 step went to eight serial load -> MFMA waits)
-    bf16x8 hfa[TAG ? 1 : MT][TAG ? 1 : H / 32];
-    if constexpr (!TAG) {
+    bf16x8 hfa[MT][H / 32];
 #pragma unroll
-      for (int kc = 0; kc < H / 32; ++kc)
+    for (int kc = 0; kc < H / 32; ++kc)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g), 0, 16));
-    }
+      for (int mt = 0; mt < MT; ++mt)
+        hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g), 0, 16));
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        if constexpr (TAG) {
-          const int kc = k0 / 32;
-          u32x4_t x;   // bf16 units k0 + 8g + 0..7 from the low halves (the shift drops the tag)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-              x[2 * hh + r] = (hw[mt][kc][hh][2 * r] & 0xffffu) | (hw[mt][kc][hh][2 * r + 1] << 16);
-          hf[mt] = __builtin_bit_cast(bf16x8, x);
-        } else {
-          hf[mt] = hfa[mt][k0 / 32];
-        }
-      }
+      for (int mt = 0; mt < MT; ++mt) hf[mt] = hfa[mt][k0 / 32];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) {
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
@@ -443,7 +363,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
         *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) =
             make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
     }
-    publish((step + 1) & 1, (unsigned)(step + 2) & 0xffffu);   // h_step
+    publish((step + 1) & 1);   // h_step
   }
   // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
   // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
@@ -466,21 +386,30 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   }
 }
 
-template <int MT, bool TAG = false>
+// Poll bound of the persistent kernel's waits: 2^22 polls (~0.1 s).  SDIAR_LSTM_SPIN_LIMIT (tests only)
+// shrinks it so a test can force the co-residency-lost path and check that it is reported.
+unsigned lstm_spin_limit() {
+  static const unsigned v = getenv("SDIAR_LSTM_SPIN_LIMIT") ? (unsigned)strtoul(getenv("SDIAR_LSTM_SPIN_LIMIT"), nullptr, 10)
+                                                           : (1u << 22);
+  return v;
+}
+
+template <int MT>
 void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                        const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                        uint16_t* hx, int Bp, unsigned* counters, int* err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, TAG>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, TAG>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
+  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
-                     counters, err);
+                     counters, err, lstm_spin_limit());
+  SD_LAUNCH_CHECK();
 }
 
 // Workgroups of lstm_group_bf16_kernel<MT> the occupancy query admits per CU (0 if none fit).
@@ -492,17 +421,10 @@ int lstm_group_blocks_per_cu() {
   static int nb = -1;
   if (nb < 0) {
     const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, false>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int v = 0;
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, false>, 256, smem));
-    if (MT <= 2) {   // the tagged variant must fit as well
-      SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT <= 2 ? MT : 1, true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      int vt = 0;
-      SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&vt, lstm_group_bf16_kernel<MT <= 2 ? MT : 1, true>, 256, smem));
-      v = std::min(v, vt);
-    }
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT>, 256, smem));
     nb = v;
   }
   return nb;
@@ -536,8 +458,7 @@ int lstm_group_mt(int B, int ndir) {
 
 // Layout of the persistent kernel's scratch inside the caller's `work`: the double-buffered bf16
 // h exchange, then (16-B aligned) one counter per group and the err word.
-// sized for the tagged exchange (4 B per value; the counter protocol uses the first half)
-size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 4 + 15) / 16 * 16; }
+size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
 
 }  // namespace
 
@@ -556,14 +477,6 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16, int* host_err) {
   SD_CHECK(H % 32 == 0, kErrInvalid, "lstm: H must be a multiple of 32");
   static const bool no_seq = getenv("SDIAR_NO_LSTM_SEQ") != nullptr;
-  if (host_err) {
-    // Deferred report of an earlier launch on this handle whose bounded polls timed out (its
-    // outputs were poisoned with NaN); the flag is the stream-ordered copy of its err word.
-    const int prev = __atomic_load_n(host_err, __ATOMIC_ACQUIRE);
-    __atomic_store_n(host_err, 0, __ATOMIC_RELEASE);
-    SD_CHECK(prev == 0, kErrHip, "lstm: a previous persistent LSTM launch lost workgroup co-residency "
-                                 "(its outputs were poisoned with NaN)");
-  }
   if (whh_bf16 && H == LS_H && !no_seq && (ldo % 4 == 0 || !out)) {
     const int mt = lstm_group_mt(B, ndir);
     if (mt) {
@@ -578,16 +491,10 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       uint16_t* hx = reinterpret_cast<uint16_t*>(work);
       unsigned* ctl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + hx_bytes);
       SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
-      // the tagged hand-off is opt-in (SDIAR_LSTM_TAG=1): measured slower than the counter (C1 11.0 vs 8.7 ms)
-      static const bool want_tag = getenv("SDIAR_LSTM_TAG") && atoi(getenv("SDIAR_LSTM_TAG")) == 1;
-      const bool tag = want_tag && mt <= 2 && T < 65000;
-      if (tag) SD_HIP(hipMemsetAsync(hx, 0, hx_bytes, st));   // no stale tag may match
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       int* err = reinterpret_cast<int*>(ctl + (size_t)groups * LS_CNT_STRIDE);
-      if (tag && mt == 1) launch_lstm_group<1, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
-      else if (tag) launch_lstm_group<2, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st);
-      else switch (mt) {
+      switch (mt) {
         case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         case 3: launch_lstm_group<3>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
@@ -595,6 +502,8 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
         case 5: launch_lstm_group<5>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
         default: launch_lstm_group<6>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
       }
+      // stream-ordered copy of the err word into this recurrence's own pinned slot; the handle reads
+      // it after the forward's stream completes (sd_*_status) or, at the latest, on its next call
       if (host_err) SD_HIP(hipMemcpyAsync(host_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
       return;
     }

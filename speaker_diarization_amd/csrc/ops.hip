@@ -1017,9 +1017,78 @@ namespace sd {
 // windows covering a frame, in window order) with the sigmoid of model.py:945-946
 // fused.  logits: (n_win, NS, Tw); window w covers label frames
 // [start_w, start_w + len_w).  out: (NS, n_frames); frames no window covers -> NaN.
-// np.mean semantics (infer.py:90-94 over float32 lists): float32 sum from 0 in window order, then
-// one correctly rounded float32 division (hipcc keeps fp32 '/' IEEE by default) — bit-identical
-// to numpy for the same probabilities.  No FMA can form (adds only).
+//
+// np.mean over a float32 list is numpy's float32 add.reduce followed by one correctly rounded
+// float32 division.  The reduction is numpy's pairwise summation (umath loops, pairwise_sum):
+// n < 8 values are summed from 0 in order; 8 <= n <= 128 go into 8 accumulators r[j] = v[j],
+// r[j] += v[i + j] for each full group of 8, combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
+// then the n % 8 tail is added in order; n > 128 splits at n2 = n/2 rounded down to a multiple
+// of 8 and adds the two halves' sums.  Reproduced exactly (adds only, __fadd_rn: no FMA can
+// form), so the result is bit-identical to numpy for the same probabilities.
+struct OverlapList {     // the covering windows of one (frame, speaker), in window order
+  const float* logits;
+  const int* start;
+  const int* len;
+  int64_t stride;        // NS * Tw
+  int64_t base;          // spk * Tw + t
+  int t, w_lo, w_hi;
+  int first;             // first covering window
+  bool contiguous;       // covering windows form [first, first + n)
+};
+
+template <bool kSigmoid>
+__device__ __forceinline__ float ol_value(const OverlapList& L, int w) {
+  const float x = L.logits[(int64_t)w * L.stride + L.base - L.start[w]];
+  return kSigmoid ? 1.f / (1.f + expf(-x)) : x;
+}
+
+template <bool kSigmoid>
+__device__ __forceinline__ float ol_at(const OverlapList& L, int k) {   // k-th covering value
+  if (L.contiguous) return ol_value<kSigmoid>(L, L.first + k);
+  for (int w = L.first; w <= L.w_hi; ++w) {
+    const int off = L.t - L.start[w];
+    if (off < 0 || off >= L.len[w]) continue;
+    if (k-- == 0) return ol_value<kSigmoid>(L, w);
+  }
+  return 0.f;
+}
+
+template <bool kSigmoid>
+__device__ float ol_block_sum(const OverlapList& L, int k0, int n) {     // n <= 128
+  if (n < 8) {
+    float s = 0.f;
+    for (int k = 0; k < n; ++k) s = __fadd_rn(s, ol_at<kSigmoid>(L, k0 + k));
+    return s;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = ol_at<kSigmoid>(L, k0 + j);
+  int k = 8;
+  for (; k < n - (n % 8); k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], ol_at<kSigmoid>(L, k0 + k + j));
+  }
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                      __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+  for (; k < n; ++k) s = __fadd_rn(s, ol_at<kSigmoid>(L, k0 + k));
+  return s;
+}
+
+// numpy's recursion for n > 128, unrolled by depth (kDepth levels cover n <= 128 << kDepth;
+// the host rejects geometries with more windows per frame than that).
+template <bool kSigmoid, int kDepth>
+__device__ __attribute__((noinline)) float ol_pairwise(const OverlapList& L, int k0, int n) {
+  if constexpr (kDepth == 0) {
+    return ol_block_sum<kSigmoid>(L, k0, n);
+  } else {
+    if (n <= 128) return ol_block_sum<kSigmoid>(L, k0, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return __fadd_rn(ol_pairwise<kSigmoid, kDepth - 1>(L, k0, n2),
+                     ol_pairwise<kSigmoid, kDepth - 1>(L, k0 + n2, n - n2));
+  }
+}
+
 template <bool kSigmoid>
 __global__ void overlap_average_kernel(const float* __restrict__ logits, int n_win, int NS, int Tw,
                                        const int* __restrict__ start, const int* __restrict__ len,
@@ -1030,17 +1099,24 @@ __global__ void overlap_average_kernel(const float* __restrict__ logits, int n_w
   const int spk = i / n_frames;
   int w_lo = (t - chunk + 1 + dis - 1);
   w_lo = w_lo > 0 ? w_lo / dis : 0;
-  int w_hi = min(n_win - 1, t / dis);
-  float acc = 0.f;
-  int cnt = 0;
+  const int w_hi = min(n_win - 1, t / dis);
+  int cnt = 0, first = -1, last = -1;
   for (int w = w_lo; w <= w_hi; ++w) {
-    int off = t - start[w];
+    const int off = t - start[w];
     if (off < 0 || off >= len[w]) continue;
-    const float x = logits[((int64_t)w * NS + spk) * Tw + off];
-    acc = __fadd_rn(acc, kSigmoid ? 1.f / (1.f + expf(-x)) : x);
+    if (first < 0) first = w;
+    last = w;
     ++cnt;
   }
-  out[i] = cnt ? __fdiv_rn(acc, (float)cnt) : __int_as_float(0x7fc00000);
+  if (cnt == 0) {
+    out[i] = __int_as_float(0x7fc00000);
+    return;
+  }
+  OverlapList L{logits, start, len, (int64_t)NS * Tw, (int64_t)spk * Tw + t, t, w_lo, w_hi, first,
+                last - first + 1 == cnt};
+  const float s = cnt <= 128 ? ol_block_sum<kSigmoid>(L, 0, cnt)
+                             : ol_pairwise<kSigmoid, kOverlapMaxDepth>(L, 0, cnt);
+  out[i] = __fdiv_rn(s, (float)cnt);
 }
 
 void overlap_average(const float* logits, int n_win, int NS, int Tw, const int* start, const int* len,

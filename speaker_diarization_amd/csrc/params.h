@@ -44,15 +44,30 @@ class DeviceArena {
   size_t total_ = 0;
 };
 
-// Pinned host int per handle: the target of a stream-ordered device->host copy of a device-side
-// failure flag (the persistent LSTM's poll timeout), read back on the handle's next call.
-class PinnedFlag {
+// Pinned host ints per handle, one slot per device-side failure flag of a forward (each persistent
+// LSTM recurrence copies its poll-timeout word into its own slot, stream-ordered).  take() reads and
+// clears every slot: callers use it once the stream has completed (the same call) or on the next call.
+class PinnedFlags {
  public:
-  PinnedFlag() { SD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), sizeof(int), hipHostMallocDefault)); *p_ = 0; }
-  ~PinnedFlag() { if (p_) (void)hipHostFree(p_); }
-  PinnedFlag(const PinnedFlag&) = delete;
-  PinnedFlag& operator=(const PinnedFlag&) = delete;
-  int* get() const { return p_; }
+  static constexpr int kSlots = 4;
+  PinnedFlags() {
+    SD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), kSlots * sizeof(int), hipHostMallocDefault));
+    for (int i = 0; i < kSlots; ++i) p_[i] = 0;
+  }
+  ~PinnedFlags() { if (p_) (void)hipHostFree(p_); }
+  PinnedFlags(const PinnedFlags&) = delete;
+  PinnedFlags& operator=(const PinnedFlags&) = delete;
+  int* get(int slot) const { return p_ + slot; }
+  int take() {
+    int any = 0;
+    for (int i = 0; i < kSlots; ++i) any |= __atomic_exchange_n(p_ + i, 0, __ATOMIC_ACQ_REL);
+    return any;
+  }
+  // kErrHip if a recurrence of an earlier launch on the handle timed out (its outputs are NaN)
+  void raise_if_set() {
+    SD_CHECK(take() == 0, kErrHip, "lstm: a persistent LSTM launch lost workgroup co-residency "
+                                   "(its outputs were poisoned with NaN)");
+  }
 
  private:
   int* p_ = nullptr;

@@ -116,18 +116,13 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
+  // an earlier forward's LSTM report nobody collected with sd_tsvad_status (a replayed graph repeats
+  // only the stream-ordered copy of the err word, so the host-side check lives here)
+  lstm_err_.raise_if_set();
   static const bool no_graph = getenv("SDIAR_NO_GRAPH") && atoi(getenv("SDIAR_NO_GRAPH")) == 1;
   if (no_graph || prof_enabled()) {
     forward_body(ref, ts, B, Tf, Tl, logits, st);
     return;
-  }
-  // Host-side part of the persistent LSTM's deferred error report (lstm_recurrence does the same on a
-  // direct run; a replayed graph only repeats the stream-ordered copy of the err word).
-  {
-    const int prev = __atomic_load_n(lstm_err_.get(), __ATOMIC_ACQUIRE);
-    __atomic_store_n(lstm_err_.get(), 0, __ATOMIC_RELEASE);
-    SD_CHECK(prev == 0, kErrHip, "lstm: a previous persistent LSTM launch lost workgroup co-residency "
-                                 "(its outputs were poisoned with NaN)");
   }
   GraphEntry* e = nullptr;
   for (GraphEntry& g : graphs_)
@@ -211,7 +206,7 @@ void TsvadModel::forward_body(const float* ref, const float* ts, int B, int Tf, 
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
-                    nullptr, lstm_work_, st, lstm_hh_bf_, lstm_err_.get());
+                    nullptr, lstm_work_, st, lstm_hh_bf_, lstm_err_.get(0));
     ConvGemmArgs f = cam_conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);

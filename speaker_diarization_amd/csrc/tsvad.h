@@ -34,6 +34,8 @@ class TsvadModel {
                float* logits, hipStream_t st);
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
+  // waits for `st` and raises kErrHip if a persistent LSTM of the forwards enqueued on it timed out
+  void status(hipStream_t st) { SD_HIP(hipStreamSynchronize(st)); lstm_err_.raise_if_set(); }
   ~TsvadModel();
 
  private:
@@ -61,7 +63,7 @@ class TsvadModel {
   TsvadConfig cfg_;
   ParamStore ps_;
   DeviceArena arena_;
-  PinnedFlag lstm_err_;   // deferred poll-timeout report of the persistent LSTM (lstm.hip)
+  PinnedFlags lstm_err_;   // poll-timeout reports of the persistent LSTMs (lstm.hip), one slot each
   bool finalized_ = false;
 
   CamTrunk cam_;     // speech_encoder.* (CAM++ get_time_out=True)

@@ -82,9 +82,11 @@ def chunk_activities(model, feats, args: EdaInferArgs, perms, c0: int = 0, c1: O
         x = feats[s0: s0 + (g1 - g0) * T].view(g1 - g0, T, feats.shape[1])
         key_len = [T] * (g1 - g0) if model.cfg.variant == 2 else None
         a, p = model.forward_infer(x, [T] * (g1 - g0), perms[c0 + g0: c0 + g1], args.max_n_speakers,
-                                   key_len=key_len)
+                                   key_len=key_len, check=False)
         acts.extend(a[i] for i in range(g1 - g0))
         probs.append(p)
+    if sub:
+        model.status()        # one wait for every group: a lost LSTM co-residency raises here
     return acts, (torch.cat(probs).cpu() if probs else torch.zeros(0, args.max_n_speakers))
 
 

@@ -135,10 +135,12 @@ class _EdaBase:
 
     # ------------------------------------------------------------------ forward
     def forward_infer(self, feats, lengths: List[int], perms, max_n_speakers: int = 15,
-                      key_len: Optional[List[int]] = None, act=None, probs=None):
+                      key_len: Optional[List[int]] = None, act=None, probs=None, check: bool = True):
         """Device-level forward of S equal-stride sequences.
         feats: CUDA (S, T, ld>=in_ld) f32; perms: list of S int tensors (randperm(lengths[s])).
-        Returns (act (S, T, max_n-1), probs (S, max_n)) CUDA f32."""
+        Returns (act (S, T, max_n-1), probs (S, max_n)) CUDA f32.  check: wait for the stream and
+        raise RuntimeError here if an EDA LSTM recurrence lost co-residency (its outputs are NaN);
+        check=False leaves that to a later status() (batched callers check once)."""
         import torch
         if self._h is None:
             raise RuntimeError("load_state_dict() must be called before infer()")
@@ -163,7 +165,14 @@ class _EdaBase:
         _lib.call("sd_eda_forward", self._h, _lib.ptr(feats), ld, S, T, _lib.ptr(len_d),
                   _lib.ptr(kl_d) if kl_d is not None else None, _lib.ptr(perm_d), _lib.ptr(probs), _lib.ptr(act),
                   _lib.stream_ptr(dev))
+        if check:
+            self.status()
         return act, probs
+
+    def status(self):
+        """sd_eda_status: wait for the device stream, raise RuntimeError if a persistent LSTM
+        recurrence of the forwards enqueued so far timed out."""
+        _lib.call("sd_eda_status", self._h, _lib.stream_ptr(self.device))
 
     def _pad_src(self, src):
         """pad_sequence(src, padding_value=-1, batch_first=True) into in_ld-wide rows."""

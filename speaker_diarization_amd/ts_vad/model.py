@@ -91,9 +91,11 @@ class TSVADModel:
         return int(_lib.load().sd_tsvad_device_bytes(self._h))
 
     # ------------------------------------------------------------------ forward
-    def forward(self, ref_speech, target_speech, labels, num_updates: int = 0, out=None):
+    def forward(self, ref_speech, target_speech, labels, num_updates: int = 0, out=None, check: bool = True):
         """ref_speech (B, T_fb, 80), target_speech (B, NS, 192), labels (B, NS, T) (only
-        labels.size(-1) is read, model.py:681/770) -> logits (B, NS, T)."""
+        labels.size(-1) is read, model.py:681/770) -> logits (B, NS, T).  check: wait for the
+        stream and raise RuntimeError in this call if the BiLSTM's persistent recurrence lost
+        co-residency (its logits are NaN); check=False defers that to status()."""
         import torch
         B, T_fb, F = ref_speech.shape
         T_lab = labels if isinstance(labels, int) else labels.size(-1)
@@ -106,11 +108,20 @@ class TSVADModel:
         if B > self.max_batch:
             for s in range(0, B, self.max_batch):
                 e = min(B, s + self.max_batch)
-                self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e])
+                self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False)
+            if check:
+                self.status()
             return out
         _lib.call("sd_tsvad_forward", self._h, _lib.ptr(ref), _lib.ptr(ts), B, T_fb, T_lab, _lib.ptr(out),
                   _lib.stream_ptr(self.device))
+        if check:
+            self.status()
         return out
+
+    def status(self):
+        """sd_tsvad_status: wait for the device stream, raise RuntimeError if a persistent LSTM
+        recurrence of the forwards enqueued so far timed out."""
+        _lib.call("sd_tsvad_status", self._h, _lib.stream_ptr(self.device))
 
     __call__ = forward
 

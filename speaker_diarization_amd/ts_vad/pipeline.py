@@ -68,8 +68,11 @@ class TSVADPipeline:
         ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
         for b0, b1, T_out, T_lab in self.device_batches(plan, w0, w1):
             ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
-            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab)
+            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab, check=False)
             out[b0 - w0:b1 - w0, :, :T_lab] = lg
+        status = getattr(self.model, "status", None)
+        if status is not None:
+            status()          # one wait per call: a lost LSTM co-residency raises here
         return out
 
     def device_batches(self, plan: WindowPlan, w0: int, w1: int):

@@ -135,7 +135,8 @@ class StreamingWindowDecoder:
         self.device = model.device
         self.chunk, self.left = decoding_chunk_size, num_decoding_left_chunks
 
-    def forward(self, ref, ts, T_lab: int):
+    def forward(self, ref, ts, T_lab: int, check: bool = True):
+        """check: accepted for TSVADModel's signature; the streaming model has no LSTM to report."""
         import torch
         n = self.model.subsampling_rate * T_lab
         if ref.shape[1] != n:

@@ -3,7 +3,9 @@
 1. ``postprocess_*.npz`` — ``egs/alimeeting/ts_vad2/infer.py`` ``postprocess(res_dict, args)``
    (:72-163) imported from /root/reference with stubs for lhotse / tqdm / tensorboard
    (SURVEY Appendix A), run on seeded res_dicts: per-frame lists of float32 window
-   probabilities (1-6 values, so the np.mean of :90-94 is exercised), values placed exactly
+   probabilities (1-6 values, so the np.mean of :90-94 is exercised; ``postprocess_win12``: the
+   lists a 12-s window / 1-s shift plan builds, 1-12 values per frame in window order, so numpy's
+   8-accumulator pairwise summation inside np.mean is exercised too), values placed exactly
    on the float32 thresholds, 1-frame speech runs, silences of exactly min_silence // frame_len
    frames, tracks starting with speech, tracks of 1 and 22 frames (below / at the medfilt
    width) and two meetings.  Stored: the res_dict (flattened), the ten ``res_rttm_<thr>``
@@ -36,7 +38,9 @@ POSTPROCESS_CASES = {
     "postprocess_smooth": (11, 2, 4, 1500, 6),
     "postprocess_edges": (12, 1, 3, 400, 4),
     "postprocess_tiny": (13, 2, 2, 22, 3),
+    "postprocess_win12": (14, 1, 4, 1500, 12),      # window layout: rs_len 12 s, shift 1 s
 }
+WINDOW_CASES = {"postprocess_win12": (12, 1)}        # name: (rs_len s, segment_shift s)
 
 
 def _import_infer():
@@ -81,8 +85,32 @@ def _track(rng, T, kind, w_max):
     return lists
 
 
+def window_probs(name):
+    """(n_win, NS, chunk) float32 window probabilities + window starts/lens of a WINDOW_CASES
+    plan (ts_vad_dataset.py:242-271 at inference: windows every shift, partial tails kept)."""
+    seed, n_meet, n_spk, T, _ = POSTPROCESS_CASES[name]
+    rs, shift = WINDOW_CASES[name]
+    chunk, dis = 25 * rs, 25 * shift
+    starts = np.arange(0, T, dis)
+    ends = np.minimum(starts + chunk, T)
+    rng = np.random.default_rng(seed)
+    base = np.stack([1 / (1 + np.exp(-np.cumsum(rng.standard_normal(T)) * 0.25)) for _ in range(n_spk)])
+    probs = np.zeros((len(starts), n_spk, chunk), np.float32)
+    for w, (s0, e0) in enumerate(zip(starts, ends)):
+        probs[w, :, : e0 - s0] = np.clip(base[:, s0:e0] + rng.normal(0, 0.05, (n_spk, e0 - s0)), 0, 1)
+    return probs, starts.astype(np.int64), (ends - starts).astype(np.int64)
+
+
 def make_res_dict(name):
     seed, n_meet, n_spk, T, w_max = POSTPROCESS_CASES[name]
+    if name in WINDOW_CASES:        # what TSVADModel.infer appends, window by window (model.py:960-966)
+        probs, starts, lens = window_probs(name)
+        res = {f"R00_M00-{s}": [[] for _ in range(T)] for s in range(1, n_spk + 1)}
+        for w in range(len(starts)):
+            for t in range(int(lens[w])):
+                for i in range(n_spk):
+                    res[f"R00_M00-{i + 1}"][int(starts[w]) + t].append(np.float32(probs[w, i, t]))
+        return res
     rng = np.random.default_rng(seed)
     kind = "smooth" if name.endswith("smooth") else "edges"
     res = {}
@@ -143,6 +171,11 @@ def run_postprocess(name, ref_infer):
     for i in range(len(keys)):
         out[f"counts_{i}"] = counts[i]
         out[f"values_{i}"] = vals[i]
+        # np.mean of every frame's list: the function infer.py:93 calls, on the same lists
+        out[f"means_{i}"] = np.array([np.mean(v) for v in res[keys[i]]], np.float32)
+    if name in WINDOW_CASES:
+        out["win_probs"], out["win_starts"], out["win_lens"] = window_probs(name)
+        out["win_geometry"] = np.array(WINDOW_CASES[name], np.int64)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     print(name, len(keys), "tracks", [len(r.splitlines()) for r in rttms], "RTTM lines")
 

@@ -1,0 +1,75 @@
+"""A persistent LSTM recurrence that loses workgroup co-residency (lstm.hip: every poll is bounded,
+a timed-out poll poisons the outputs with NaN and sets an err word) is reported by the SAME forward
+call that ran it: the Python mirrors wait for the stream after the forward and sd_tsvad_status /
+sd_eda_status raise RuntimeError.  The timeout is forced with the test-only SDIAR_LSTM_SPIN_LIMIT=0
+(every wait gives up at its first unsuccessful poll) in a child process, since the limit is read
+once per process.  Models: the ots_vad BiLSTM (ts_vad2/model.py:360-366) and the EDA encoder /
+decoder LSTMs (encoder_decoder_attractor.py:19-59)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+TSVAD = r"""
+import sys, torch
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {repo!r} + "/tests/golden")
+from make_golden import TSVAD_CASES, tsvad_inputs
+from speaker_diarization_amd.ts_vad.model import TSVADModel
+from speaker_diarization_amd.weights import TSVADConfig, to_torch, tsvad_state_dict
+v, rs, B, T, nl, iseed, wseed = TSVAD_CASES["tsvad_v1_rs6"]
+cfg = TSVADConfig.ots_vad_v1(rs_len=rs)
+m = TSVADModel(cfg, device="cuda:0", precision="bf16", max_batch=B)
+m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=wseed)))
+x, ts = tsvad_inputs(B, T, nl, seed=iseed)
+x, ts = torch.from_numpy(x).cuda(), torch.from_numpy(ts).cuda()
+try:
+    out = m.forward(x, ts, nl)
+except RuntimeError as e:
+    print("RAISED:", e); sys.exit(0)
+print("NO-RAISE nan=%d" % int(torch.isnan(out).any())); sys.exit(1)
+"""
+
+EDA = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+from speaker_diarization_amd.eend_eda.models import EendEdaModel
+from speaker_diarization_amd.weights import EDAConfig, eda_state_dict, to_torch
+m = EendEdaModel(n_speakers=3, in_size=345, n_heads=4, n_units=256, n_layers=2, device="cuda:0",
+                 precision="bf16", max_seqs=2, max_frames=600)
+m.load_state_dict(to_torch(eda_state_dict(EDAConfig(model_type="EendEda", n_speakers=3, n_layers=2), seed=5)))
+g = torch.Generator().manual_seed(1)
+x = torch.randn(2, 600, m.in_ld, generator=g).cuda()
+perms = [torch.randperm(600, generator=g) for _ in range(2)]
+try:
+    act, probs = m.forward_infer(x, [600, 600], perms)
+except RuntimeError as e:
+    print("RAISED:", e); sys.exit(0)
+print("NO-RAISE nan=%d" % int(torch.isnan(act).any())); sys.exit(1)
+"""
+
+
+def _child(code, limit):
+    env = dict(os.environ)
+    if limit is None:
+        env.pop("SDIAR_LSTM_SPIN_LIMIT", None)
+    else:
+        env["SDIAR_LSTM_SPIN_LIMIT"] = str(limit)
+    return subprocess.run([sys.executable, "-c", code.format(repo=REPO)], capture_output=True, text=True,
+                          timeout=110, env=env)
+
+
+@pytest.mark.parametrize("name,code", [("tsvad_bilstm", TSVAD), ("eda_lstms", EDA)])
+def test_forced_lstm_timeout_raises_in_the_same_call(gpu, name, code):
+    r = _child(code, 0)
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-1500:])
+    assert "RAISED:" in r.stdout and "co-residency" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("name,code", [("tsvad_bilstm", TSVAD), ("eda_lstms", EDA)])
+def test_default_limit_does_not_raise(gpu, name, code):
+    r = _child(code, None)
+    assert r.returncode == 1 and "NO-RAISE nan=0" in r.stdout, (r.stdout[-1500:], r.stderr[-1500:])

@@ -379,10 +379,13 @@ def _np_mean_lists(prob, plan):
     return ref
 
 
-@pytest.mark.parametrize("n_lab,rs,shift", [(1000, 6, 1), (777, 4, 1), (613, 6, 2), (3, 4, 1)])
+@pytest.mark.parametrize("n_lab,rs,shift", [(1000, 6, 1), (777, 4, 1), (613, 6, 2), (3, 4, 1), (1500, 10, 1),
+                                            (901, 16, 1), (4000, 140, 1)])
 def test_overlap_mean_bit_exact(gpu, n_lab, rs, shift):
     """sd_overlap_mean == np.mean over the res_dict lists, bit for bit (values chosen to make
-    float32 rounding order matter)."""
+    float32 rounding order matter).  Up to 6 windows per frame numpy sums in order; the
+    streaming recipe's rs_len 10 (10 per frame), 16 and 140 (numpy's > 128 split) exercise its
+    pairwise summation."""
     from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
     from speaker_diarization_amd.ts_vad.windows import plan_windows
     plan = plan_windows(n_lab, rs, shift)

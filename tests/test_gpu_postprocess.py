@@ -95,7 +95,8 @@ def test_eend_make_rttm(gpu, T, nspk, median, thr):
     assert got == want
 
 
-@pytest.mark.parametrize("name", ["postprocess_smooth", "postprocess_edges", "postprocess_tiny"])
+@pytest.mark.parametrize("name", ["postprocess_smooth", "postprocess_edges", "postprocess_tiny",
+                                  "postprocess_win12"])
 def test_gpu_writer_matches_reference_run(gpu, name):
     """posteriors_to_rttm_gpu (medfilt + thresholds + run-length filters on the GPU) reproduces
     the res_rttm_<thr> files the reference's own infer.postprocess wrote (make_postprocess_golden.py),
@@ -121,5 +122,30 @@ def test_gpu_writer_matches_reference_run(gpu, name):
             out[t].extend(part[t])
         i = j
     # the reference writes key by key into every threshold file: same order, same bytes
+    for jt, thr in enumerate(THRESHOLDS):
+        assert "".join(out[thr]) == str(g["rttm"][jt]), thr
+
+
+def test_gpu_window_mean_matches_reference_run(gpu):
+    """postprocess_win12: a 12-s window / 1-s shift plan (up to 12 values per frame, so numpy's
+    pairwise summation inside np.mean decides the last bit in ~16 % of the frames).  The GPU
+    overlap mean over the window probabilities equals np.mean of the reference's res_dict lists
+    bit for bit, and the GPU writer on those means reproduces the reference's RTTM files."""
+    import os
+    from make_postprocess_golden import THRESHOLDS
+    from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
+    from speaker_diarization_amd.ts_vad.postprocess import posteriors_to_rttm_gpu
+    from speaker_diarization_amd.ts_vad.windows import plan_windows
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "postprocess_win12.npz"))
+    rs, shift = (int(x) for x in g["win_geometry"])
+    n_lab = len(g["counts_0"])
+    plan = plan_windows(n_lab, rs, shift)
+    np.testing.assert_array_equal(plan.starts, g["win_starts"])
+    np.testing.assert_array_equal(plan.lens, g["win_lens"])
+    mean = TSVADPipeline.mean_probs(torch.from_numpy(g["win_probs"]).to(gpu), plan)
+    want = np.stack([g[f"means_{i}"] for i in range(len(g["keys"]))])
+    np.testing.assert_array_equal(mean.cpu().numpy(), want)
+    keys = [str(k) for k in g["keys"]]
+    out = posteriors_to_rttm_gpu(keys, mean)
     for jt, thr in enumerate(THRESHOLDS):
         assert "".join(out[thr]) == str(g["rttm"][jt]), thr

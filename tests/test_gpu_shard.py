@@ -82,15 +82,20 @@ def test_tsvad_rank_reads_only_its_span(gpu, c4_meeting):
 
 
 @pytest.mark.parametrize("world", WORLDS)
-def test_eda_chunk_shards_bit_identical(gpu, world):
+@pytest.mark.parametrize("seconds,max_seqs", [(15 * 60.0 + 3.3, 8), (53 * 60.0 + 20.3, 16)])
+def test_eda_chunk_shards_bit_identical(gpu, world, seconds, max_seqs):
+    """9003 frames (4 x 2000 + 1003) and 32003 frames (16 equal chunks + a 3-frame tail): with 16
+    chunks the one-rank forward batches M = 32 000 rows, a rank of world 2 / 4 / 8 M = 16 000 /
+    8 000 / 4 000 — any GEMM choice that depended on the batched M (e.g. a split-K count) would
+    change the fp32 summation and show here."""
     from speaker_diarization_amd.eend_eda.infer import (EdaInferArgs, chunk_activities, gen_chunk_indices,
                                                         recording_features, shard_chunks)
     from speaker_diarization_amd.eend_eda.models import EendEdaModel
     from speaker_diarization_amd.weights import EDAConfig, eda_state_dict
-    meeting = make_meeting(15 * 60.0 + 3.3, n_spk=3, seed=99)   # 9003 frames: 4 x 2000 + 1003
+    meeting = make_meeting(seconds, n_spk=3, seed=99)
     torch.manual_seed(777)
     m = EendEdaModel(n_speakers=3, in_size=345, n_heads=4, n_units=256, n_layers=2, device=gpu,
-                     precision="bf16", max_seqs=8, max_frames=2000)
+                     precision="bf16", max_seqs=max_seqs, max_frames=2000)
     m.load_state_dict(to_torch(eda_state_dict(EDAConfig(model_type="EendEda", n_speakers=3, n_layers=2),
                                               seed=5)))
     args = EdaInferArgs(num_speakers=None)
