@@ -379,15 +379,18 @@ int sd_op_attention(const float* qkv, int S, int T, int D, int nh, int causal, i
 /* Chunk-streaming attention (ts_vad2_streaming forward_chunk_by_chunk's KV caches as one
  * block-causal mask): query i sees key j iff j / chunk <= i / chunk and, when left >= 0,
  * j / chunk >= i / chunk - left.  precision as sd_op_attention. */
+/* Test op: time attention over a (S, T, C) token grid — qkv (S, T, C, 3D) rows, out (S, T, C, D) —
+ * one sequence per (s, c) whose tokens are C rows apart, as the FS-EEND fusion decoder runs it
+ * (fs_eend.py:459-478: MHA over time per speaker slot, causal mask).  precision as sd_op_attention. */
+int sd_op_attention_grid(const float* qkv, int S, int T, int C, int D, int nh, int causal, int causal_delay,
+                         float* out, int precision, void* stream);
 int sd_op_attention_chunk(const float* qkv, int S, int T, int D, int nh, int chunk, int left, float* out,
                           int precision, void* stream);
-/* Diagnostics: the attention above (causal / key_len / chunk terms as given) with every visited
+/* Test probe: the attention above (causal / key_len / chunk terms as given) with every visited
  * (query, key) decision of sequence 0, head 0 written to mask_dump (T*T int32, caller-zeroed:
- * 0 = tile not visited, 1 = visible, 2 = masked).  mask_form 0 = the product's per-query key
- * window, 1 = the per-key division form of the chunk term, 2 = form 1 over the unclipped key range
- * (the round-1 kernel).  Used by the mask tests only. */
+ * 0 = tile not visited, 1 = visible, 2 = masked).  Used by the mask tests only. */
 int sd_probe_attention_mask(const float* qkv, int S, int T, int D, int nh, int causal, int causal_delay,
-                            const int* key_len, int chunk, int left, int mask_form, int* mask_dump, float* out,
+                            const int* key_len, int chunk, int left, int* mask_dump, float* out,
                             int precision, void* stream);
 int sd_op_layernorm(const float* x, int rows, int D, const float* g, const float* b, float eps,
                     float* y, void* stream);

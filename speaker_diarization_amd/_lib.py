@@ -185,10 +185,12 @@ _SIGS = {
                              c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                 c_void_p]),
+    "sd_op_attention_grid": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                     c_void_p]),
     "sd_op_attention_chunk": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                       c_void_p]),
     "sd_probe_attention_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
-                                        c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+                                        c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "sd_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "sd_op_lstm": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p]),

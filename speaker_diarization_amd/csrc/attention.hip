@@ -31,19 +31,10 @@ __device__ __forceinline__ KeyWindow chunk_window(const AttnArgs& a, int q) {
   const int qc = q / a.chunk;
   return {a.left < 0 ? 0 : max(0, qc - a.left) * a.chunk, (qc + 1) * a.chunk};
 }
-// Key visibility of query myq (key_len, causal and chunk terms).  mask_form 1 is the per-key
-// division form of the chunk term, mask_form 2 that form over the unclipped key range 0 .. klen
-// (the round-1 kernel before the key-window change); diagnostics only (sd_probe_attention_mask).
-// a.mask_dump records the decision of every visited (query, key) pair of sequence 0, head 0.
+// Key visibility of query myq (key_len, causal and chunk-window terms).  a.mask_dump (tests,
+// sd_probe_attention_mask) records the decision of every visited (query, key) pair of sequence 0, head 0.
 __device__ __forceinline__ bool key_visible(const AttnArgs& a, const KeyWindow& kw, int klen, int key, int myq) {
-  bool ok = key < klen && (!a.causal || key <= myq + a.causal_delay);
-  if (a.mask_form != 0 && a.chunk) {
-    const int kc = key / a.chunk, qc = myq / a.chunk;
-    ok = ok && kc <= qc && (a.left < 0 || kc >= qc - a.left);
-  } else {
-    ok = ok && key >= kw.lo && key < kw.hi;
-  }
-  return ok;
+  return key < klen && (!a.causal || key <= myq + a.causal_delay) && key >= kw.lo && key < kw.hi;
 }
 __device__ __forceinline__ void dump_mask(const AttnArgs& a, int s, int h, int T, int key, int myq, bool ok) {
   if (a.mask_dump && s == 0 && h == 0 && myq < T && key < T) a.mask_dump[(int64_t)myq * T + key] = ok ? 1 : 2;
@@ -118,7 +109,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const KeyWindow kw = chunk_window(a, myq);
   int k_end = klen;
   if (a.causal) k_end = min(k_end, blockIdx.x * kQB + kQB + a.causal_delay);
-  const bool clip = a.chunk && a.mask_form != 2;
+  const bool clip = a.chunk != 0;
   if (clip) k_end = min(k_end, ((blockIdx.x * kQB + kQB - 1) / a.chunk + 1) * a.chunk);
   // left >= 0: tiles wholly before the block's first query window hold no visible key
   const int k_begin = (clip && a.left >= 0) ? chunk_window(a, blockIdx.x * kQB).lo / kKT * kKT : 0;
@@ -384,7 +375,7 @@ __global__ __launch_bounds__(256) void attn_short_kernel(AttnArgs a, int TP, int
       const KeyWindow kw = chunk_window(a, myq);
       int k_end = klen;
       if (a.causal) k_end = min(k_end, q0 + 16 + a.causal_delay);
-      const bool clip = a.chunk && a.mask_form != 2;
+      const bool clip = a.chunk != 0;
       if (clip) k_end = min(k_end, ((q0 + 15) / a.chunk + 1) * a.chunk);
       const int k_begin = (clip && a.left >= 0) ? chunk_window(a, q0).lo / 32 * 32 : 0;
       for (int k0 = k_begin; k0 < k_end; k0 += 32) {
@@ -515,12 +506,10 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   // XCD-aware order: the query blocks of one (sequence, head) are consecutive logical ids on one XCD, so
   // its K/V prefix (1.5 MB at T 6000, d 64) is fetched into that XCD's L2 once instead of into all eight
   // (FETCH_SIZE: 150 MB per decoder launch for 37 MB of K/V)
-  // split-KV halves are the fastest-varying block index (a heavy query block's two halves start together)
-  const int ns = a.nsplit, pz = (int)blockIdx.x % ns;
-  const int nqb = (int)gridDim.x / ns;
+  const int nqb = (int)gridDim.x;
   // (large grids only: a small grid's heads would land whole on few XCDs, heavy query blocks together)
-  const int lin = (int)(blockIdx.y * nqb + (int)blockIdx.x / ns);
-  const int lid = (HOIST == 2 || ns > 1) ? lin : xcd_remap(lin, nqb * (int)gridDim.y);
+  const int lin = (int)(blockIdx.y * nqb + (int)blockIdx.x);
+  const int lid = HOIST == 2 ? lin : xcd_remap(lin, nqb * (int)gridDim.y);
   const int sh = lid / nqb, s = sh / a.nh, h = sh % a.nh;
   const int T = a.T, D = a.D;
   const int qbi = lid - sh * nqb;
@@ -554,9 +543,8 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   if (a.causal) k_end = min(k_end, qblk0 + kQB + a.causal_delay);
   const int ntile = k_end > 0 ? (k_end + kLKT - 1) / kLKT : 0;
   const int npair = (ntile + 1) / 2;
-  // split-KV (small grids): this workgroup takes pairs pz, pz + ns, ... of the query block's key range
-  const int nit = npair > pz ? (npair - pz + ns - 1) / ns : 0;
-  auto P = [&](int i) { return pz + ns * i; };
+  const int nit = npair;
+  auto P = [&](int i) { return i; };
   // staging map: chunk c = tid + 512 i -> pair row c / CPR, 16-B chunk c % CPR.  Two register sets: pair
   // p + 1 is staged from one at the end of pair p while pair p + 2 is in flight in the other.
   struct KV { u32x4_t k[CHK], v[CHK]; };   // native vectors: HIP's uint4 wrapper kept the sets in scratch
@@ -753,56 +741,6 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) o[dt][r] = o[dt][r] * f0 + mg[256 * (2 + 4 * dt + r)] * f1;
     m_run = m;
   }
-  if (ns > 1) {
-    // Split-KV: publish this half's (m, l, O) partial, count arrivals on the query block's counter; the
-    // later finisher merges both partials (in half order, so the result does not depend on which finished
-    // first) and stores the output.  The hand-off of the LSTM (MI355X guide R1): write-through (sc1) stores,
-    // every storing wave's vmcnt(0), barrier, one agent-scope count; the reader's loads are sc1 too.  (A
-    // __threadfence() release here cost 4x the kernel: it writes back the XCD's whole L2.)
-    const int slot = lin;
-    const int ltid = qw * 64 + lane;   // 256 threads of the even half
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        a.split_ws + (int64_t)slot * 2 * MW * 256, (short)0, (int)(2 * MW * 256 * sizeof(float)), 0x00020000);
-    auto off = [&](int half_, int j) { return (uint32_t)(((half_ * MW + j) * 256 + ltid) * sizeof(float)); };
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_run), rw, off(pz, 0), 0, 16);   // sc1
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run), rw, off(pz, 1), 0, 16);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[dt][r]), rw, off(pz, 2 + 4 * dt + r), 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // the odd-half waves have exited: the barrier counts the 4 remaining waves
-    // the flag lives in the (dead) V buffer: one more static LDS word would push the workgroup past 80 KiB
-    // and halve its occupancy (2 -> 1 per CU)
-    int* s_last = reinterpret_cast<int*>(&Vs[0][0]);
-    if (ltid == 0) {
-      const int old = __hip_atomic_fetch_add(a.split_cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_last = old == ns - 1;
-      if (old == ns - 1) __hip_atomic_store(a.split_cnt + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!*s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the count
-    const int oth = 1 - pz;
-    auto ld = [&](int j) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, off(oth, j), 0, 16)); };
-    const float mo = ld(0), lo = ld(1);
-    const float m0 = pz == 0 ? m_run : mo, m1 = pz == 1 ? m_run : mo;
-    const float l0 = pz == 0 ? l_run : lo, l1 = pz == 1 ? l_run : lo;
-    const float m = vmax(m0, m1);
-    const float f0 = m0 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m0 - m);
-    const float f1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - m);
-    l_run = __fadd_rn(__fmul_rn(l0, f0), __fmul_rn(l1, f1));
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ov = ld(2 + 4 * dt + r);
-        const float o0 = pz == 0 ? o[dt][r] : ov;
-        const float o1 = pz == 1 ? o[dt][r] : ov;
-        o[dt][r] = __fadd_rn(__fmul_rn(o0, f0), __fmul_rn(o1, f1));
-      }
-  }
   if (myq < T) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + (row0 + (int64_t)myq * a.tok_stride) * a.ldo + h * HD;
@@ -903,7 +841,7 @@ __global__ __launch_bounds__(256) void attn_tiny_kernel(AttnArgs a) {
 template <int HD>
 bool launch_tiny(const AttnArgs& a, bool bf16, hipStream_t st) {
   static const bool off = getenv("SDIAR_NO_ATTN_TINY") != nullptr;   // A/B switch: attn_short
-  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || a.T > 16 || HD % 8 || HD > 128 ||
+  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_dump || a.T > 16 || HD % 8 || HD > 128 ||
       (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 8) || (a.tok_stride * a.ld_qkv) % 8)
     return false;
   const int64_t n = (int64_t)a.S * a.nh * a.T;
@@ -911,36 +849,10 @@ bool launch_tiny(const AttnArgs& a, bool bf16, hipStream_t st) {
   return true;
 }
 
-// Per-stream split-KV scratch (launches on one stream are ordered, so one buffer per stream suffices; the
-// counters are zeroed once and reset by the finishing workgroup).  Not under stream capture (allocation).
-bool split_scratch(hipStream_t st, size_t ws_floats, size_t n_cnt, float** ws, int** cnt) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-  struct Buf { float* ws = nullptr; int* cnt = nullptr; size_t ws_n = 0, cnt_n = 0; };
-  static std::mutex mu;
-  static std::unordered_map<hipStream_t, Buf> bufs;
-  std::lock_guard<std::mutex> lock(mu);
-  Buf& b = bufs[st];
-  if (b.ws_n < ws_floats) {
-    if (b.ws) SD_HIP(hipFree(b.ws));
-    SD_HIP(hipMalloc(&b.ws, ws_floats * sizeof(float)));
-    b.ws_n = ws_floats;
-  }
-  if (b.cnt_n < n_cnt) {
-    if (b.cnt) SD_HIP(hipFree(b.cnt));
-    SD_HIP(hipMalloc(&b.cnt, n_cnt * sizeof(int)));
-    SD_HIP(hipMemset(b.cnt, 0, n_cnt * sizeof(int)));
-    b.cnt_n = n_cnt;
-  }
-  *ws = b.ws;
-  *cnt = b.cnt;
-  return true;
-}
-
 template <int HD>
 bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
   static const bool off = getenv("SDIAR_NO_ATTN_LONG") != nullptr;   // A/B switch: the generic kernel
-  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_form || a.mask_dump || HD % 32 || a.T <= 256 ||
+  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_dump || HD % 32 || a.T <= 256 ||
       (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 4) || (a.tok_stride * a.ld_qkv) % 8)
     return false;
   static int n_cu = 0;
@@ -953,23 +865,10 @@ bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
   // fewer than 2 workgroups per CU: latency-bound, hoist the fragment reads (measured: T 6000 with 4
   // heads 67 -> 57 us; with 24 sequence-heads the occupancy loss made it 215 -> 244 us)
   if ((int64_t)grid.x * grid.y < 2LL * n_cu) {
-    // Or split each query block's key pairs over two workgroups (the causal heaviest block's serial chain
-    // is the launch's length), partials merged by the later finisher through per-stream scratch; that
-    // doubles the grid, so it runs the 116-VGPR variant (two workgroups per CU; the hoisting one's 142
-    // VGPRs admit one).  T 6000 with 4 heads: 60 -> 54 us.  Opt-in (SDIAR_ATTN_SPLIT=1): the split changes
-    // the summation and the decision depends on the grid (S), so sharded runs (EDA chunk shards, bit-identical
-    // for any world size: test_eda_chunk_shards_bit_identical) would differ by world size.
-    AttnArgs b = a;
-    static const bool split = getenv("SDIAR_ATTN_SPLIT") && atoi(getenv("SDIAR_ATTN_SPLIT")) == 1;
-    const size_t slots = (size_t)grid.x * grid.y;
-    if (split && a.T >= 1024 && split_scratch(st, slots * 2 * (2 + 4 * (HD / 16)) * 256, slots, &b.split_ws,
-                                              &b.split_cnt)) {
-      b.nsplit = 2;
-      grid.x *= 2;
-      hipLaunchKernelGGL((attn_long_kernel<HD, 0>), grid, dim3(512), 0, st, b);
-    } else {
-      hipLaunchKernelGGL((attn_long_kernel<HD, 2>), grid, dim3(512), 0, st, a);
-    }
+    // (a split of each query block's key pairs over two workgroups measured 60 -> 54 us here, but the split
+    // depends on the grid, so sharded runs — EDA chunk shards, bit-identical for any world size — would
+    // differ by world size; not kept)
+    hipLaunchKernelGGL((attn_long_kernel<HD, 2>), grid, dim3(512), 0, st, a);
   } else {
     // large grids: K and the first V half hoisted (126 VGPRs, still 4 waves per SIMD): 187 -> 178 us on the
     // FS-EEND decoder shape against the unhoisted variant (116 VGPRs)
@@ -1035,10 +934,7 @@ void launch_hd(const AttnArgs& a, bool bf16, hipStream_t st) {
 }  // namespace
 
 void attention(const AttnArgs& a_in, bool bf16, hipStream_t st) {
-  // SDIAR_ATTN_MASK_FORM=1|2 runs whole models with a diagnostic chunk-term form (see key_visible)
-  static const int env_form = getenv("SDIAR_ATTN_MASK_FORM") ? atoi(getenv("SDIAR_ATTN_MASK_FORM")) : 0;
-  AttnArgs a = a_in;
-  if (!a.mask_form && env_form >= 1 && env_form <= 2) a.mask_form = env_form;
+  const AttnArgs& a = a_in;
   SD_CHECK(a.nh > 0 && a.D % a.nh == 0, kErrInvalid, "attention: D % nh != 0");
   SD_CHECK(a.ld_qkv % 4 == 0 && a.D % 4 == 0, kErrInvalid, "attention: ld_qkv % 4 != 0");
   const int hd = a.D / a.nh;

@@ -691,15 +691,18 @@ int sd_op_conv2d(const float* x, int B, int H, int W, int Cin, const float* w, i
 
 namespace {
 void op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, int causal_delay, const int* key_len,
-                  int chunk, int left, float* out, int precision, hipStream_t st, int mask_form = 0,
-                  int* mask_dump = nullptr) {
+                  int chunk, int left, float* out, int precision, hipStream_t st, int* mask_dump = nullptr,
+                  int grid_c = 0) {
   SD_CHECK(precision >= 0 && precision <= 2, sd::kErrInvalid, "precision must be 0, 1 or 2");
   sd::AttnArgs a;
   a.qkv = qkv; a.S = S_; a.T = T; a.D = D; a.nh = nh; a.ld_qkv = 3 * D;
   a.out = out; a.ldo = D; a.scale = 1.f / std::sqrt((float)(D / nh));
   a.causal = causal; a.causal_delay = causal_delay; a.key_len = key_len;
   a.chunk = chunk; a.left = left;
-  a.mask_form = mask_form; a.mask_dump = mask_dump;
+  a.mask_dump = mask_dump;
+  if (grid_c > 0) {   // time attention over a (S/C, T, C) token grid: sequence (s, c) walks tokens with stride C
+    a.seq_inner = grid_c; a.seq_outer = (int64_t)T * grid_c; a.seq_inner_stride = 1; a.tok_stride = grid_c;
+  }
   if (precision == 2) {   // bf16 storage: qkv and out in bf16 (the encoders' layout)
     Scratch qb((size_t)S_ * T * 3 * D * 2, st), ob((size_t)S_ * T * D * 2, st);
     sd::f32_to_bf16(qkv, (int64_t)S_ * T * 3 * D, qb.p, st);
@@ -717,6 +720,14 @@ int sd_op_attention(const float* qkv, int S_, int T, int D, int nh, int causal, 
   return guard([&] { op_attention(qkv, S_, T, D, nh, causal, causal_delay, key_len, 0, -1, out, precision, S(stream)); });
 }
 
+int sd_op_attention_grid(const float* qkv, int S_, int T, int C, int D, int nh, int causal, int causal_delay,
+                         float* out, int precision, void* stream) {
+  return guard([&] {
+    SD_CHECK(S_ >= 1 && C >= 1 && T >= 1, sd::kErrInvalid, "attention_grid: empty grid");
+    op_attention(qkv, S_ * C, T, D, nh, causal, causal_delay, nullptr, 0, -1, out, precision, S(stream), nullptr, C);
+  });
+}
+
 int sd_op_attention_chunk(const float* qkv, int S_, int T, int D, int nh, int chunk, int left, float* out,
                           int precision, void* stream) {
   return guard([&] {
@@ -726,13 +737,12 @@ int sd_op_attention_chunk(const float* qkv, int S_, int T, int D, int nh, int ch
 }
 
 int sd_probe_attention_mask(const float* qkv, int S_, int T, int D, int nh, int causal, int causal_delay,
-                            const int* key_len, int chunk, int left, int mask_form, int* mask_dump, float* out,
+                            const int* key_len, int chunk, int left, int* mask_dump, float* out,
                             int precision, void* stream) {
   return guard([&] {
-    SD_CHECK(mask_form >= 0 && mask_form <= 2, sd::kErrInvalid, "mask_form must be 0, 1 or 2");
     SD_CHECK(mask_dump != nullptr, sd::kErrInvalid, "mask_dump is required");
     op_attention(qkv, S_, T, D, nh, causal, causal_delay, key_len, chunk, left, out, precision, S(stream),
-                 mask_form, mask_dump);
+                 mask_dump);
   });
 }
 

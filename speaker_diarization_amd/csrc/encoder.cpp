@@ -130,11 +130,6 @@ ConformerL LayerLoader::conformer(const std::string& p, bool group_norm) {
       (f == 1 ? L.rp_f1_b1 : L.rp_f2_b1) = arena.upload(b1);
     }
     L.rp_out = put(rowprog_pack_pre(w32(p + ".self_attn.out_proj.weight", 1.f), E, E));
-    if (L.group_norm) {   // conv_block.hip takes the GroupNorm variant (its stats feed the pw2 program)
-      int N, Cin, kh, kw;
-      const std::vector<float> w1 = ps.pack(p + ".conv_module.sequential.0.weight", N, Cin, kh, kw);
-      if (N == 2 * E && Cin == E && kh * kw == 1) L.cb_w1 = put(conv_block_pack_w1(w1, N, Cin));
-    }
     L.rp_pw2 = put(rowprog_pack_pre(w32(p + ".conv_module.sequential.5.weight", 1.f), E, E));
   }
   return L;
@@ -205,16 +200,10 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   ffn_body(L.f1_w1, L.f1_b1, L.f1_w2, L.f1_b2);
   // self attention block (key_padding_mask from lengths)
   if (mha_block_supported(E, nh, T, bf)) {
-    // in-projection + attention in one launch (mha_block.hip); SDIAR_MHA_LN=1 also folds the residual
-    // add + self_attn_layer_norm into its prologue, else they run as the HBM-rate add_layernorm
-    static const bool fold_ln = getenv("SDIAR_MHA_LN") && atoi(getenv("SDIAR_MHA_LN")) == 1;
+    // in-projection + attention in one launch (mha_block.hip) on the LayerNorm'd rows
+    add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
     MhaBlockArgs m;
-    if (fold_ln) {
-      m.X = X; m.t = y.p;
-    } else {
-      add_layernorm(X, y.p, bf, rows, E, L.at_lng, L.at_lnb, 1e-5f, true, y.p, bf, st);
-      m.y = y.p;
-    }
+    m.y = y.p;
     m.ln_g = L.at_lng; m.ln_b = L.at_lnb; m.eps = 1e-5f;
     m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
     m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
@@ -303,12 +292,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
       rowprog(r, "rowprog_out", st);
     }
-    if (L.cb_w1 && conv_block_supported(E, T, kernel, true)) {
-      ConvBlockArgs c;   // pw1 + GLU + depthwise conv per sequence, h never leaves LDS
-      c.y = y.p; c.w1 = L.cb_w1; c.b1 = L.pw1_b; c.dw_w = L.dw_w; c.dw_b = L.dw_b; c.k = kernel;
-      c.out = ao.p; c.partial = w.partial; c.S = S; c.T = T;
-      conv_block(c, st);
-    } else {
+    {
       ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
       p1.glu = 1;
       const bool glu_epi = gemm_stream_supported(p1);

@@ -50,7 +50,6 @@ struct ConformerL {       // torchaudio.models.conformer.ConformerLayer (conv af
   // rowprog.hip pieces (bf16 mode, D 384): ffn1 / ffn2 (W1 | ½W2), out_proj, pointwise_conv2
   const void *rp_f1 = nullptr, *rp_f2 = nullptr, *rp_out = nullptr, *rp_pw2 = nullptr;
   const float *rp_f1_b1 = nullptr, *rp_f2_b1 = nullptr;   // up-projection biases with the LN shift folded in
-  const void* cb_w1 = nullptr;   // conv_block.hip pw1 pieces (bf16 mode, D 384)
   int rp_hidden = 0;
 };
 

@@ -172,29 +172,19 @@ struct AttnArgs {
   int64_t seq_outer = 0;
   int seq_inner_stride = 0;
   int tok_stride = 1;
-  // Diagnostics (sd_probe_attention_mask): 1 = per-key division form of the chunk term, 2 = that
-  // form over the unclipped key range (the round-1 kernel);
-  // mask_dump (T*T int32, zeroed) receives 1/2 = visible/masked for each visited pair of seq 0, head 0.
-  int mask_form = 0;
+  // Test probe (sd_probe_attention_mask): mask_dump (T*T int32, zeroed) receives 1/2 = visible/masked
+  // for each visited pair of seq 0, head 0.
   int* mask_dump = nullptr;
-  // Internal (attention.hip): split-KV of the long kernel's small grids — blockIdx.z halves of a query
-  // block's key pairs, partials merged by the later finisher through split_ws / split_cnt.
-  int nsplit = 1;
-  float* split_ws = nullptr;
-  int* split_cnt = nullptr;
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 
 // ---------------------------------------------------------------- mha_block.hip
-// Conformer self-attention block in one launch (bf16, D 384, 8 heads, T <= 160): X += t (t bf16,
-// nullable), y = LN(X) * g + b, q|k|v = y · W_inᵀ + bias (W_in packed bf16 (3D, D)), per head
-// softmax(q kᵀ * scale) v -> out (S*T rows of stride ldo, bf16).  key_len (device int32 per
-// sequence) optional.
+// Conformer self-attention block in one launch (bf16, D 384, 8 heads, T <= 160): q|k|v = y · W_inᵀ + bias
+// (y the LayerNorm'd bf16 rows, W_in packed bf16 (3D, D)), per head softmax(q kᵀ * scale) v -> out (S*T
+// rows of stride ldo, bf16).  key_len (device int32 per sequence) optional.
 struct MhaBlockArgs {
-  float* X = nullptr;
-  const void* t = nullptr;
-  const void* y = nullptr;   // when set: bf16 rows already normalised; X / t / ln_* unused
-  const float* ln_g = nullptr;
+  const void* y = nullptr;   // bf16 rows, already LayerNorm'd (self_attn_layer_norm)
+  const float* ln_g = nullptr;   // (informational: the norm the rows went through)
   const float* ln_b = nullptr;
   float eps = 1e-5f;
   const void* W = nullptr;
@@ -204,29 +194,9 @@ struct MhaBlockArgs {
   int S = 0, T = 0, D = 0, nh = 0;
   float scale = 1.f;
   const int* key_len = nullptr;
-  int probe = 0;   // timing probes (SDIAR_MHA_PROBE bits): 1 no attention, 2 no projection MFMA, 4 no
-                   // weight DMA, 8 no LayerNorm statistics pass — outputs are wrong with any bit set
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
 
-// ---------------------------------------------------------------- conv_block.hip
-// Conformer conv-module body per sequence (bf16, D 384, T <= 152): h = GLU(y · W1ᵀ + b1) kept in LDS,
-// out = depthwise_conv_k(h) + dw_b (bf16, (S*T, 384)), partial = GroupNorm sums per (sequence, 64 channels)
-// as glu_dwconv writes them.  w1 from conv_block_pack_w1 (original row order), b1 interleaved as the
-// GLU-epilogue GEMMs take it ([16 values | 16 gates] per 32-row group).
-struct ConvBlockArgs {
-  const void* y = nullptr;
-  const void* w1 = nullptr;
-  const float* b1 = nullptr;
-  const float *dw_w = nullptr, *dw_b = nullptr;
-  int k = 0;
-  void* out = nullptr;
-  float* partial = nullptr;
-  int S = 0, T = 0;
-};
-bool conv_block_supported(int D, int T, int k, bool bf16);
-std::vector<uint16_t> conv_block_pack_w1(const std::vector<float>& W, int N, int K);
-void conv_block(const ConvBlockArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------- rowprog.hip
 // Conformer per-token row program (bf16 weights, D 384): acc = X; [acc += A·W0ᵀ + b0];

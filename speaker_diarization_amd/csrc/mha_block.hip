@@ -6,9 +6,8 @@
 //
 // A workgroup owns TWO sequences (10 waves; wave w: sequence w / 5, tokens 32 (w % 5) .. +31, i.e. two
 // 16-token MFMA row tiles), D = 384, 8 heads of 48:
-//   prologue  x = X + t (fp32), two-pass LayerNorm per token (row re-read from L1 between passes),
-//             X <- x; the normalised rows become the wave's MFMA B-operand fragments (2 x 16 tokens x
-//             384, 96 VGPRs), read once from HBM;
+//   prologue  the LayerNorm'd bf16 rows (the preceding row program / add_layernorm writes them) become
+//             the wave's MFMA B-operand fragments (2 x 16 tokens x 384, 96 VGPRs), read once from HBM;
 //   pieces    16 in-projection rows (one head's 16 features of q, k or v), 12 KiB, stream through a
 //             3-slot LDS-DMA ring (buffer_load ... lds, 16-B chunk c of row r at c ^ (r & 7)), two pieces
 //             in flight behind counted vmcnt waits; each weight fragment read from LDS feeds both row
@@ -19,7 +18,7 @@
 //   attention after a head's last V piece: Sᵀ = K·Qᵀ, online softmax, Oᵀ = Vᵀ·Pᵀ with Vᵀ from
 //             ds_read_b64_tr_b16 (the attn_short scheme), 8-B bf16 stores of the head's 48 features.
 // The in-projection weights (864 KiB bf16) come from L2 once per workgroup, i.e. once per two sequences;
-// HBM sees X (read + write, fp32), t and the attention output only.
+// HBM sees the normalised rows and the attention output only.
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -53,11 +52,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// PROBE: timing probes as a compile-time constant (a runtime probe word put a branch around every MFMA
-// pair and split the projection loop into 2-MFMA blocks); -1 = read the bits from a.probe.
-template <int PROBE>
 __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
-  const int probe = PROBE >= 0 ? PROBE : a.probe;
   extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
   uint16_t* Ws = sm;                                          // [kNSlot][kKC][16][64]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -92,10 +87,8 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     }
   };
   const int my_dma = (w < kDmaPerPiece - kWaves) ? 2 : 1;      // instructions this wave issues per piece
-  if (!(probe & 4)) {
-    issue_piece(0);
-    issue_piece(1);
-  }
+  issue_piece(0);
+  issue_piece(1);
   for (int i = tid; i < 3 * kD; i += kThreads) s_bias[i] = a.bias[i];
   for (int i = tid; i < kSeq * kTP * 2; i += kThreads) {   // zero Q/K features 48..63 (never written later)
     const int q = i / (kTP * 2), r = (i >> 1) % kTP, c = kHD + (i & 1) * 8;
@@ -104,88 +97,17 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     *reinterpret_cast<uint4*>(qs + kTP * kQS + r * kQS + c) = make_uint4(0u, 0u, 0u, 0u);
   }
 
-  // ---- prologue: per row tile, x = X + t, LayerNorm, X <- x; af[rt][kk] = LN(x)[32kk + 8lk .. +7]
+  // ---- prologue: af[rt][kk] = y[32kk + 8lk .. +7] of the LayerNorm'd bf16 rows (B-operand fragments)
   bf16x8 af[2][kKT32];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     const int row = r0 + 16 * rt;
     const bool live = seq_ok && row < T;
-    const int64_t grow = (int64_t)s * T + row;
-    if (a.y) {   // already-normalised bf16 rows (the LayerNorm ran as its own HBM-rate kernel)
-      const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + grow * kD;
+    const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + ((int64_t)s * T + row) * kD;
 #pragma unroll
-      for (int kk = 0; kk < kKT32; ++kk)
-        af[rt][kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(yr + 32 * kk + 8 * lk)
-                                                     : make_uint4(0u, 0u, 0u, 0u));
-      continue;
-    }
-    const float* xr = a.X + grow * kD;
-    const uint16_t* tr = reinterpret_cast<const uint16_t*>(a.t) + grow * kD;
-    auto load8 = [&](int kk, float* v) {
-      const int k = 32 * kk + 8 * lk;
-      const float4 x0 = *reinterpret_cast<const float4*>(xr + k);
-      const float4 x1 = *reinterpret_cast<const float4*>(xr + k + 4);
-      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-      if (a.t) {
-        const uint4 tv = *reinterpret_cast<const uint4*>(tr + k);
-        const uint32_t tw[4] = {tv.x, tv.y, tv.z, tv.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          v[2 * u] += __uint_as_float(tw[u] << 16);
-          v[2 * u + 1] += __uint_as_float(tw[u] & 0xffff0000u);
-        }
-      }
-    };
-    float mean = 0.f, rstd = 0.f;
-    if (live && !(probe & 8)) {
-      float sum = 0.f;
-      for (int kk = 0; kk < kKT32; ++kk) {
-        float v[8];
-        load8(kk, v);
-        sum += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-      }
-      asm volatile("" ::: "memory");   // re-read the row below (L1 hit) instead of keeping 96 values live
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      mean = sum / (float)kD;
-      float q = 0.f;
-      for (int kk = 0; kk < kKT32; ++kk) {
-        float v[8];
-        load8(kk, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) q += (v[j] - mean) * (v[j] - mean);
-      }
-      asm volatile("" ::: "memory");
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      rstd = rsqrtf(q / (float)kD + a.eps);
-    }
-#pragma unroll
-    for (int kk = 0; kk < kKT32; ++kk) {
-      uint32_t pk[4] = {0u, 0u, 0u, 0u};
-      if (live) {
-        const int k = 32 * kk + 8 * lk;
-        float v[8];
-        load8(kk, v);
-        if (a.t) {
-          float* xw = a.X + grow * kD + k;
-          *reinterpret_cast<float4*>(xw) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(xw + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-        const float4 g0 = *reinterpret_cast<const float4*>(a.ln_g + k);
-        const float4 g1 = *reinterpret_cast<const float4*>(a.ln_g + k + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(a.ln_b + k);
-        const float4 b1 = *reinterpret_cast<const float4*>(a.ln_b + k + 4);
-        const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          pk[u] = pack_bf16x2((v[2 * u] - mean) * rstd * gg[2 * u] + bb[2 * u],
-                              (v[2 * u + 1] - mean) * rstd * gg[2 * u + 1] + bb[2 * u + 1]);
-      }
-      af[rt][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
-      asm volatile("" ::: "memory");   // one k-step's loads at a time (register pressure)
-    }
+    for (int kk = 0; kk < kKT32; ++kk)
+      af[rt][kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(yr + 32 * kk + 8 * lk)
+                                                   : make_uint4(0u, 0u, 0u, 0u));
   }
 
   const int klen = seq_ok ? (a.key_len ? min(a.key_len[s], T) : T) : 0;
@@ -196,13 +118,13 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
 
   for (int i = 0; i < kPieces; ++i) {
     // Piece i landed: the only younger DMA is piece i+1's (this wave's my_dma instructions), unless
-    // stores were issued after it (prologue X stores, attention outputs) -> full drain.
-    if (drain || i + 1 >= kPieces || (probe & 4)) wait_vm<0>();
+    // stores were issued after it (attention outputs) -> full drain.
+    if (drain || i + 1 >= kPieces) wait_vm<0>();
     else if (my_dma == 2) wait_vm<2>();
     else wait_vm<1>();
     drain = false;
     __syncthreads();   // every wave's part of piece i is in LDS; slot (i+2) % 3 (piece i-1) is free
-    if (i + 2 < kPieces && !(probe & 4)) issue_piece(i + 2);
+    if (i + 2 < kPieces) issue_piece(i + 2);
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
     const uint16_t* slot = Ws + (i % kNSlot) * kSlot;
     floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -217,10 +139,8 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     for (int kk = 0; kk < kKT32; ++kk) {
       bf16x8 wnext = wcur;
       if (kk + 1 < kKT32) wnext = wfrag(kk + 1);
-      if (!(probe & 2)) {
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
-      }
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
       asm volatile("" ::: "memory");
       wcur = wnext;
     }
@@ -237,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
                      pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2) continue;
     __syncthreads();   // head h's Q, K, V images complete (both sequences)
-    if ((probe & 1) || !seq_ok) continue;
+    if (!seq_ok) continue;
 
     // ---- attention of head h for this wave's two 16-query tiles
 #pragma unroll 1
@@ -326,23 +246,18 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st) {
   SD_CHECK(mha_block_supported(kD, a.nh, a.T, true) && a.D == kD, kErrInvalid, "mha_block: unsupported shape");
   SD_CHECK(a.ldo % 4 == 0, kErrInvalid, "mha_block: output row stride must be a multiple of 4");
   if (a.S <= 0) return;
+  SD_CHECK(a.y != nullptr, kErrInvalid, "mha_block: y (LayerNorm'd bf16 rows) is required");
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<0>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<-1>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     attr = true;
   }
   const double rows = (double)a.S * a.T;
   const double flops = 2.0 * rows * 3 * kD * kD + 4.0 * a.S * (double)a.T * a.T * kD;
-  const double bytes = rows * kD * (a.y ? 2.0 + 2.0 : 4.0 + (a.t ? 2.0 + 4.0 : 0.0) + 2.0) + 2.0 * 3 * kD * kD;
+  const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
   ProfScope prof("mha_block", flops, bytes, st);
-  static const int probe = getenv("SDIAR_MHA_PROBE") ? atoi(getenv("SDIAR_MHA_PROBE")) : 0;
-  MhaBlockArgs b = a;
-  b.probe = probe;
-  if (probe) hipLaunchKernelGGL(mha_block_kernel<-1>, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
-  else hipLaunchKernelGGL(mha_block_kernel<0>, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, b);
+  hipLaunchKernelGGL(mha_block_kernel, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, a);
   SD_LAUNCH_CHECK();
 }
 

@@ -746,102 +746,6 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
   }
 }
 
-// bf16 conformer depthwise conv on already-gated rows (the pw1 GLU epilogue's output): the C2 path.
-// Lane = a PAIR of channels, so the k-tap FMAs run as packed f32 (v_pk_fma_f32: two outputs per
-// instruction) — the one-channel-per-lane kernel above is VALU-bound (31 FMAs per output at the
-// unpacked f32 rate), this one does the same arithmetic (same fp32 weights, same tap order) at twice
-// the rate on half the waves.  Block = (sequence, 128 channels), the whole sequence (+ halo) staged
-// once in LDS as bf16; each wave emits runs of kDwR rows, transposed through LDS into 16-B stores.
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-constexpr int kDw2CB = 128;
-constexpr int kDw2TT = 80;
-__global__ __launch_bounds__(256) void dwconv_pk_kernel(const uint16_t* __restrict__ x, int T, int C,
-                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                        int k, uint16_t* __restrict__ y, float* __restrict__ partial,
-                                                        int fused_silu) {
-  __shared__ __attribute__((aligned(16))) uint16_t g[(kDw2TT + kDwMaxK - 1) * kDw2CB];
-  __shared__ float red[2][256];
-  __shared__ __attribute__((aligned(16))) uint16_t otile[4][kDwR * kDw2CB];
-  const int pad = (k - 1) / 2;
-  const int s = blockIdx.y;
-  const int c0 = blockIdx.x * kDw2CB;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = c0 + 2 * lane;   // this lane's channels c, c + 1
-  const bool cv = c < C;         // C % 16 == 0: both or neither
-  f32x2_t wr[kDwMaxK];
-#pragma unroll
-  for (int j = 0; j < kDwMaxK; ++j)
-    wr[j] = (j < k && cv) ? f32x2_t{w[(int64_t)c * k + j], w[(int64_t)(c + 1) * k + j]} : f32x2_t{0.f, 0.f};
-  const f32x2_t bv = (bias && cv) ? f32x2_t{bias[c], bias[c + 1]} : f32x2_t{0.f, 0.f};
-  const uint16_t* xs = x + (int64_t)s * T * C;
-  uint16_t* ys = y + (int64_t)s * T * C;
-  float lsum = 0.f, lsq = 0.f;
-  constexpr int CPR = kDw2CB / 8;   // 16-B chunks per staged row
-  for (int t0 = 0; t0 < T; t0 += kDw2TT) {
-    const int span = min(kDw2TT, T - t0) + k - 1;
-    __syncthreads();
-    for (int i = threadIdx.x; i < span * CPR; i += blockDim.x) {
-      const int tt = i / CPR, ch = (i % CPR) * 8;
-      const int t = t0 - pad + tt;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (t >= 0 && t < T && c0 + ch < C) v = *reinterpret_cast<const uint4*>(xs + (int64_t)t * C + c0 + ch);
-      *reinterpret_cast<uint4*>(g + tt * kDw2CB + ch) = v;
-    }
-    __syncthreads();
-    const int nout = min(kDw2TT, T - t0);
-    for (int r0 = wv * kDwR; r0 < nout; r0 += 4 * kDwR) {
-      f32x2_t win[kDwR + kDwMaxK - 1];
-#pragma unroll
-      for (int i = 0; i < kDwR + kDwMaxK - 1; ++i) {
-        const uint32_t u = (i < kDwR + k - 1) ? *reinterpret_cast<const uint32_t*>(g + (r0 + i) * kDw2CB + 2 * lane) : 0u;
-        win[i] = f32x2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
-      }
-#pragma unroll
-      for (int r = 0; r < kDwR; ++r) {
-        f32x2_t acc = bv;
-#pragma unroll
-        for (int j = 0; j < kDwMaxK; ++j) acc = __builtin_elementwise_fma(wr[j], win[r + j], acc);
-        if (fused_silu) {
-          acc.x = acc.x / (1.f + __expf(-acc.x));
-          acc.y = acc.y / (1.f + __expf(-acc.y));
-        }
-        *reinterpret_cast<uint32_t*>(&otile[wv][r * kDw2CB + 2 * lane]) = pack_bf16x2(acc.x, acc.y);
-        if (r0 + r < nout && cv) {
-          lsum += acc.x + acc.y;
-          lsq += acc.x * acc.x + acc.y * acc.y;
-        }
-      }
-      // lane l: rows l / 16 and l / 16 + 4 of the run, channels 8 * (l % 16) .. +7 (same-wave LDS round trip)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int rr = (lane >> 4) + 4 * h, cc = (lane & 15) * 8;
-        const uint4 v = *reinterpret_cast<const uint4*>(&otile[wv][rr * kDw2CB + cc]);
-        if (r0 + rr < nout && c0 + cc < C) *reinterpret_cast<uint4*>(ys + (int64_t)(t0 + r0 + rr) * C + c0 + cc) = v;
-      }
-    }
-  }
-  if (fused_silu) return;   // uniform across the block
-  red[0][threadIdx.x] = lsum;
-  red[1][threadIdx.x] = lsq;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {   // the partials keep glu_dwconv_kernel's 64-channel block layout (nblk64 per
-    const int nb64 = (C + 63) / 64;   // sequence): this block's sum in its first entry, 0 in the second
-    const int e = 2 * blockIdx.x;
-    partial[((int64_t)s * nb64 + e) * 2 + 0] = red[0][0];
-    partial[((int64_t)s * nb64 + e) * 2 + 1] = red[1][0];
-    if (e + 1 < nb64) {
-      partial[((int64_t)s * nb64 + e + 1) * 2 + 0] = 0.f;
-      partial[((int64_t)s * nb64 + e + 1) * 2 + 1] = 0.f;
-    }
-  }
-}
 
 void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
                 void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st) {
@@ -851,15 +755,7 @@ void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
   dim3 grid(cdiv(C, kDwCB), S);
   const double eb = io_bf16 ? 2.0 : 4.0;
   ProfScope prof(glu_in ? "glu_dwconv" : "dwconv", 2.0 * S * T * C * k, eb * S * T * (glu_in ? 3.0 : 2.0) * C, st);
-  // opt-in (SDIAR_DWCONV_PK=1): measured slower on C2 (1.65 vs 1.52 ms for 6 launches; 167 VGPRs and the
-  // 128-channel stage leave 3 waves per SIMD, and the one-channel kernel is latency-, not VALU-bound)
-  static const bool pk = getenv("SDIAR_DWCONV_PK") && atoi(getenv("SDIAR_DWCONV_PK")) == 1;
-  if (io_bf16 && !glu_in && pk) {
-    hipLaunchKernelGGL(dwconv_pk_kernel, dim3(cdiv(C, kDw2CB), S), dim3(256), 0, st, reinterpret_cast<const uint16_t*>(x),
-                       T, C, w, bias, k, reinterpret_cast<uint16_t*>(y), partial, (int)fused_silu);
-    SD_LAUNCH_CHECK();
-    return;
-  }
+  // (a channel-pair packed-f32 variant measured slower on C2 — 1.65 vs 1.52 ms for 6 launches — and was removed)
   if (io_bf16)
     hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<const uint16_t*>(x), T,
                        C, w, bias, k, reinterpret_cast<uint16_t*>(y), partial, (int)fused_silu, (int)glu_in);

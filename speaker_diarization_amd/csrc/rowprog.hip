@@ -517,18 +517,13 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(a.X && a.Xo && (a.w0 || a.n_ffn > 0 || a.y), kErrInvalid, "rowprog: empty program");
   if (a.M <= 0) return;
   static int grid_max = 0;
-  static const int tt = getenv("SDIAR_RP_TT") ? atoi(getenv("SDIAR_RP_TT")) : 1;   // token tiles per wave
-  static const int probe = getenv("SDIAR_RP_PROBE") ? atoi(getenv("SDIAR_RP_PROBE")) : 0;
-  SD_CHECK(tt == 1 || tt == 2, kErrInvalid, "SDIAR_RP_TT must be 1 or 2");
   if (!grid_max) {
     int dev = 0, cus = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const void* ks[] = {reinterpret_cast<const void*>(rowprog_kernel<1, 0, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 2>),
                         reinterpret_cast<const void*>(rowprog_kernel<1, 0, 3>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 5>),
-                        reinterpret_cast<const void*>(rowprog_kernel<1, 0>), reinterpret_cast<const void*>(rowprog_kernel<2, 0>),
-                        reinterpret_cast<const void*>(rowprog_kernel<1, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 2>),
-                        reinterpret_cast<const void*>(rowprog_kernel<1, 4>), reinterpret_cast<const void*>(rowprog_kernel<1, 3>)};
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 0>)};
     for (const void* k : ks)
       SD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     grid_max = cus > 0 ? cus : 256;
@@ -545,12 +540,7 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   const double bytes = rows * kD * (8.0 + (a.w0 ? 2.0 : 0.0) + (a.y ? 2.0 : 0.0)) + wbytes;
   ProfScope prof(name, flops, bytes, st);
   const dim3 g3(grid);
-  if (tt == 2) hipLaunchKernelGGL((rowprog_kernel<2, 0>), g3, dim3(256), kSmemBytes, st, a);
-  else if (probe == 1) hipLaunchKernelGGL((rowprog_kernel<1, 1>), g3, dim3(512), kSmemBytes, st, a);
-  else if (probe == 2) hipLaunchKernelGGL((rowprog_kernel<1, 2>), g3, dim3(512), kSmemBytes, st, a);
-  else if (probe == 3) hipLaunchKernelGGL((rowprog_kernel<1, 3>), g3, dim3(512), kSmemBytes, st, a);
-  else if (probe == 4) hipLaunchKernelGGL((rowprog_kernel<1, 4>), g3, dim3(512), kSmemBytes, st, a);
-  else {
+  {
     const int prog = (a.w0 ? 1 : 0) | (a.n_ffn << 1);
     if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, a);
     else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, a);

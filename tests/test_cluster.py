@@ -29,3 +29,19 @@ def test_cluster_trivial_and_merge_edges():
     assert spectral.cluster(np.ones((2, 8), np.float32)) == [0, 0]
     subs = {"u": [(0.0, 1.5, "0"), (0.75, 2.25, "0"), (1.5, 3.0, "1"), (3.5, 4.0, "1")]}
     assert spectral.merge_segments(subs) == [("u", 0.0, 1.875, "0"), ("u", 1.875, 3.0, "1"), ("u", 3.5, 4.0, "1")]
+
+
+def test_vectorised_merge_matches_sequential_oracle():
+    """Random sub-segment streams (1.5 s windows every 0.75 s with jitter, gaps, 1-4 labels) through
+    the vectorised merge and the reference's sequential loop (oracle/cluster_ref.py): identical
+    segments, bit for bit."""
+    from oracle.cluster_ref import merge_segments_seq
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        subs = {}
+        for u in range(int(rng.integers(1, 4))):
+            n = int(rng.integers(1, 40))
+            t = np.cumsum(rng.choice([0.75, 0.75, 0.75, 2.0, 0.5], size=n)) + rng.random() * 3
+            lab = rng.integers(0, int(rng.integers(1, 5)), size=n)
+            subs[f"rec{u}"] = [(float(a), float(a + 1.5), str(l)) for a, l in zip(t, lab)]
+        assert spectral.merge_segments(subs) == merge_segments_seq(subs), trial

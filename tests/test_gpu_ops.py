@@ -186,6 +186,26 @@ def test_attention_long_bf16(gpu, S, T, D, nh, causal, delay, kl):
     assert _rel_err(out.cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("S,T,C,D,nh,delay", [(1, 3000, 6, 256, 4, 0), (1, 2200, 4, 256, 4, 2), (2, 1100, 6, 256, 4, 0)])
+def test_attention_grid_large_bf16(gpu, S, T, C, D, nh, delay):
+    """The FS-EEND decoder's time attention (fs_eend.py:459-478): causal MHA per speaker slot over a
+    (T, C) token grid, tokens C rows apart, bf16 io — at >= 512 workgroups (ceil(T / 64) x S*C*nh:
+    1128 / 560 / 816), i.e. the large-grid attn_long_kernel variant (K / V hoisted, XCD-aware block
+    order) the C5 decoder launches run, vs the fp32 torch reference of each slot's sequence."""
+    g = torch.Generator().manual_seed(T + C)
+    qkv = torch.randn(S, T, C, 3 * D, generator=g)
+    out = torch.empty(S * T * C, D, device=gpu)
+    _lib.call("sd_op_attention_grid", _d(qkv.reshape(-1, 3 * D), gpu), S, T, C, D, nh, 1, delay, out.data_ptr(), 2,
+              _lib.stream_ptr(gpu))
+    torch.cuda.synchronize()
+    assert ((T + 63) // 64) * S * C * nh >= 512
+    got = out.cpu().view(S, T, C, D)
+    for c in range(C):
+        seq = qkv[:, :, c].reshape(S * T, 3 * D)
+        ref = _attn_ref(seq, S, T, D, nh, 1, delay).view(S, T, D)
+        assert _rel_err(got[:, :, c], ref) < 2e-2, c
+
+
 def _chunk_mask(T, chunk, left):
     """Key visibility of forward_chunk_by_chunk's KV caches (ts_vad2_streaming/model.py:594-655,
     transformer_chunk_streaming.py:305-373): chunks max(0, c - left) .. c."""
