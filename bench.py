@@ -60,9 +60,10 @@ WORKLOADS = {
                      "simulate_streaming), 4 speakers, every window decoded at its own length, 256 windows "
                      "per device call; replicas only"),
     "c5s": dict(kind="fseend_stream", n_spk=3, minutes=10.0, chunk=1,
-                desc="C5 latency mode: FS-EEND streamed 1 model frame (100 ms of 8 kHz audio) per push, "
-                     "per-layer K/V histories, each chunk's forward replayed as a captured hipGraph, host "
-                     "waits for every chunk's scores; replicas only"),
+                desc="C5 latency mode: FS-EEND fed 8 kHz audio in 80 ms pushes (640 samples); each model frame "
+                     "(100 ms) runs its STFT/logmel/splice and the causal encoder as one captured hipGraph, "
+                     "per-layer K/V histories, scores final 9 frames later; host waits for every push; "
+                     "replicas only"),
 }
 
 PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
@@ -93,6 +94,8 @@ def parse(argv=None):
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--chunk", type=int, default=None, help="c5s: model frames per streaming push")
     ap.add_argument("--no-graph", action="store_true", help="c5s: direct launches instead of hipGraph replay")
+    ap.add_argument("--feature-rows", action="store_true", help="c5s: push precomputed feature rows (model only)")
+    ap.add_argument("--push-samples", type=int, default=640, help="c5s: audio samples per push (640 = 80 ms)")
     return ap.parse_args(argv)
 
 
@@ -665,6 +668,7 @@ def main_eend(a, wl):
     kind = wl["kind"]
     prec = a.precision
     cpu_fn = None
+    parity_fn = None
     extra = {}
     if kind == "eda":
         from speaker_diarization_amd.eend_eda.infer import EdaInferArgs, chunk_outputs, select_chunks, stitch
@@ -688,6 +692,9 @@ def main_eend(a, wl):
 
         def cpu_fn():
             return eda_cpu_baseline(wl, meeting, sd_np, wl["num_speakers"])
+
+        def parity_fn():
+            return eda_oracle_parity(m, wav, meeting, sd_np, wl, iargs)
 
         def after(outs):
             """Speaker selection + the h5 stitch (infer_eda.py:112-121) on the timed run's outputs,
@@ -757,6 +764,9 @@ def main_eend(a, wl):
 
         def cpu_fn():
             return fseend_cpu_baseline(meeting, sd_np, a.cpu_seconds)
+
+        def parity_fn():
+            return fseend_oracle_parity(meeting, sd_np, step()[0][0], frames=1000)
     elapsed, out = timed(step, a.warmup, a.steps, world, dev)
     if kind == "eda":
         after(out)
@@ -776,10 +786,46 @@ def main_eend(a, wl):
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = cpu_fn()
             line["speedup_vs_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+            if parity_fn is not None:
+                line["parity"] = parity_fn()
         print(json.dumps(line))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def eda_oracle_parity(m, wav, meeting, sd_np, wl, iargs, n_chunks=2):
+    """EEND-EDA activities and attractor probabilities of the product path vs the fp32 CPU oracle
+    (oracle/eend_ref.py: infer_eda.py:92-124 restated) on the first n_chunks 2000-frame chunks, both driven
+    by the SAME per-chunk randperm draws (the frame shuffle decides the attractors, models.py:229-233):
+    max / mean |diff| over all (max_n - 1) attractor columns and the decisions (> 0.5, make_rttm's
+    threshold) that differ."""
+    import torch
+    from oracle import eend_ref
+    from speaker_diarization_amd.eend_eda.infer import chunk_activities, gen_chunk_indices, recording_features
+    from speaker_diarization_amd.weights import EDAConfig, to_torch
+    torch.set_num_threads(host_threads())
+    cfg = EDAConfig(model_type=wl["model_type"], n_speakers=wl["n_spk"], n_layers=wl["layers"])
+    feats = recording_features(m, wav, iargs)
+    chunks = list(gen_chunk_indices(feats.shape[0], iargs.chunk_size))[:n_chunks]
+    g = torch.Generator().manual_seed(777)
+    perms = [torch.randperm(e - s, generator=g) for s, e in chunks]
+    acts, probs = chunk_activities(m, feats, iargs, perms, 0, len(chunks))
+    Y = eend_ref.features(meeting.wav.astype(np.float64))
+    dmax, dsum, cnt, flips, pmax = 0.0, 0.0, 0, 0, 0.0
+    for c, (s, e) in enumerate(chunks):
+        src = [torch.from_numpy(np.ascontiguousarray(Y[s:e], np.float32))]
+        act_ref, probs_ref = eend_ref.infer_full(to_torch(sd_np), cfg, src, [perms[c]])
+        a = acts[c].cpu().numpy().astype(np.float64)
+        r = act_ref[0].numpy().astype(np.float64)
+        d = np.abs(a - r)
+        dmax, dsum, cnt = max(dmax, float(d.max())), dsum + float(d.sum()), cnt + d.size
+        flips += int(((a > 0.5) != (r > 0.5)).sum())
+        pmax = max(pmax, float(np.abs(probs[c].numpy() - np.asarray(probs_ref[0])).max()))
+    return {"chunks_compared": len(chunks), "frames_compared": int(sum(e - s for s, e in chunks)),
+            "max_abs_diff": dmax, "mean_abs_diff": dsum / max(cnt, 1), "decision_flips_at_0.5": flips,
+            "decisions": cnt, "attractor_prob_max_abs_diff": pmax,
+            "reference": "oracle/eend_ref.py infer_full (fp32 torch-CPU, librosa-restated frontend), same randperms"}
 
 
 def tss_cpu_baseline(meeting, plan, wl, n_win=8):
@@ -815,16 +861,17 @@ def tss_cpu_baseline(meeting, plan, wl, n_win=8):
 
 
 def main_stream(a, wl):
-    """C5 latency mode: one recording per GPU streamed chunk by chunk through the C ABI
-    (sd_fseend_stream_push on device feature rows); every push is synchronised, as a
-    live caller waiting for each chunk's scores would be.  value = 10 ms frames/s of the
-    streamed recording (N replicas: summed); per-chunk latency percentiles alongside.
-    Chunks are whole model frames: FS-EEND's model frame is 100 ms (8 kHz, hop 80,
-    subsampling 10), so BASELINE's 80 ms push is not realisable; 1 frame = 100 ms."""
+    """C5 latency mode: one recording per GPU streamed through the C ABI as it would arrive live.
+    Default: raw 8 kHz audio in BASELINE C5's 80 ms pushes (640 samples, sd_fseend_stream_push_audio):
+    each model frame's STFT / logmel / splice (fs_eend/dataset.py:217-223, feature.py:130-184) runs inside
+    the encoder chunk's captured hipGraph; a push returns 0 or 1 final frame (a model frame is 100 ms, its
+    score is final 9 frames later).  `--feature-rows` pushes precomputed feature rows instead (model only).
+    Every push is synchronised, as a live caller waiting for its scores would be.  value = 10 ms frames/s
+    of the streamed recording (N replicas: summed); per-push latency percentiles alongside."""
     import ctypes
     import torch
     from speaker_diarization_amd import _lib
-    from speaker_diarization_amd.feature import eend_features
+    from speaker_diarization_amd.feature import _mel_device, eend_features
     from speaker_diarization_amd.fs_eend.model import OnlineTransformerDADiarization
     from speaker_diarization_amd.synth import make_meeting
     from speaker_diarization_amd.weights import FSEENDConfig, fseend_state_dict, to_torch
@@ -832,11 +879,13 @@ def main_stream(a, wl):
     world, rank, dev = dist_setup()
     minutes = a.minutes if a.minutes is not None else wl["minutes"]
     chunk = a.chunk or wl["chunk"]
+    audio = not a.feature_rows
     meeting = make_meeting(minutes * 60.0, n_spk=wl["n_spk"], seed=777 + rank, sample_rate=8000)
     wav = torch.from_numpy(meeting.wav.astype(np.float32)).to(dev)
+    sd_np = fseend_state_dict(FSEENDConfig(), seed=777)
     m = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=a.precision,
                                        max_seqs=1, max_frames=64, max_nspks=6)
-    m.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(), seed=777)))
+    m.load_state_dict(to_torch(sd_np))
     feats = eend_features(wav, 8000, 200, 80, "logmel23", 7, 10, ld=m.in_ld).contiguous()
     T = feats.shape[0]
     lib = _lib.load()
@@ -846,20 +895,35 @@ def main_stream(a, wl):
     sp = _lib.stream_ptr(dev)
     cnt = ctypes.c_int()
     base, row_bytes = feats.data_ptr(), m.in_ld * 4
+    fb = _mel_device(8000, 256, dev)
+    push_samples = a.push_samples
     lat = []
 
     def step(record):
         lib.sd_fseend_stream_reset(s, sp)
         out = 0
-        for i in range(0, T, chunk):
-            n = min(chunk, T - i)
-            t0 = time.perf_counter()
-            _lib.check(lib.sd_fseend_stream_push(s, base + i * row_bytes, m.in_ld, n, preds.data_ptr() + out * 24,
-                                                 preds.shape[0] - out, ctypes.byref(cnt), sp))
-            torch.cuda.synchronize()
-            if record:
-                lat.append(time.perf_counter() - t0)
-            out += cnt.value
+        if audio:
+            _lib.call("sd_fseend_stream_set_audio", s, fb.data_ptr(), 23, 200, 80, 7, 10)
+            n = wav.numel()
+            for i in range(0, n, push_samples):
+                k = min(push_samples, n - i)
+                t0 = time.perf_counter()
+                _lib.check(lib.sd_fseend_stream_push_audio(s, wav.data_ptr() + 4 * i, k, preds.data_ptr() + out * 24,
+                                                           preds.shape[0] - out, ctypes.byref(cnt), sp))
+                torch.cuda.synchronize()
+                if record:
+                    lat.append(time.perf_counter() - t0)
+                out += cnt.value
+        else:
+            for i in range(0, T, chunk):
+                n = min(chunk, T - i)
+                t0 = time.perf_counter()
+                _lib.check(lib.sd_fseend_stream_push(s, base + i * row_bytes, m.in_ld, n, preds.data_ptr() + out * 24,
+                                                     preds.shape[0] - out, ctypes.byref(cnt), sp))
+                torch.cuda.synchronize()
+                if record:
+                    lat.append(time.perf_counter() - t0)
+                out += cnt.value
         _lib.check(lib.sd_fseend_stream_flush(s, preds.data_ptr() + out * 24, preds.shape[0] - out,
                                               ctypes.byref(cnt), sp))
         torch.cuda.synchronize()
@@ -867,38 +931,71 @@ def main_stream(a, wl):
 
     elapsed, _ = timed(lambda: step(True), a.warmup, a.steps, world, dev)
     lat[:] = lat[-(len(lat) // (a.warmup + a.steps)) * a.steps:]   # timed steps only
-    # parity spot check of this very run against the whole-recording forward of the first
-    # 2000 frames (its last 9 frames see zero look-ahead there, so they are not compared)
+    # parity of this very run: against the whole-recording GPU test() on the same features, and against
+    # the fp32 CPU oracle (oracle/fseend_ref.py test() on oracle/eend_ref.py features) over the first frames
     Tc = min(T, 2000)
     m2 = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, precision=a.precision,
                                         max_seqs=1, max_frames=Tc, max_nspks=6)
-    m2.load_state_dict(to_torch(fseend_state_dict(FSEENDConfig(), seed=777)))
+    m2.load_state_dict(to_torch(sd_np))
     full, _, _ = m2.test_device(feats[None, :Tc], [Tc], 6, want_emb=False, want_attractors=False)
-    nc = Tc - 9 if Tc < T else Tc
+    nc = Tc - 9 if Tc < T else Tc     # the truncated reference sees no look-ahead for its last 9 frames
     err = float((full[0, :nc] - preds[:nc]).abs().max())
+    parity = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        parity = fseend_oracle_parity(meeting, sd_np, preds[:T], frames=min(T, 1000))
     lib.sd_fseend_stream_destroy(s)
     L = np.array(lat) * 1e3
     frames = meeting.wav.size // 80 * world
     if rank == 0:
+        unit_ms = push_samples / 8.0 if audio else chunk * 100
         line = {"metric": "diarized frames/sec (10 ms hop)", "value": round(frames * a.steps / elapsed, 1),
                 "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(elapsed / a.steps * 1000.0, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
                 "data": "synthetic 8 kHz recording (speaker_diarization_amd/synth.py), seeded random weights",
-                "config": {"workload": wl["desc"], "minutes_per_gpu": minutes, "chunk_frames": chunk,
-                           "chunk_audio_ms": chunk * 100, "model_frames": T,
+                "config": {"workload": wl["desc"], "minutes_per_gpu": minutes, "input": "audio" if audio else
+                           "feature rows", "push_audio_ms": unit_ms, "push_samples": push_samples if audio else None,
+                           "chunk_frames": chunk, "model_frames": T, "pushes_per_step": len(L) // max(a.steps, 1),
                            "hipgraph": not a.no_graph,
                            "parallelism": "replicas x%d" % world if world > 1 else "1 GPU"},
-                "latency_ms": {"p50": round(float(np.percentile(L, 50)), 4),
+                "latency_ms": {"per": "push of %.0f ms of audio incl. frontend" % unit_ms if audio else
+                               "push of %d model frame(s), model only" % chunk,
+                               "p50": round(float(np.percentile(L, 50)), 4),
                                "p90": round(float(np.percentile(L, 90)), 4),
                                "p99": round(float(np.percentile(L, 99)), 4),
                                "max": round(float(L.max()), 4), "mean": round(float(L.mean()), 4)},
-                "real_time_factor": round(float(L.mean()) / (chunk * 100.0), 5),
-                "max_abs_diff_vs_test": err}
+                "real_time_factor": round(float(L.mean()) / unit_ms, 5),
+                "max_abs_diff_vs_test": err, "parity": parity}
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = fseend_cpu_baseline(meeting, sd_np, a.cpu_seconds)
+            line["speedup_vs_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
         print(json.dumps(line))
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def fseend_oracle_parity(meeting, sd_np, gpu_scores, frames=1000):
+    """FS-EEND scores (fs_eend.py:79-96; activity = score > 0, i.e. sigmoid > 0.5, loss.py:214) of the
+    product path vs the fp32 CPU oracle (oracle/eend_ref.py frontend + oracle/fseend_ref.py test()) on the
+    first `frames` model frames of the same recording (the oracle sees only those frames, so its last 9
+    lack their look-ahead and are not compared)."""
+    import torch
+    from oracle import eend_ref, fseend_ref
+    from speaker_diarization_amd.weights import FSEENDConfig, to_torch
+    torch.set_num_threads(host_threads())
+    Y = eend_ref.features(meeting.wav[: frames * 800 + 700].astype(np.float64), 8000, 200, 80, 7, 10, "logmel23")
+    Tn = min(frames, len(Y))
+    x = torch.from_numpy(np.ascontiguousarray(Y[:Tn], np.float32))[None]
+    with torch.no_grad():
+        ro = fseend_ref.fseend_test(to_torch(sd_np), FSEENDConfig(), x, [Tn], 6)[0][0].numpy()
+    n = Tn - 9
+    g = gpu_scores[:n].float().cpu().numpy()
+    c = ro[:n]
+    d = np.abs(g.astype(np.float64) - c)
+    return {"frames_compared": int(n), "slots": int(g.shape[1]), "max_abs_diff": float(d.max()),
+            "mean_abs_diff": float(d.mean()), "decision_flips_at_0": int(((g > 0) != (c > 0)).sum()),
+            "decisions": int(g.size), "reference": "oracle/fseend_ref.py test() on oracle/eend_ref.py features, fp32"}
 
 
 if __name__ == "__main__":

@@ -286,6 +286,21 @@ int sd_fseend_stream_create(sd_fseend* h, int chunk, int max_frames, int max_nsp
  * preds: device (cap, max_nspks) f32; *n_out = frames whose scores were written. */
 int sd_fseend_stream_push(sd_fseend_stream* s, const float* feats, int ld_feats, int n, float* preds, int cap,
                           int* n_out, void* stream);
+/* Audio input instead of feature rows (latency mode from raw audio): the FS-EEND frontend of
+ * fs_eend/dataset.py:217-223 (transform 'logmel23' at the hardcoded 8 kHz: frame_size 200, frame_shift 80,
+ * n_fft 256, 23 mels, no CMN) + feature.splice (context_size 7) + [::subsampling 10] (feature.py:130-184)
+ * computed incrementally on the device: each chunk's STFT frames, logmel and spliced rows run inside its
+ * captured encoder graph, reading the stream's audio history at the device cursor.  mel_fb: device
+ * (n_mels, n_fft/2 + 1) f32 (librosa.filters.mel, Slaney), kept by pointer.  Call on a fresh or reset
+ * stream; reset() returns the stream to feature rows.  push_audio: n samples (device f32, any n >= 0,
+ * e.g. 640 = 80 ms); a model frame (100 ms) is encoded once its last spliced STFT frame has all its
+ * samples, and scored 9 frames later (look-ahead); flush() then knows the length (feature.stft's frame
+ * count, feature.py:176-184) and finishes.  The rows equal eend_features() of the whole recording bit
+ * for bit, so the scores equal sd_fseend_test on them (as for feature pushes). */
+int sd_fseend_stream_set_audio(sd_fseend_stream* s, const float* mel_fb, int n_mels, int frame_size, int frame_shift,
+                               int context_size, int subsampling);
+int sd_fseend_stream_push_audio(sd_fseend_stream* s, const float* samples, int64_t n, float* preds, int cap,
+                                int* n_out, void* stream);
 int sd_fseend_stream_flush(sd_fseend_stream* s, float* preds, int cap, int* n_out, void* stream);
 int sd_fseend_stream_reset(sd_fseend_stream* s, void* stream);
 int64_t sd_fseend_stream_device_bytes(const sd_fseend_stream* s);

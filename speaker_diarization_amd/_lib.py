@@ -159,6 +159,8 @@ _SIGS = {
     "sd_fseend_destroy": (c_int, [c_void_p]),
     "sd_fseend_stream_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "sd_fseend_stream_push": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int), c_void_p]),
+    "sd_fseend_stream_set_audio": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int]),
+    "sd_fseend_stream_push_audio": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int, POINTER(c_int), c_void_p]),
     "sd_fseend_stream_flush": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_int), c_void_p]),
     "sd_fseend_stream_reset": (c_int, [c_void_p, c_void_p]),
     "sd_fseend_stream_device_bytes": (c_int64, [c_void_p]),

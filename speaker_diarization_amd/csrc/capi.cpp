@@ -322,6 +322,22 @@ int sd_fseend_stream_push(sd_fseend_stream* s, const float* feats, int ld_feats,
   });
 }
 
+int sd_fseend_stream_set_audio(sd_fseend_stream* s, const float* mel_fb, int n_mels, int frame_size, int frame_shift,
+                               int context_size, int subsampling) {
+  return guard([&] {
+    SD_CHECK(s, sd::kErrInvalid, "null handle");
+    s->s->set_audio(mel_fb, n_mels, frame_size, frame_shift, context_size, subsampling);
+  });
+}
+
+int sd_fseend_stream_push_audio(sd_fseend_stream* s, const float* samples, int64_t n, float* preds, int cap,
+                                int* n_out, void* stream) {
+  return guard([&] {
+    SD_CHECK(s && n_out, sd::kErrInvalid, "null argument");
+    *n_out = s->s->push_audio(samples, n, preds, cap, S(stream));
+  });
+}
+
 int sd_fseend_stream_flush(sd_fseend_stream* s, float* preds, int cap, int* n_out, void* stream) {
   return guard([&] {
     SD_CHECK(s && n_out, sd::kErrInvalid, "null argument");

@@ -32,11 +32,16 @@ constexpr int kMaxMels = 64;
 // computed) and each mel filter's nonzero bin range, so the projection runs over ~20 bins instead of
 // BINS (the skipped terms are exact zeros: same sums, same order).  The butterfly stages of a frame
 // belong to its wave alone, so they are ordered by a wave barrier, not a workgroup barrier.
-template <int LOG2N>
+// STREAM: the streaming frontend (sd_fseend_stream_push_audio) — local frame f is global frame
+// f + frame0 with frame0 = cursor[0] * sub - context (the first frame a chunk's splice reads) and the
+// sample bound min(n_samples, bound[0]) read from device memory, so one captured graph serves every
+// chunk; the arithmetic per global frame is the whole-recording kernel's, bit for bit.
+template <int LOG2N, bool STREAM>
 __global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                           int n_frames, int hop, int win_len,
                                                           const float* __restrict__ mel_fb, int n_mels,
-                                                          double* __restrict__ out) {
+                                                          double* __restrict__ out, const int* __restrict__ cursor,
+                                                          const int* __restrict__ bound, int sub, int context) {
   constexpr int N = 1 << LOG2N;
   constexpr int BINS = N / 2 + 1;
   constexpr int FPB = 8;
@@ -76,7 +81,12 @@ __global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restric
   // Frame f covers padded samples [f*hop, f*hop + N) of the wav zero-padded by N/2;
   // the periodic Hann window of win_len sits at offset (N - win_len)/2.
   const int lpad = (N - win_len) / 2;
-  const int64_t base = (int64_t)f * hop - N / 2 + lpad;
+  int64_t fg = f;
+  if constexpr (STREAM) {
+    fg += (int64_t)cursor[0] * sub - context;
+    n_samples = min(n_samples, (int64_t)bound[0]);
+  }
+  const int64_t base = fg * hop - N / 2 + lpad;
   __syncthreads();   // window table
   for (int n = lane; n < N; n += 64) {
     double v = 0.0;
@@ -154,6 +164,29 @@ __global__ __launch_bounds__(256) void splice_kernel(const double* __restrict__ 
   }
 }
 
+// Streaming splice: row r is model frame i = cursor[0] + r, built from the chunk's logmel frames
+// (local frame = global frame - (cursor[0] * sub - context)); frames outside [0, bound[1]) are the splice's
+// zero padding and rows of model frames >= ceil(bound[1] / sub) (past the end of the input) are zero.
+__global__ __launch_bounds__(128) void splice_stream_kernel(const double* __restrict__ lm, int n_mels, int context,
+                                                            int sub, const int* __restrict__ cursor,
+                                                            const int* __restrict__ bound, float* __restrict__ out,
+                                                            int ld_out) {
+  const int r = blockIdx.x;
+  const int i = cursor[0] + r;
+  const int nf = bound[1];
+  const bool row_live = (int64_t)i * sub < (int64_t)nf;
+  const int width = (2 * context + 1) * n_mels;
+  for (int e = threadIdx.x; e < ld_out; e += blockDim.x) {
+    float v = 0.f;
+    if (row_live && e < width) {
+      const int c = e / n_mels, m = e % n_mels;
+      const int64_t fgl = (int64_t)i * sub + c - context;
+      if (fgl >= 0 && fgl < nf) v = (float)lm[(int64_t)(r * sub + c) * n_mels + m];
+    }
+    out[(int64_t)r * ld_out + e] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ x, int T, int D,
                                                           const int* __restrict__ perm,
                                                           const int* __restrict__ lengths,
@@ -220,11 +253,33 @@ void stft_logmel(const float* wav, int64_t n_samples, int n_frames, int n_fft, i
                  4.0 * (double)n_frames * hop + 8.0 * n_frames * n_mels, st);
   const dim3 grid(cdiv(n_frames, 8));
   if (n_fft == 512)
-    hipLaunchKernelGGL(stft_logmel_kernel<9>, grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
-                       mel_fb, n_mels, out);
+    hipLaunchKernelGGL((stft_logmel_kernel<9, false>), grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
+                       mel_fb, n_mels, out, nullptr, nullptr, 0, 0);
   else
-    hipLaunchKernelGGL(stft_logmel_kernel<8>, grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
-                       mel_fb, n_mels, out);
+    hipLaunchKernelGGL((stft_logmel_kernel<8, false>), grid, dim3(512), 0, st, wav, n_samples, n_frames, hop, win_len,
+                       mel_fb, n_mels, out, nullptr, nullptr, 0, 0);
+  SD_LAUNCH_CHECK();
+}
+
+void stream_frontend(const float* wav, int64_t cap_samples, int rows, int n_fft, int hop, int win_len,
+                     const float* mel_fb, int n_mels, int context, int sub, const int* cursor, const int* bound,
+                     double* lm, float* out, int ld_out, hipStream_t st) {
+  SD_CHECK(n_fft == 256 || n_fft == 512, kErrInvalid, "stream frontend: n_fft must be 256 or 512");
+  SD_CHECK(win_len > 0 && win_len <= n_fft && hop > 0, kErrInvalid, "stream frontend: bad frame_size/frame_shift");
+  SD_CHECK(n_mels > 0 && n_mels <= kMaxMels, kErrInvalid, "stream frontend: n_mels out of range");
+  SD_CHECK(ld_out >= (2 * context + 1) * n_mels, kErrInvalid, "stream frontend: ld_out < spliced width");
+  const int n_frames = (rows - 1) * sub + 2 * context + 1;   // logmel frames the chunk's splice reads
+  ProfScope prof("stream_frontend", 5.0 * n_fft * std::log2((double)n_fft) * n_frames,
+                 4.0 * (double)n_frames * hop + 4.0 * rows * ld_out, st);
+  const dim3 grid(cdiv(n_frames, 8));
+  if (n_fft == 512)
+    hipLaunchKernelGGL((stft_logmel_kernel<9, true>), grid, dim3(512), 0, st, wav, cap_samples, n_frames, hop,
+                       win_len, mel_fb, n_mels, lm, cursor, bound, sub, context);
+  else
+    hipLaunchKernelGGL((stft_logmel_kernel<8, true>), grid, dim3(512), 0, st, wav, cap_samples, n_frames, hop,
+                       win_len, mel_fb, n_mels, lm, cursor, bound, sub, context);
+  hipLaunchKernelGGL(splice_stream_kernel, dim3(rows), dim3(128), 0, st, lm, n_mels, context, sub, cursor, bound, out,
+                     ld_out);
   SD_LAUNCH_CHECK();
 }
 

@@ -4,6 +4,7 @@
 #include "fseend_stream.h"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 
 namespace sd {
@@ -120,6 +121,8 @@ void FsEendStream::enc_chunk(hipStream_t st) {
   const FsEendModel& m = m_;
   const int D = m.cfg_.n_units, nh = m.cfg_.n_heads, c = c_;
   const Tens qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
+  if (audio_)   // the chunk's feature rows from the audio history, at the encoder cursor
+    stream_frontend(aud_, aud_cap_, c, nfft_, hop_, fsz_, fb_, n_mels_, ctx_, sub_, state_, bound_, lm_, F_, m.in_ld_, st);
   conv_gemm(lin(Tens{F_, false}, c, m.in_ld_, m.in_.w, m.in_.beta, Tens{Y_, false}, D), bf_, st);
   float* xb[2] = {X_, X2_};
   int xi = 0;
@@ -257,6 +260,7 @@ int FsEendStream::emit(float* preds, int cap, int rows, hipStream_t st) {
 }
 
 int FsEendStream::push(const float* feats, int ld, int n, float* preds, int cap, hipStream_t st) {
+  SD_CHECK(!audio_, kErrState, "stream takes audio (push_audio); reset() it to push feature rows");
   SD_CHECK(!closed_, kErrState, "stream input already ended (partial chunk or flush); call reset()");
   SD_CHECK(n >= 1 && n <= c_, kErrInvalid, "push: 1..chunk frames");
   SD_CHECK(feats && ld >= m_.in_ld_, kErrInvalid, "push: feature row stride below the input stride");
@@ -265,6 +269,57 @@ int FsEendStream::push(const float* feats, int ld, int n, float* preds, int cap,
                           (size_t)m_.in_ld_ * sizeof(float), n, hipMemcpyDeviceToDevice, st));
   if (n < c_) SD_HIP(hipMemsetAsync(F_ + (size_t)n * m_.in_ld_, 0, (size_t)(c_ - n) * m_.in_ld_ * sizeof(float), st));
   run(0, st);
+  return after_enc(n, preds, cap, st);
+}
+
+void FsEendStream::set_audio(const float* mel_fb, int n_mels, int frame_size, int frame_shift, int context, int sub) {
+  SD_CHECK(n_enc_ == 0 && n_samp_ == 0 && !closed_, kErrState, "set_audio: call on a fresh or reset stream");
+  SD_CHECK(mel_fb && n_mels >= 1 && frame_size >= 1 && frame_shift >= 1 && context >= 0 && sub >= 1, kErrInvalid,
+           "set_audio: bad frontend geometry");
+  SD_CHECK((2 * context + 1) * n_mels <= m_.in_ld_ && (2 * context + 1) * n_mels == m_.cfg_.in_size, kErrInvalid,
+           "set_audio: spliced width does not match the model's in_size");
+  const int nfft = 1 << (32 - __builtin_clz((unsigned)(frame_size - 1)));
+  SD_CHECK(nfft == 256 || nfft == 512, kErrInvalid, "set_audio: n_fft must be 256 or 512");
+  fb_ = mel_fb; n_mels_ = n_mels; fsz_ = frame_size; hop_ = frame_shift; nfft_ = nfft; ctx_ = context; sub_ = sub;
+  if (!aud_) {
+    aud_cap_ = (int64_t)cap_ * sub * frame_shift + nfft;
+    aud_ = wsb<float>((size_t)aud_cap_);
+    lm_ = wsb<double>((size_t)((c_ - 1) * sub + 2 * context + 1) * n_mels);
+    bound_ = wsb<int>(2);
+  }
+  const int open_bound[2] = {INT_MAX, INT_MAX};
+  SD_HIP(hipMemcpy(bound_, open_bound, sizeof(open_bound), hipMemcpyHostToDevice));
+  // the encoder graph now starts with the frontend: capture it anew
+  if (exec_[0]) (void)hipGraphExecDestroy(exec_[0]);
+  if (graph_[0]) (void)hipGraphDestroy(graph_[0]);
+  exec_[0] = nullptr; graph_[0] = nullptr; ran_direct_[0] = false;
+  audio_ = true;
+}
+
+int FsEendStream::push_audio(const float* samples, int64_t n, float* preds, int cap, hipStream_t st) {
+  SD_CHECK(audio_, kErrState, "push_audio: the stream has no audio frontend (set_audio)");
+  SD_CHECK(!closed_, kErrState, "stream input already ended (flush); call reset()");
+  SD_CHECK(n >= 0 && (samples || n == 0), kErrInvalid, "push_audio: bad sample buffer");
+  SD_CHECK(n_samp_ + n <= aud_cap_ - nfft_, kErrInvalid, "stream exceeds max_frames");
+  if (n > 0)
+    SD_HIP(hipMemcpyAsync(aud_ + n_samp_, samples, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st));
+  n_samp_ += n;
+  // STFT frame j is final once the last sample its window reads, j hop + reach - 1 (the window of
+  // frame_size sits at (n_fft - frame_size) / 2 in the centred n_fft frame), has arrived — such frames are
+  // frames of the input whatever its final length; model frame i once its last spliced frame i sub + context is
+  const int64_t reach = (nfft_ - fsz_) / 2 + fsz_ - nfft_ / 2;
+  const int64_t n_stft = n_samp_ >= reach ? (n_samp_ - reach) / hop_ + 1 : 0;
+  const int64_t n_model = n_stft >= ctx_ + 1 ? (n_stft - ctx_ - 1) / sub_ + 1 : 0;
+  int out = 0;
+  while (n_model - n_enc_ >= c_) {
+    SD_CHECK(n_enc_ + c_ <= cap_, kErrInvalid, "stream exceeds max_frames");
+    run(0, st);
+    out += after_enc(c_, preds ? preds + (size_t)out * C_ : nullptr, cap - out, st);
+  }
+  return out;
+}
+
+int FsEendStream::after_enc(int n, float* preds, int cap, hipStream_t st) {
   n_enc_ += c_;
   n_valid_ = n_enc_ - c_ + n;
   if (n < c_) {
@@ -281,8 +336,25 @@ int FsEendStream::push(const float* feats, int ld, int n, float* preds, int cap,
 }
 
 int FsEendStream::flush(float* preds, int cap, hipStream_t st) {
-  closed_ = true;
   int out = 0;
+  if (audio_ && !closed_) {
+    // the input length is known now: feature.stft's frame count (the last frame dropped when the length
+    // is a multiple of the hop, feature.py:176-184), [::sub] rows; the remaining chunks see zero samples
+    // past the end and zero splice rows past the last frame, exactly as the whole-recording frontend
+    const int64_t nf = n_samp_ < 1 ? 0 : 1 + n_samp_ / hop_ - (n_samp_ % hop_ == 0 ? 1 : 0);
+    const int64_t n_rows = (nf + sub_ - 1) / sub_;
+    const int b[2] = {(int)n_samp_, (int)nf};
+    SD_HIP(hipMemcpyAsync(bound_, b, sizeof(b), hipMemcpyHostToDevice, st));
+    SD_HIP(hipStreamSynchronize(st));   // b lives on this stack frame
+    while (n_enc_ < n_rows) {
+      SD_CHECK(n_enc_ + c_ <= cap_, kErrInvalid, "stream exceeds max_frames");
+      const int n = (int)std::min<int64_t>(c_, n_rows - n_enc_);
+      run(0, st);
+      out += after_enc(n, preds ? preds + (size_t)out * C_ : nullptr, cap - out, st);
+      if (n < c_) break;
+    }
+  }
+  closed_ = true;
   while (n_dec_ < n_valid_) {
     run(1, st);
     const int rows = std::min(c_, n_valid_ - n_dec_);
@@ -296,6 +368,13 @@ void FsEendStream::reset(hipStream_t st) {
   SD_HIP(hipMemsetAsync(state_, 0, 4 * sizeof(int), st));
   n_enc_ = n_valid_ = n_dec_ = n_out_ = 0;
   closed_ = false;
+  if (audio_) {   // back to feature rows until set_audio() again (the next capture rebuilds the encoder graph)
+    audio_ = false;
+    n_samp_ = 0;
+    if (exec_[0]) (void)hipGraphExecDestroy(exec_[0]);
+    if (graph_[0]) (void)hipGraphDestroy(graph_[0]);
+    exec_[0] = nullptr; graph_[0] = nullptr; ran_direct_[0] = false;
+  }
 }
 
 }  // namespace sd

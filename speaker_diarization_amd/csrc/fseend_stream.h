@@ -25,6 +25,13 @@ class FsEendStream {
   // Writes the scores of every frame that became final to preds (device, rows of C, capacity
   // cap rows) and returns their number.
   int push(const float* feats, int ld, int n, float* preds, int cap, hipStream_t st);
+  // Audio input (fs_eend/dataset.py:217-223 + feature.py:130-184: centred STFT, logmel, splice ±context,
+  // [::sub]) instead of feature rows: configure once on a fresh or reset stream (mel_fb: device
+  // (n_mels, n_fft/2 + 1) f32, the librosa Slaney basis), then push_audio() any number of samples.  Each
+  // chunk's frontend runs inside its captured encoder graph; the rows are the ones eend_features() computes
+  // for the whole recording, bit for bit.
+  void set_audio(const float* mel_fb, int n_mels, int frame_size, int frame_shift, int context, int sub);
+  int push_audio(const float* samples, int64_t n, float* preds, int cap, hipStream_t st);
   // Ends the input (if not already) and emits the remaining frames.
   int flush(float* preds, int cap, hipStream_t st);
   void reset(hipStream_t st);
@@ -35,6 +42,7 @@ class FsEendStream {
 
  private:
   void enc_chunk(hipStream_t st);
+  int after_enc(int n, float* preds, int cap, hipStream_t st);   // cursor bookkeeping + decoder chunks
   void dec_chunk(hipStream_t st);
   void run(int which, hipStream_t st);   // 0 encoder, 1 decoder: graph replay or direct launches
   int emit(float* preds, int cap, int rows, hipStream_t st);
@@ -58,6 +66,14 @@ class FsEendStream {
   // histories
   std::vector<void*> kv_enc_, kv_dec_;
   float* hist_ = nullptr;
+  // audio frontend (set_audio)
+  bool audio_ = false;
+  const float* fb_ = nullptr;
+  int n_mels_ = 0, fsz_ = 0, hop_ = 0, nfft_ = 0, ctx_ = 0, sub_ = 0;
+  float* aud_ = nullptr;               // every sample of the stream (the frontend reads its window by cursor)
+  int64_t aud_cap_ = 0, n_samp_ = 0;
+  double* lm_ = nullptr;               // the chunk's logmel frames
+  int* bound_ = nullptr;               // [0] samples, [1] STFT frames of the input (INT_MAX while open)
   // graphs
   hipStream_t cap_st_ = nullptr;
   hipGraph_t graph_[2] = {nullptr, nullptr};

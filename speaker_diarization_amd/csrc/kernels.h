@@ -362,6 +362,14 @@ void bf16_to_f32(const void* x, int64_t n, float* y, hipStream_t st);
 // librosa-style centred STFT (float64) -> log10 mel power: out (n_frames, n_mels) float64.
 void stft_logmel(const float* wav, int64_t n_samples, int n_frames, int n_fft, int hop, int win_len,
                  const float* mel_fb /*(n_mels, n_fft/2+1)*/, int n_mels, double* out, hipStream_t st);
+// Streaming frontend of one FS-EEND chunk (sd_fseend_stream_push_audio): the logmel frames the splice of
+// model frames [cursor[0], cursor[0] + rows) reads (frame0 = cursor[0] * sub - context, (rows - 1) * sub +
+// 2 context + 1 frames into lm), then the spliced rows into out (rows, ld_out).  bound (device int[2]):
+// [0] samples of the input (INT_MAX while open), [1] STFT frames of the input (INT_MAX while open).
+// Per frame the arithmetic of stft_logmel + splice_subsample, bit for bit.
+void stream_frontend(const float* wav, int64_t cap_samples, int rows, int n_fft, int hop, int win_len,
+                     const float* mel_fb, int n_mels, int context, int sub, const int* cursor, const int* bound,
+                     double* lm, float* out, int ld_out, hipStream_t st);
 void col_mean(const double* x, int rows, int cols, double* mean, hipStream_t st);
 // out (n_out, ld_out) f32: row r = splice of frame r*sub (±context, zero pad), minus mean (nullable).
 void splice_subsample(const double* lm, int n_frames, int n_mels, const double* mean, int context, int sub,

@@ -165,11 +165,42 @@ class FsEendStream:
         self._pending = data[full:]
         return torch.cat(outs, 0) if outs else self._out[:0].clone()
 
+    def set_audio(self, sample_rate: int = 8000, frame_size: int = 200, frame_shift: int = 80,
+                  context_size: int = 7, subsampling: int = 10):
+        """Take raw audio from now on (push_audio): the FS-EEND frontend of fs_eend/dataset.py:217-223
+        (transform 'logmel23', sr hardcoded 8000) + splice + subsample, incrementally on the device
+        inside each chunk's captured graph.  Valid on a fresh or reset() stream."""
+        from ..feature import _mel_device
+        n_fft = 1 << (frame_size - 1).bit_length()
+        self._fb = _mel_device(sample_rate, n_fft, self.device)
+        _lib.call("sd_fseend_stream_set_audio", self._s, _lib.ptr(self._fb), self._fb.shape[0], frame_size,
+                  frame_shift, context_size, subsampling)
+        self._hop_rows = frame_shift * subsampling       # samples per model frame
+        self._audio = True
+        return self
+
+    def _ensure_out(self, rows: int):
+        if self._out.shape[0] < rows:
+            self._out = torch.empty(rows, self.C, device=self.device, dtype=torch.float32)
+
+    def push_audio(self, samples) -> torch.Tensor:
+        """samples: 1-D float32 audio at the frontend's rate (any length, e.g. 640 = 80 ms) ->
+        the (m, C) scores of the frames that became final."""
+        if not getattr(self, "_audio", False):
+            raise RuntimeError("push_audio: call set_audio() first")
+        x = samples.to(self.device, torch.float32).reshape(-1).contiguous()
+        self._ensure_out(x.numel() // self._hop_rows + 2 * (self.chunk + 10))
+        cnt = ctypes.c_int()
+        _lib.call("sd_fseend_stream_push_audio", self._s, _lib.ptr(x) if x.numel() else None, x.numel(),
+                  _lib.ptr(self._out), self._out.shape[0], ctypes.byref(cnt), _lib.stream_ptr(self.device))
+        return self._out[: cnt.value].clone()
+
     def flush(self) -> torch.Tensor:
         outs = []
         if self._pending.shape[0] > 0:
             outs.append(self._push_rows(self._pending))
             self._pending = self._pending[:0]
+        self._ensure_out(4 * (self.chunk + 10))
         cnt = ctypes.c_int()
         _lib.call("sd_fseend_stream_flush", self._s, _lib.ptr(self._out), self._out.shape[0], ctypes.byref(cnt),
                   _lib.stream_ptr(self.device))
@@ -177,7 +208,9 @@ class FsEendStream:
         return torch.cat(outs, 0)
 
     def reset(self):
+        """Back to an empty stream taking feature rows (set_audio() again for audio)."""
         self._pending = self._pending[:0]
+        self._audio = False
         _lib.call("sd_fseend_stream_reset", self._s, _lib.stream_ptr(self.device))
 
     def close(self):

@@ -150,3 +150,101 @@ def test_stream_errors(gpu):
     md = _model(808, max_frames=64, delay=2)
     with pytest.raises(ValueError, match="mask_delay"):
         md.stream(chunk=4)
+
+
+# ----------------------------------------------------------------------------- audio in (latency mode)
+def _wav8k(seconds, seed, extra=0):
+    from speaker_diarization_amd.synth import make_meeting
+    w = make_meeting(seconds, n_spk=3, seed=seed, sample_rate=8000).wav.astype(np.float32)
+    return w[: int(seconds * 8000) + extra] if extra >= 0 else w[: int(seconds * 8000) + extra]
+
+
+def _audio_stream(m, wav, chunk, pieces, precision_graph=True):
+    s = m.stream(chunk=chunk, max_frames=wav.size // 800 + 64, use_graph=precision_graph).set_audio()
+    x = torch.from_numpy(wav).cuda()
+    outs, i, k = [], 0, 0
+    while i < wav.size:
+        p = pieces[k % len(pieces)]
+        outs.append(s.push_audio(x[i : i + p]))
+        i += p
+        k += 1
+    outs.append(s.flush())
+    return torch.cat(outs, 0), s
+
+
+def _whole(m, wav):
+    from speaker_diarization_amd.feature import eend_features
+    f = eend_features(torch.from_numpy(wav).cuda(), 8000, 200, 80, "logmel23", 7, 10, ld=m.in_ld)
+    out, _, _ = m.test_device(f[None], [f.shape[0]], 6, want_emb=False, want_attractors=False)
+    return out[0]
+
+
+@pytest.mark.parametrize("seconds,extra,chunk", [(30.0, 0, 1), (30.0, 37, 4), (12.0, -80 * 3, 7), (25.0, 5, 32)])
+def test_audio_stream_matches_test_fp32(gpu, seconds, extra, chunk):
+    """80 ms pushes (640 samples at 8 kHz) of raw audio == eend_features(whole wav) + test(): lengths
+    with and without the multiple-of-hop last-frame drop (feature.py:176-184), chunks 1..32."""
+    wav = _wav8k(seconds, 90 + chunk, extra)
+    m = _model(811, max_frames=wav.size // 800 + 64)
+    ref = _whole(m, wav)
+    out, _ = _audio_stream(m, wav, chunk, [640])
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.cpu().numpy(), atol=FP32_ATOL)
+
+
+def test_audio_stream_matches_oracle(gpu):
+    """Against the CPU oracle end to end: the restated librosa frontend (fp64) + fs_eend.py test()."""
+    from oracle import eend_ref
+    wav = _wav8k(20.0, 95, 13)
+    m = _model(812, max_frames=400)
+    out, _ = _audio_stream(m, wav, 2, [640, 17, 1300])
+    Y = eend_ref.features(wav.astype(np.float64), 8000, 200, 80, 7, 10, "logmel23")
+    sd = to_torch(fseend_state_dict(FSEENDConfig(), seed=812))
+    ro, _, _ = fseend_ref.fseend_test(sd, FSEENDConfig(), [torch.from_numpy(np.ascontiguousarray(Y, np.float32))],
+                                      [len(Y)], 6)
+    assert out.shape[0] == len(Y)
+    np.testing.assert_allclose(out.cpu().numpy(), ro[0].numpy(), atol=FP32_ATOL)
+
+
+def test_audio_stream_bf16_graph_and_ragged(gpu):
+    """bf16, chunk 1: graph replay == direct launches bit for bit, ragged pushes == 80 ms pushes bit for
+    bit (the frontend rows do not depend on how the audio was cut), and both == test() within bf16."""
+    wav = _wav8k(24.0, 97, 3)
+    m = _model(813, "bf16", max_frames=400)
+    a, _ = _audio_stream(m, wav, 1, [640])
+    b, _ = _audio_stream(m, wav, 1, [640], precision_graph=False)
+    c, _ = _audio_stream(m, wav, 1, [1, 799, 5000, 64, 640 * 7 + 3])
+    assert torch.equal(a, b) and torch.equal(a, c)
+    np.testing.assert_allclose(a.cpu().numpy(), _whole(m, wav).cpu().numpy(), atol=BF16_ATOL)
+
+
+@pytest.mark.parametrize("n", [200, 500, 800, 881, 1600])
+def test_audio_stream_short_inputs(gpu, n):
+    """Shorter than one model frame's look-ahead: everything comes out of flush()."""
+    wav = _wav8k(1.0, 99, 0)[:n]
+    m = _model(814, max_frames=64)
+    out, _ = _audio_stream(m, wav, 4, [640])
+    np.testing.assert_allclose(out.cpu().numpy(), _whole(m, wav).cpu().numpy(), atol=FP32_ATOL)
+
+
+def test_audio_stream_reset_modes_and_errors(gpu):
+    wav = _wav8k(6.0, 98, 0)
+    m = _model(815, max_frames=128)
+    ref = _whole(m, wav).cpu().numpy()
+    s = m.stream(chunk=3, max_frames=128)
+    with pytest.raises(RuntimeError, match="set_audio"):
+        s.push_audio(torch.zeros(10))
+    for _ in range(2):
+        s.set_audio()
+        outs = [s.push_audio(torch.from_numpy(wav[i : i + 640]).cuda()) for i in range(0, wav.size, 640)]
+        np.testing.assert_allclose(torch.cat(outs + [s.flush()]).cpu().numpy(), ref, atol=FP32_ATOL)
+        with pytest.raises(SdiarError, match="ended"):
+            s.push_audio(torch.zeros(10).cuda())
+        s.reset()
+    # back to feature rows after reset: same scores from the whole-recording features
+    from speaker_diarization_amd.feature import eend_features
+    f = eend_features(torch.from_numpy(wav).cuda(), 8000, 200, 80, "logmel23", 7, 10)[:, :345]
+    np.testing.assert_allclose(torch.cat([s.push(f), s.flush()]).cpu().numpy(), ref, atol=FP32_ATOL)
+    s.reset()
+    s.set_audio()
+    with pytest.raises(SdiarError, match="audio"):
+        s._push_rows(f[:3])
