@@ -1,0 +1,426 @@
+// One CAM++ dense layer (CAMDenseTDNNLayer, egs/alimeeting/ts_vad2/cam_pplus_wespeaker.py:127-168 with
+// CAMLayer :79-123) per item in ONE launch, bf16, for items of up to kMaxT frames (C2 / C4 windows,
+// the 6-s enrollment chunks):
+//
+//   h[t, n]   = relu(a2[n] * sum_k W[n][k] relu(s1[k] x[t, k] + h1[k]) + b2[n])   bottleneck (1x1, 128)
+//   ctx[s, n] = mean_t h[t, n] + mean_{t in segment s} h[t, n]                    (seg_len 100, ceil)
+//   gate[s]   = sigmoid(W2 relu(W1 ctx[s] + c1) + c2)
+//   out[t, o] = (sum_{tap, n} Wl[o][tap][n] h[t + (tap - 1) dil, n] + bl[o]) * gate[t / 100, o]
+//
+// written into the dense block's channel slice [cin, cin + 32).  The unfused path ran the bottleneck as
+// a ring GEMM into a (B, T, 128) HBM buffer that the context kernel and the local conv then read back
+// (three launches, 128 channels written and read twice per frame); here the workgroup of an item keeps
+// h in LDS, so HBM sees the item's input rows once and the 32 new channels.
+//
+// Workgroup = one item, 8 waves, one workgroup per CU (121 KiB LDS).
+// Phase 1 (HBM-bound): per 32-deep k-step the item's input rows (one 1-KiB MFMA B-operand fragment per
+// 16-frame tile) and the bottleneck weights (8 fragments, L2-resident, shared by every item) stream
+// HBM/L2 -> LDS by LDS-DMA, lane-linear (conflict-free ds_read_b128), through a 4-slot ring with three
+// k-steps (81 KiB) in flight; the fragments of k-step s + 1 are read from LDS while the MFMAs of k-step s
+// run; BN-ReLU is applied on the way from LDS to the MFMA.  Transposed MFMA (weights as the A operand): a
+// lane ends with 4 consecutive bottleneck channels of one frame -> BN2 + ReLU -> 8-B bf16 stores into the
+// LDS image of h (rows XOR-swizzled by 16-B chunk, zero halo rows for the conv), which takes over the
+// ring's LDS.  The layer weights of phases 2-3 are requested at the end of the GEMM and stay in flight
+// through the epilogue (plain barriers, see below).
+// Phase 2: per-segment channel sums of h (16-B LDS reads, wave shuffles), the k-3 local conv on MFMA from
+// the h image (independent of the gate, so it runs here), then the context and the gate MLP with one
+// output per 8 / 16 lanes.  Phase 3: (conv + bias) x gate, 8-B stores of the new channels.
+// Measured per item (C2, T = 299, s_memrealtime probes): GEMM 13 us (cin 128) .. 40 us (cin 896), epilogue
+// 2.6 us, phase 2 5.8 us, phase 3 0.9 us.
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace sd {
+namespace {
+
+constexpr int kC = 128, kC1 = 64, kC2 = 32;   // bn_channels, reduction 2, growth rate
+constexpr int kSeg = 100;
+constexpr int kMaxDil = 2;
+constexpr int kMaxT = 320;                    // frames per item held in LDS
+constexpr int kMaxSegs = (kMaxT + kSeg - 1) / kSeg;
+constexpr int kHR = kMaxT + 2 * kMaxDil;      // h image rows (halo rows at both ends)
+constexpr int kMaxCin = 1024;
+constexpr int kWaves = 8, kThreads = 64 * kWaves;
+constexpr int kFrag = 512;                    // bf16 per MFMA fragment (1 KiB)
+constexpr int kMaxTT = kMaxT / 16;            // 16-frame tiles
+// ring slot of one k-step: 8 weight fragments (out tiles of 16 channels) then kMaxTT input fragments
+constexpr int kSlot = (8 + kMaxTT) * kFrag;
+constexpr int kNSlot = 4;
+constexpr int kDmaPerWave = 4;
+                // per k-step: the wave's weight fragment + its 3 frame tiles
+constexpr int kRingBytes = kNSlot * kSlot * 2;
+constexpr int kHBytes = kHR * kC * 2;         // h image (after the GEMM, in the ring's LDS)
+// phase-2 scratch after the h image: per wave x segment channel sums, then ctx / hid / gate
+constexpr int kScratchBytes = (kWaves * kMaxSegs * kC + kMaxSegs * (kC + kC1 + kC2)) * 4;
+constexpr int kSshBytes = (2 * kMaxCin + 2 * kC) * 4;   // BN1 scale | shift, BN2 scale | shift
+constexpr size_t kSmemBytes = (size_t)kRingBytes + kSshBytes;
+static_assert(kHBytes + kScratchBytes <= kRingBytes, "h image + phase-2 scratch inside the ring");
+static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// h image: row r = frame r - kMaxDil, 128 channels (one 256-B bank row), 16-B chunk q at q ^ (r & 15)
+__device__ __forceinline__ int h_off(int r, int c) { return r * kC + ((((c >> 3) ^ (r & 15)) << 3) | (c & 7)); }
+
+struct CamDenseArgs {
+  const uint16_t* x;        // (B, T, ld) bf16 dense-block map; input channels [0, cin)
+  int ld, cin, T, dil;
+  const float *s1, *h1;     // BN1 (nonlinear1) folded scale / shift, [cin]
+  const uint16_t* wb;       // bottleneck weights bf16 [128][cin]
+  const float *a2, *b2;     // BN2 (nonlinear2) folded, [128]
+  const uint16_t* wl;       // linear_local bf16 [32][3 * 128], k = tap * 128 + c
+  const float* bl;          // linear_local bias [32] or null
+  const float *w1, *c1, *w2, *c2;   // CAMLayer linear1 (64 x 128) / linear2 (32 x 64) + biases, fp32
+  uint16_t* out;            // channel slice [cin, cin + 32) of the same map (stride ld)
+};
+
+__global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
+  extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
+  uint16_t* ring = sm;                                            // phase 1: [kNSlot][8 + kMaxTT][kFrag]
+  uint16_t* hs = sm;                                              // after it: [kHR][kC] h image
+  float* ssh = reinterpret_cast<float*>(sm + kRingBytes / 2);     // s1 | h1
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const int T = a.T, cin = a.cin, nk = cin / 32;
+  const int n_tt = (T + 15) / 16;
+  const uint16_t* xb = a.x + (int64_t)b * T * a.ld;
+
+  for (int i = tid; i < cin; i += kThreads) {
+    ssh[i] = a.s1[i];
+    ssh[kMaxCin + i] = a.h1[i];
+  }
+  float* ab2 = ssh + 2 * kMaxCin;                                  // BN2 for the epilogue
+  if (tid < kC) {
+    ab2[tid] = a.a2[tid];
+    ab2[kC + tid] = a.b2[tid];
+  }
+
+  // ---- phase 1: bottleneck GEMM.  Wave w owns frame tiles w, w + 8, w + 16 (the third only when
+  // w + 16 < n_tt; its DMA is then a repeat of the second tile's, so every wave issues kDmaPerWave per k-step
+  // and the vmcnt counts are uniform).
+  const bool has3 = w + 16 < n_tt;
+  const int tt2 = has3 ? w + 16 : w + 8;
+  const int tts[3] = {w, w + 8, tt2};
+  const uint16_t* xsrc[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) xsrc[j] = xb + (int64_t)min(tts[j] * 16 + l15, T - 1) * a.ld + 8 * g;
+  const uint16_t* wsrc = a.wb + (int64_t)(w * 16 + l15) * cin + 8 * g;       // weight fragment w
+  // LDS byte addresses for the inline-asm reads below: a compiler-visible ds_read of LDS that an LDS-DMA
+  // writes gets an s_waitcnt vmcnt(0) in front of it (the compiler cannot rule out the alias), which would
+  // drain the whole DMA pipeline every k-step
+  const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)ring) + (uint32_t)lane * 16u;
+  const uint32_t ssh_lds = (uint32_t)reinterpret_cast<uintptr_t>((lds_ptr_t)ssh) + (uint32_t)g * 32u;
+  floatx4 acc[3][8];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) acc[j][ot] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int s) {
+    uint16_t* slot = ring + (s % kNSlot) * kSlot;
+    dma_lds16(wsrc + s * 32, (lds_ptr_t)(slot + w * kFrag));
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      dma_lds16(xsrc[j] + s * 32, (lds_ptr_t)(slot + (8 + tts[j]) * kFrag));
+  };
+  // Software pipeline over k-steps: the LDS fragments of k-step s + 1 are read (asm, no wait) while the
+  // MFMAs of k-step s run from registers; one barrier per k-step certifies both that s + 1 has landed for
+  // every wave and that every wave has its k-step s fragments in registers, which frees slot s % 4 for the
+  // DMAs of k-step s + 4.
+  struct Frags {
+    u32x4_t wf[8], xv[3], sc4[2], sh4[2];
+  };
+  auto read_issue = [&](Frags& f, int s) {
+    const uint32_t sb = ring_lds + (uint32_t)((s % kNSlot) * kSlot * 2);
+    asm volatile(
+        "ds_read_b128 %0, %15\n\t"
+        "ds_read_b128 %1, %15 offset:1024\n\t"
+        "ds_read_b128 %2, %15 offset:2048\n\t"
+        "ds_read_b128 %3, %15 offset:3072\n\t"
+        "ds_read_b128 %4, %15 offset:4096\n\t"
+        "ds_read_b128 %5, %15 offset:5120\n\t"
+        "ds_read_b128 %6, %15 offset:6144\n\t"
+        "ds_read_b128 %7, %15 offset:7168\n\t"
+        "ds_read_b128 %8, %16\n\t"
+        "ds_read_b128 %9, %17\n\t"
+        "ds_read_b128 %10, %18\n\t"
+        "ds_read_b128 %11, %19\n\t"
+        "ds_read_b128 %12, %19 offset:16\n\t"
+        "ds_read_b128 %13, %19 offset:%c20\n\t"
+        "ds_read_b128 %14, %19 offset:%c21"
+        : "=&v"(f.wf[0]), "=&v"(f.wf[1]), "=&v"(f.wf[2]), "=&v"(f.wf[3]), "=&v"(f.wf[4]), "=&v"(f.wf[5]),
+          "=&v"(f.wf[6]), "=&v"(f.wf[7]), "=&v"(f.xv[0]), "=&v"(f.xv[1]), "=&v"(f.xv[2]), "=&v"(f.sc4[0]),
+          "=&v"(f.sc4[1]), "=&v"(f.sh4[0]), "=&v"(f.sh4[1])
+        : "v"(sb), "v"(sb + (uint32_t)((8 + tts[0]) * kFrag * 2)), "v"(sb + (uint32_t)((8 + tts[1]) * kFrag * 2)),
+          "v"(sb + (uint32_t)((8 + tts[2]) * kFrag * 2)), "v"(ssh_lds + (uint32_t)s * 128u), "i"(kMaxCin * 4),
+          "i"(kMaxCin * 4 + 16)
+        : "memory");
+  };
+  // the reads above have landed; the "+v" ties keep every use of f behind this wait
+  auto read_wait = [&](Frags& f) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(f.wf[0]), "+v"(f.wf[1]), "+v"(f.wf[2]), "+v"(f.wf[3]), "+v"(f.wf[4]), "+v"(f.wf[5]),
+                   "+v"(f.wf[6]), "+v"(f.wf[7]), "+v"(f.xv[0]), "+v"(f.xv[1]), "+v"(f.xv[2]), "+v"(f.sc4[0]),
+                   "+v"(f.sc4[1]), "+v"(f.sh4[0]), "+v"(f.sh4[1])
+                 :
+                 : "memory");
+  };
+  auto compute = [&](const Frags& f) {
+    // B operand: BN-ReLU of the lane's 8 input channels s*32 + 8g .. +7 (frame tile tt, frame l15), bf16
+    float sc[8], sh[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sc[u] = __uint_as_float(f.sc4[0][u]); sc[4 + u] = __uint_as_float(f.sc4[1][u]);
+      sh[u] = __uint_as_float(f.sh4[0][u]); sh[4 + u] = __uint_as_float(f.sh4[1][u]);
+    }
+    bf16x8 xf[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const u32x4_t v = f.xv[j];
+      u32x4_t o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float x0 = fmaxf(fmaf(__uint_as_float(v[u] << 16), sc[2 * u], sh[2 * u]), 0.f);
+        const float x1 = fmaxf(fmaf(__uint_as_float(v[u] & 0xffff0000u), sc[2 * u + 1], sh[2 * u + 1]), 0.f);
+        o[u] = pack_bf16x2(x0, x1);
+      }
+      xf[j] = __builtin_bit_cast(bf16x8, o);
+    }
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) {
+      const bf16x8 wfr = __builtin_bit_cast(bf16x8, f.wf[ot]);
+      acc[0][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr, xf[0], acc[0][ot], 0, 0, 0);
+      acc[1][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr, xf[1], acc[1][ot], 0, 0, 0);
+      if (has3) acc[2][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr, xf[2], acc[2][ot], 0, 0, 0);
+    }
+  };
+  // Every barrier of this kernel is a plain s_barrier behind lgkmcnt(0): __syncthreads()' workgroup fence
+  // waits for vmcnt(0), which would drain the ring every k-step, and after the GEMM would stall on the
+  // layer-weight loads that are meant to stay in flight through the epilogue.  A ring slot is in LDS for
+  // every wave after each wave's own counted vmcnt wait + the barrier.
+  auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto step = [&](const Frags& use, Frags& fill, int s) {
+    const bool more = s + 1 < nk;
+    if (more) {
+      if (s + 3 < nk) wait_vm<2 * kDmaPerWave>();      // k-step s + 1 landed: only s + 2, s + 3 are younger
+      else if (s + 2 < nk) wait_vm<kDmaPerWave>();
+      else wait_vm<0>();
+      barrier();
+      if (s + 4 < nk) issue(s + 4);
+      read_issue(fill, s + 1);
+    }
+    compute(use);
+    if (more) read_wait(fill);
+  };
+  const int npro = min(nk, kNSlot);
+  for (int s = 0; s < npro; ++s) issue(s);
+  if (npro == 4) wait_vm<3 * kDmaPerWave>();
+  else if (npro == 3) wait_vm<2 * kDmaPerWave>();
+  else if (npro == 2) wait_vm<kDmaPerWave>();
+  else wait_vm<0>();
+  barrier();                      // k-step 0 (and the staged BN1 / BN2 parameters) visible
+  Frags fa, fb;
+  read_issue(fa, 0);
+  read_wait(fa);
+  for (int s = 0; s < nk; s += 2) {
+    step(fa, fb, s);
+    if (s + 1 < nk) step(fb, fa, s + 1);
+  }
+  // the L2-resident weights of the rest of the layer are requested here, in one batch, so their latency
+  // hides behind the epilogue and the channel sums: the conv's fragments, this thread's 16-wide slice of linear1 (row tid / 8) and 4-wide slice of linear2 (row tid / 16)
+  bf16x8 wl[2][12];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk)
+      wl[nt][kk] = *reinterpret_cast<const bf16x8*>(a.wl + (nt * 16 + l15) * (3 * kC) + kk * 32 + g * 8);
+  const int j1 = tid >> 3, k1 = (tid & 7) * 16, j2 = tid >> 4, k2 = (tid & 15) * 4;
+  float4 w1v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) w1v[u] = *reinterpret_cast<const float4*>(a.w1 + j1 * kC + k1 + 4 * u);
+  const float4 w2v = *reinterpret_cast<const float4*>(a.w2 + j2 * kC1 + k2);
+  const float c1v = a.c1[j1], c2v = a.c2[j2];
+  float bl4[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bl4[nt][r] = a.bl ? a.bl[nt * 16 + 4 * g + r] : 0.f;
+  barrier();   // every wave is done with the ring: its LDS becomes the h image
+  // epilogue: BN2 + ReLU -> bf16 into the h image (frames >= T: zero rows, the conv's padding)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tt = w + 8 * j;
+    if (tt >= n_tt) continue;
+    const int t = tt * 16 + l15;
+#pragma unroll
+    for (int ot = 0; ot < 8; ++ot) {
+      const int n = ot * 16 + 4 * g;
+      const float4 al = *reinterpret_cast<const float4*>(ab2 + n);
+      const float4 be = *reinterpret_cast<const float4*>(ab2 + kC + n);
+      uint2 v = make_uint2(0u, 0u);
+      if (t < T)
+        v = make_uint2(pack_bf16x2(fmaxf(fmaf(acc[j][ot][0], al.x, be.x), 0.f), fmaxf(fmaf(acc[j][ot][1], al.y, be.y), 0.f)),
+                       pack_bf16x2(fmaxf(fmaf(acc[j][ot][2], al.z, be.z), 0.f), fmaxf(fmaf(acc[j][ot][3], al.w, be.w), 0.f)));
+      *reinterpret_cast<uint2*>(hs + h_off(t + kMaxDil, n)) = v;
+    }
+  }
+  // halo rows: kMaxDil before frame 0, and from the last tile's end up to what the conv reads
+  for (int i = tid; i < kMaxDil * (kC / 4); i += kThreads) {
+    const int r = i / (kC / 4), c = (i % (kC / 4)) * 4;
+    *reinterpret_cast<uint2*>(hs + h_off(r, c)) = make_uint2(0u, 0u);
+    *reinterpret_cast<uint2*>(hs + h_off(n_tt * 16 + kMaxDil + r, c)) = make_uint2(0u, 0u);
+  }
+  barrier();   // h complete
+
+  // ---- phase 2: per-segment channel sums of h, the context (mean + segment mean), the gate MLP
+  float* red = reinterpret_cast<float*>(sm + kHBytes / 2);         // [kWaves][kMaxSegs][kC]
+  float* ctx = red + kWaves * kMaxSegs * kC;                       // [kMaxSegs][kC]
+  float* hid = ctx + kMaxSegs * kC;                                // [kMaxSegs][kC1]
+  float* gate = hid + kMaxSegs * kC1;                              // [kMaxSegs][kC2]
+  const int nseg = (T + kSeg - 1) / kSeg;
+  {
+    // lane (cg, rg): channels 8cg .. 8cg + 7 of frames rg, rg + 4, ... of the wave's frame stripe
+    const int cg = lane & 15, rg = (lane >> 4) + 4 * w;            // 32 row groups over the block
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q) {
+      float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (q < nseg) {
+        const int t1 = min(T, (q + 1) * kSeg);
+        for (int t = q * kSeg + ((rg - q * kSeg) & 31); t < t1; t += 32) {
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(t + kMaxDil, 8 * cg));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            sv[2 * u] += __uint_as_float(v[u] << 16);
+            sv[2 * u + 1] += __uint_as_float(v[u] & 0xffff0000u);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {                                  // the wave's 4 row groups
+        sv[u] += __shfl_xor(sv[u], 16);
+        sv[u] += __shfl_xor(sv[u], 32);
+      }
+      if (lane < 16 && q < nseg) {
+        float4* d = reinterpret_cast<float4*>(red + (w * kMaxSegs + q) * kC + 8 * cg);
+        d[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        d[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+      }
+    }
+  }
+  // local conv (k 3, dilation dil, zero padding) of the wave's frame tiles w, w + 8, w + 16: it only needs
+  // h, so its MFMAs run here; the gate is applied once the MLP below has produced it
+  floatx4 cacc[3][2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    cacc[j][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    cacc[j][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (w + 8 * j < n_tt) {
+      const int t = (w + 8 * j) * 16 + l15;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) {
+        const int tap = kk >> 2, c = (kk & 3) * 32 + g * 8;
+        const bf16x8 hf = *reinterpret_cast<const bf16x8*>(hs + h_off(t + kMaxDil + (tap - 1) * a.dil, c));
+        cacc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[0][kk], hf, cacc[j][0], 0, 0, 0);
+        cacc[j][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[1][kk], hf, cacc[j][1], 0, 0, 0);
+      }
+    }
+  }
+  barrier();
+  if (tid < kC) {                        // ctx[q][c] = mean over all frames + mean over segment q
+    float sq[kMaxSegs], tot = 0.f;
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q) {
+      sq[q] = 0.f;
+      if (q < nseg)
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) sq[q] += red[(ww * kMaxSegs + q) * kC + tid];
+      tot += sq[q];
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q)
+      if (q < nseg) ctx[q * kC + tid] = tot / (float)T + sq[q] / (float)(min(T, (q + 1) * kSeg) - q * kSeg);
+  }
+  barrier();
+  for (int q = 0; q < nseg; ++q) {       // hid = relu(W1 ctx + c1): 8 lanes per output, 16 k each
+    const float4* cq = reinterpret_cast<const float4*>(ctx + q * kC + k1);
+    float p = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 c4 = cq[u];
+      p = fmaf(w1v[u].x, c4.x, p); p = fmaf(w1v[u].y, c4.y, p);
+      p = fmaf(w1v[u].z, c4.z, p); p = fmaf(w1v[u].w, c4.w, p);
+    }
+    p += __shfl_xor(p, 1); p += __shfl_xor(p, 2); p += __shfl_xor(p, 4);
+    if ((tid & 7) == 0) hid[q * kC1 + j1] = fmaxf(p + c1v, 0.f);
+  }
+  barrier();
+  for (int q = 0; q < nseg; ++q) {       // gate = sigmoid(W2 hid + c2): 16 lanes per output, 4 k each
+    const float4 h4 = *reinterpret_cast<const float4*>(hid + q * kC1 + k2);
+    float p = w2v.x * h4.x;
+    p = fmaf(w2v.y, h4.y, p); p = fmaf(w2v.z, h4.z, p); p = fmaf(w2v.w, h4.w, p);
+    p += __shfl_xor(p, 1); p += __shfl_xor(p, 2); p += __shfl_xor(p, 4); p += __shfl_xor(p, 8);
+    if ((tid & 15) == 0) gate[q * kC2 + j2] = 1.f / (1.f + expf(-(p + c2v)));
+  }
+  barrier();
+
+  // ---- phase 3: (conv + bias) x gate -> the new 32 channels
+  uint16_t* ob = a.out + (int64_t)b * T * a.ld;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int t = (w + 8 * j) * 16 + l15;
+    if (w + 8 * j < n_tt && t < T) {
+      const float* gq = gate + (t / kSeg) * kC2;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = nt * 16 + 4 * g;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (cacc[j][nt][r] + bl4[nt][r]) * gq[n + r];
+        *reinterpret_cast<uint2*>(ob + (int64_t)t * a.ld + n) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, int taps, int dil, int seg_len,
+                         bool bf16) {
+  static const bool off = getenv("SDIAR_NO_CAM_DENSE") != nullptr;   // A/B switch: the three-launch path
+  return !off && bf16 && T >= 1 && T <= kMaxT && cin >= 32 && cin % 32 == 0 && cin <= kMaxCin && cin + kC2 <= ld &&
+         ld % 8 == 0 && bn == kC && C1 == kC1 && C2 == kC2 && N == kC2 && taps == 3 && dil >= 1 && dil <= kMaxDil &&
+         seg_len == kSeg;
+}
+
+void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
+               const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
+               const float* c1, const float* w2, const float* c2, void* out, hipStream_t st) {
+  SD_CHECK(B >= 1 && T >= 1 && T <= kMaxT, kErrInvalid, "cam_dense: bad item shape");
+  SD_CHECK((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0, kErrInvalid,
+           "cam_dense: misaligned map");
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cam_dense_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
+    attr = true;
+  }
+  const int nseg = cdiv(T, kSeg);
+  ProfScope prof("cam_dense",
+                 2.0 * B * T * kC * (double)cin + 2.0 * B * T * kC2 * 3 * kC + 2.0 * B * nseg * (kC * kC1 + kC1 * kC2),
+                 2.0 * B * T * ((double)cin + kC2) + 2.0 * kC * cin, st);
+  CamDenseArgs a{static_cast<const uint16_t*>(x), ld, cin, T, dil, s1, h1, static_cast<const uint16_t*>(wb), a2, b2,
+                 static_cast<const uint16_t*>(wl), bl, w1, c1, w2, c2, static_cast<uint16_t*>(out)};
+  hipLaunchKernelGGL(cam_dense_kernel, dim3(B), dim3(kThreads), kSmemBytes, st, a);
+  SD_LAUNCH_CHECK();
+}
+
+}  // namespace sd

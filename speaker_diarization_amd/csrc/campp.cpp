@@ -226,6 +226,15 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
     const int ld = ctot[b];
     for (const DenseL& L : dense_[b]) {
       SD_CHECK(L.bottleneck.w.Cin == cin, kErrParam, "dense layer input width");
+      if (!no_fused_ && cam_dense_supported(T2, cin, ld, L.bottleneck.w.N, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil,
+                                            100, bf)) {
+        // the whole layer per item in one launch, the 128-channel bottleneck kept in LDS (cam_dense.hip)
+        cam_dense(D.p, B, T2, ld, cin, L.dil, L.bottleneck.pre_s, L.bottleneck.pre_h, L.bottleneck.w.w,
+                  L.bottleneck.alpha, L.bottleneck.beta, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
+                  act_at(D, cin).p, st);
+        cin += L.local.w.N;
+        continue;
+      }
       ConvGemmArgs p = cam_conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp_, bf}, 128);
       p.act = kActRelu;
       conv_gemm(p, bf, st);

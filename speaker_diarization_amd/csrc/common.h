@@ -65,6 +65,17 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// 16-B-per-lane global -> LDS DMA (global_load_lds_dwordx4): lane i's 16 B land at lds + 16 i.  Issued as
+// inline asm rather than __builtin_amdgcn_global_load_lds on purpose: the compiler's wait-count pass knows
+// about a builtin LDS DMA in flight and then puts s_waitcnt vmcnt(0) in front of EVERY later LDS access it
+// cannot prove disjoint (all of one dynamic LDS array) - draining a multi-stage DMA ring at each fragment
+// read.  Callers own the ordering: a counted s_waitcnt vmcnt(N) + barrier before the slot is read.
+// `lds` must be wave-uniform (it goes to M0).
+__device__ __forceinline__ void dma_lds16(const void* g, const void __attribute__((address_space(3)))* lds) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0v), "v"(g) : "memory", "m0");
+}
+
 __device__ __forceinline__ float bf_bits2f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }

@@ -121,6 +121,14 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
                  int C2, float* gate, hipStream_t st);
 // CAM++ dense-layer tail fused (cam_fused.hip): context gate + linear_local k3 conv + gating
 // for one bf16 bottleneck map x (B, T, 128) -> out (B, T, 32) at row stride ldo (bf16).
+// One CAM++ dense layer (bottleneck BN-ReLU-1x1-BN-ReLU, CAMLayer context gate, k-3 local conv x gate) per
+// item in one launch, h kept in LDS (cam_dense.hip); x: (B, T, ld) bf16 map whose channels [0, cin) are the
+// input, out: its channel slice at cin.  bf16, T <= 320.
+bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, int taps, int dil, int seg_len,
+                         bool bf16);
+void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
+               const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
+               const float* c1, const float* w2, const float* c2, void* out, hipStream_t st);
 bool cam_local_fused_supported(int C, int C1, int C2, int N, int taps, int dil, int seg_len, int ldo, bool bf16);
 void cam_local_fused(const void* x, int B, int T, int dil, const void* wt, const float* bias, const float* w1,
                      const float* b1, const float* w2, const float* b2, void* out, int ldo, hipStream_t st);

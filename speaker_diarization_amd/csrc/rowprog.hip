@@ -101,15 +101,15 @@ struct Ring {
 #pragma unroll
     for (int j = 0; j < kDpw; ++j) {
       const int f = w + kWaves * j;
-      __builtin_amdgcn_global_load_lds((const void*)(s + f * kFrag + lane * 8), (lds_ptr_t)(slot + f * kFrag), 16,
-                                       0, 0);
+      dma_lds16(s + f * kFrag + lane * 8, (lds_ptr_t)(slot + f * kFrag));
     }
   }
   // Wait for piece g and make every wave's part visible; returns g's slot.  The slot of piece g - 1 is
   // free from here on: refill(g) (called a few MFMAs into the piece) streams piece g + kNSlot - 1 into it.
   __device__ __forceinline__ const uint16_t* wait(int g) const {
     wait_piece<kDpw>(min(kNSlot - 2, total - 1 - g));
-    __syncthreads();
+    // plain s_barrier: __syncthreads()' workgroup fence waits for vmcnt(0) and would drain the ring
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     return ring + (g % kNSlot) * kPiece;
   }
   __device__ __forceinline__ void refill(int g) const { issue(g + kNSlot - 1); }
