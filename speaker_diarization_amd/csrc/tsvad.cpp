@@ -103,71 +103,19 @@ void TsvadModel::alloc_workspace() {
   lstm_work_ = ws(lstm_work_floats((int)Bm, cfg_.lstm_hidden, 2));
 }
 
-TsvadModel::~TsvadModel() {
-  for (GraphEntry& e : graphs_) {
-    if (e.exec) (void)hipGraphExecDestroy(e.exec);
-    if (e.graph) (void)hipGraphDestroy(e.graph);
-  }
-  if (cap_st_) (void)hipStreamDestroy(cap_st_);
-}
+TsvadModel::~TsvadModel() = default;
 
+// Direct launches only.  A hipGraph replay of this forward was tried (round 2-3) and dropped: it measured no
+// faster on C2 (34.3 vs 34.4 ms per 10-min step: ~150 launches against a 34-ms GPU span) and its replays did
+// not reproduce the direct launches' posteriors (max |diff| 0.098 from the second replay on, and a replayed
+// persistent LSTM reported lost co-residency) - tools/lstm_repro.py.
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
                          hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
-  // an earlier forward's LSTM report nobody collected with sd_tsvad_status (a replayed graph repeats
-  // only the stream-ordered copy of the err word, so the host-side check lives here)
+  // an earlier forward's LSTM report nobody collected with sd_tsvad_status
   lstm_err_.raise_if_set();
-  static const bool no_graph = getenv("SDIAR_NO_GRAPH") && atoi(getenv("SDIAR_NO_GRAPH")) == 1;
-  if (no_graph || prof_enabled()) {
-    forward_body(ref, ts, B, Tf, Tl, logits, st);
-    return;
-  }
-  GraphEntry* e = nullptr;
-  for (GraphEntry& g : graphs_)
-    if (g.ref == ref && g.ts == ts && g.logits == logits && g.B == B && g.Tf == Tf && g.Tl == Tl) e = &g;
-  if (!e) {
-    if (graphs_.size() >= 8) {   // bounded: the oldest key is dropped
-      GraphEntry& o = graphs_.front();
-      if (o.exec) (void)hipGraphExecDestroy(o.exec);
-      if (o.graph) (void)hipGraphDestroy(o.graph);
-      graphs_.erase(graphs_.begin());
-    }
-    graphs_.push_back(GraphEntry{ref, ts, logits, B, Tf, Tl});
-    e = &graphs_.back();
-  }
-  if (e->failed || ++e->seen < 2) {   // first sight: direct launches (and the launchers' one-time setup)
-    forward_body(ref, ts, B, Tf, Tl, logits, st);
-    return;
-  }
-  if (!e->exec) {
-    if (!cap_st_) SD_HIP(hipStreamCreateWithFlags(&cap_st_, hipStreamNonBlocking));
-    SD_HIP(hipStreamBeginCapture(cap_st_, hipStreamCaptureModeThreadLocal));
-    bool ok = true;
-    try {
-      forward_body(ref, ts, B, Tf, Tl, logits, cap_st_);
-    } catch (...) {
-      ok = false;
-    }
-    hipGraph_t g = nullptr;
-    const hipError_t ec = hipStreamEndCapture(cap_st_, &g);
-    if (ok && ec == hipSuccess && g && hipGraphInstantiate(&e->exec, g, nullptr, nullptr, 0) == hipSuccess) {
-      e->graph = g;
-    } else {   // not capturable (or failed): this key runs direct launches from now on
-      if (g) (void)hipGraphDestroy(g);
-      e->exec = nullptr;
-      e->failed = true;
-      (void)hipGetLastError();
-      forward_body(ref, ts, B, Tf, Tl, logits, st);
-      return;
-    }
-  }
-  SD_HIP(hipGraphLaunch(e->exec, st));
-}
-
-void TsvadModel::forward_body(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
-                              hipStream_t st) {
   const bool bf = cfg_.bf16;
   const Tens x4 = cam_.forward(ref, B, Tf, st);   // CAM++ up to transit3, (B, T2, 512)
   const int T2 = CamTrunk::out_frames(Tf);

@@ -39,21 +39,6 @@ class TsvadModel {
   ~TsvadModel();
 
  private:
-  void forward_body(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits, hipStream_t st);
-  // hipGraph replay of the whole forward for a recurring (pointers, shapes) key: the second call with a key
-  // captures (on cap_st_) and instantiates, later calls launch the graph.  SDIAR_NO_GRAPH=1 or per-kernel
-  // timing (sd_prof) run direct launches.
-  struct GraphEntry {
-    const float *ref, *ts;
-    float* logits;
-    int B, Tf, Tl;
-    int seen = 0;
-    bool failed = false;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-  };
-  std::vector<GraphEntry> graphs_;
-  hipStream_t cap_st_ = nullptr;
   ConvL conv_bn(const std::string& wname, const std::string& bn, const std::string& bias = "");
   LayerLoader loader() { return LayerLoader{ps_, arena_, cfg_.bf16}; }
   EncoderWork enc_work() const { return EncoderWork{Y_, QKV_, AO_, H_, partial_, cfg_.bf16}; }

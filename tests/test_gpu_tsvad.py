@@ -113,10 +113,9 @@ def test_tsvad_v1_large_batch_uses_wide_gemm_paths(gpu):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-def test_tsvad_graph_replay_matches_direct(gpu, variant):
-    """The second forward with the same (pointers, shapes) captures the whole forward into a hipGraph and
-    later ones replay it (tsvad.cpp): every replay must give the direct-launch logits bit for bit, a new
-    output buffer must not reuse the old graph, and the fp32 golden still holds through the graph."""
+def test_tsvad_repeated_forward_bit_identical(gpu, variant):
+    """Repeated forwards on one handle (its workspaces, LSTM exchange buffers and counters reused) give
+    the first call's logits bit for bit, also into a new output buffer, and the golden still holds."""
     name = "tsvad_v0_rs4" if variant == 0 else "tsvad_v1_rs6"
     v, rs, B, T, nl, iseed, wseed = TSVAD_CASES[name]
     cfg = _cfg(v, rs)
@@ -126,7 +125,7 @@ def test_tsvad_graph_replay_matches_direct(gpu, variant):
     xd, tsd = torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu)
     out = torch.empty(B, 4, nl, device=gpu)
     outs = []
-    for _ in range(4):   # direct, capture + launch, replay, replay
+    for _ in range(4):
         out.fill_(float("nan"))
         m.forward(xd, tsd, nl, out=out)
         outs.append(out.cpu().numpy().copy())

@@ -36,6 +36,7 @@ CATEGORIES = {
     "dwconv": r"glu_dwconv_kernel",
     "groupnorm_silu": r"groupnorm\w*kernel",
     "cam_context": r"cam_context\w*kernel",
+    "cam_dense": r"cam_dense_kernel",
     "fbank_kaldi": r"fbank\w*kernel",
 }
 
