@@ -1,14 +1,19 @@
 #!/bin/bash
 # Per-workload evidence for DESIGN.md §6 (run on the GPU box from the repo root):
-#   bench JSON line (5 timed steps, no CPU baseline) + rocprofv3 kernel-trace stats of the same command.
-#   bash tools/profile_round.sh <outdir> c1 c3 c5 ...
+#   bench JSON line (5 timed steps; with CPU baseline + parity block when FULL=1) + rocprofv3 kernel-trace
+#   stats of the same command (no CPU baseline).
+#   [FULL=1] bash tools/profile_round.sh <outdir> c1 c3 c5 ...
 set -euo pipefail
 OUT=$1; shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for WL in "$@"; do
   BENCH="bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline"
-  timeout -k 10 240 python3 $BENCH > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
+  if [ "${FULL:-0}" = 1 ]; then
+    timeout -k 10 400 python3 bench.py --workload $WL --steps 5 --warmup 2 > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
+  else
+    timeout -k 10 240 python3 $BENCH > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
+  fi
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$WL" -o run -- python3 $BENCH \
     > "$OUT/trace_$WL.log" 2>&1
   cp "$(find "$OUT/trace_$WL" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats_$WL.csv"
