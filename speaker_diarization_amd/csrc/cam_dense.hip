@@ -305,9 +305,11 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {                                  // the wave's 4 row groups
-        sv[u] += __shfl_xor(sv[u], 16);
-        sv[u] += __shfl_xor(sv[u], 32);
+      for (int u = 0; u < 8; ++u) {   // the wave's 4 row groups: lane l + (l ^ 16), then + (l ^ 32), on the VALU
+        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(sv[u]), __float_as_uint(sv[u]), false, false);
+        sv[u] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+        const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sv[u]), __float_as_uint(sv[u]), false, false);
+        sv[u] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
       }
       if (lane < 16 && q < nseg) {
         float4* d = reinterpret_cast<float4*>(red + (w * kMaxSegs + q) * kC + 8 * cg);

@@ -76,6 +76,15 @@ __device__ __forceinline__ void dma_lds16(const void* g, const void __attribute_
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0v), "v"(g) : "memory", "m0");
 }
 
+// The buffer form (bounds-checked by the resource: out-of-range lanes land as zeros), same contract.
+__device__ __forceinline__ void dma_lds16_buf(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                              const void __attribute__((address_space(3)))* lds) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(voff),
+               "s"(rsrc)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ float bf_bits2f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }

@@ -110,8 +110,7 @@ __global__ __launch_bounds__(512) void gemm_areg_kernel(ConvGemmArgs p) {
     const uint32_t base = (uint32_t)(((int64_t)(c * NB + wr) * K + wsrc) * 2);
 #pragma unroll
     for (int kc = 0; kc < PIECES; ++kc)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(dst + (size_t)kc * NB * 64), 16, base + kc * 128,
-                                               0, 0, 0);
+      dma_lds16_buf(rw, base + kc * 128, (lds_ptr_t)(dst + (size_t)kc * NB * 64));
   };
 
   // ---- A fragments of this wave's 32 rows: af[mt][kk] = row tile*256 + 32*wid + 16*mt + l15,

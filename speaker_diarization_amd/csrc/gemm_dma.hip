@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
       const uint32_t off = ok ? (uint32_t)((((int64_t)(a_bh[j] + hi) * p.W + wi) * p.lda + p.a_coff + c) * 2)
                               : kOOB;
       lds_ptr_t dst = (lds_ptr_t)(As + (wid * (BM / 4) + j * 8) * BK);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, 0, 0, 0);
+      dma_lds16_buf(ra, off, dst);
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
       const bool ok = b_row[j] < p.N && k < ke;
       const uint32_t off = ok ? (uint32_t)(((int64_t)b_row[j] * p.K + k) * 2) : kOOB;
       lds_ptr_t dst = (lds_ptr_t)(Bs + (wid * (BN / 4) + j * 8) * BK);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, dst, 16, off, 0, 0, 0);
+      dma_lds16_buf(rb, off, dst);
     }
   };
 

@@ -42,7 +42,6 @@ constexpr int kQS = 64;                        // Q / K row stride (features 48.
 constexpr int kVS = 48;                        // V row stride
 constexpr int kSeqLds = 2 * kTP * kQS + kTP * kVS;   // bf16 elements of one sequence's Q, K, V images
 constexpr int kPieces = kNH * 3 * (kHD / kPR); // 72
-constexpr uint32_t kOOB = 0x80000000u;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr size_t kSmemBytes = sizeof(uint16_t) * ((size_t)kNSlot * kSlot + (size_t)kSeq * kSeqLds) +
                               sizeof(float) * 3 * kD;
@@ -68,8 +67,6 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   const int T = a.T;
   const int r0 = (w % kWavesPerSeq) * 32 + l15;               // token of row tile 0 (tile 1: +16)
 
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), (short)0,
-                                                                      (int)kOOB, 0x00020000);
   const int lrow = lane >> 3, lch = lane & 7;
   // Piece i: head h = i / 9, component c = (i / 3) % 3, feature tile ft = i % 3 -> in_proj rows
   // c*D + 48h + 16ft .. +15, all K, as 12 1-KiB DMA instructions (k-block kc, 8-row group) over the
@@ -82,8 +79,9 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
       const int r = rg * 8 + lrow;
       const uint32_t off =
           (uint32_t)((((int64_t)(c * kD + h * kHD + ft * kPR + r)) * kD + kc * 64 + ((lch ^ (r & 7)) * 8)) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(slot + ((size_t)kc * kPR + rg * 8) * 64), 16, off, 0,
-                                               0, 0);
+      // asm DMA (common.h dma_lds16): with the builtin, the compiler put s_waitcnt vmcnt(0) in front of
+      // every fragment read of the piece loop (it cannot tell the slots apart), draining the ring
+      dma_lds16(reinterpret_cast<const char*>(a.W) + off, (lds_ptr_t)(slot + ((size_t)kc * kPR + rg * 8) * 64));
     }
   };
   const int my_dma = (w < kDmaPerPiece - kWaves) ? 2 : 1;      // instructions this wave issues per piece
