@@ -4,10 +4,13 @@
 // add_layernorm + the QKV GEMM (gemm_areg) + attn_short, whose (S*T, 3D) bf16 QKV intermediate made a
 // full HBM round trip (2.3 KiB per token each way at D = 384).
 //
-// A workgroup owns TWO sequences (10 waves; wave w: sequence w / 5, tokens 32 (w % 5) .. +31, i.e. two
-// 16-token MFMA row tiles), D = 384, 8 heads of 48:
+// A workgroup owns TWO sequences = 20 16-token MFMA row tiles (tile t: sequence t / 10, tokens 16 (t % 10)
+// .. +15) over 8 waves: wave w takes tiles w, w + 8 and, for w < 4, w + 16, so each SIMD (waves w, w + 4)
+// carries 5 tiles — the earlier 10-wave layout (2 tiles per wave) put 3 waves on two SIMDs and 2 on the
+// others, and the 2-wave SIMDs spent 21 % of the block parked at the per-piece barrier (s_memtime stamps).
+// D = 384, 8 heads of 48:
 //   prologue  the LayerNorm'd bf16 rows (the preceding row program / add_layernorm writes them) become
-//             the wave's MFMA B-operand fragments (2 x 16 tokens x 384, 96 VGPRs), read once from HBM;
+//             the wave's MFMA B-operand fragments (up to 3 x 16 tokens x 384, 144 VGPRs), read once from HBM;
 //   pieces    16 in-projection rows (one head's 16 features of q, k or v), 12 KiB, stream through a
 //             3-slot LDS-DMA ring (buffer_load ... lds, 16-B chunk c of row r at c ^ (r & 7)), two pieces
 //             in flight behind counted vmcnt waits; each weight fragment read from LDS feeds both row
@@ -31,8 +34,10 @@ constexpr int kKT32 = kD / 32;                 // 32-wide k-steps of the project
 constexpr int kKC = kD / 64;                   // 64-wide k-blocks of a weight piece
 constexpr int kTP = 160;                       // padded tokens per sequence
 constexpr int kSeq = 2;                        // sequences per workgroup
-constexpr int kWavesPerSeq = kTP / 32;         // 5 waves x 32 tokens
-constexpr int kWaves = kSeq * kWavesPerSeq;
+constexpr int kTilesPerSeq = kTP / 16;         // 10 row tiles of 16 tokens
+constexpr int kTiles = kSeq * kTilesPerSeq;     // 20
+constexpr int kWaves = 8;
+constexpr int kMaxTiles = (kTiles + kWaves - 1) / kWaves;   // 3 (waves 0-3), others 2
 constexpr int kThreads = kWaves * 64;
 constexpr int kPR = 16;                        // weight rows per piece (one MFMA column tile)
 constexpr int kSlot = kKC * kPR * 64;          // bf16 elements per ring slot (12 KiB)
@@ -57,15 +62,18 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lk = lane >> 4;
-  const int sq = w / kWavesPerSeq;                            // this wave's sequence slot
-  uint16_t* Qs = Ws + kNSlot * kSlot + sq * kSeqLds;          // [kTP][kQS]
-  uint16_t* Ks = Qs + kTP * kQS;                              // [kTP][kQS]
-  uint16_t* Vs = Ks + kTP * kQS;                              // [kTP][kVS]
   float* s_bias = reinterpret_cast<float*>(Ws + kNSlot * kSlot + kSeq * kSeqLds);   // [3 * kD]
-  const int s = blockIdx.x * kSeq + sq;
-  const bool seq_ok = s < a.S;
   const int T = a.T;
-  const int r0 = (w % kWavesPerSeq) * 32 + l15;               // token of row tile 0 (tile 1: +16)
+  const int ntile = w < kTiles - (kMaxTiles - 1) * kWaves ? kMaxTiles : kMaxTiles - 1;   // wave-uniform
+  // tile j of this wave: sequence slot sqj[j], token row rowj[j] (this lane's token)
+  int sqj[kMaxTiles], rowj[kMaxTiles];
+#pragma unroll
+  for (int j = 0; j < kMaxTiles; ++j) {
+    const int t = w + kWaves * j;
+    sqj[j] = min(t, kTiles - 1) / kTilesPerSeq;
+    rowj[j] = (min(t, kTiles - 1) % kTilesPerSeq) * 16 + l15;
+  }
+  auto qimg = [&](int sq) { return Ws + kNSlot * kSlot + sq * kSeqLds; };   // [kTP][kQS] Q, then K, then V
 
   const int lrow = lane >> 3, lch = lane & 7;
   // Piece i: head h = i / 9, component c = (i / 3) % 3, feature tile ft = i % 3 -> in_proj rows
@@ -96,11 +104,12 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   }
 
   // ---- prologue: af[rt][kk] = y[32kk + 8lk .. +7] of the LayerNorm'd bf16 rows (B-operand fragments)
-  bf16x8 af[2][kKT32];
+  bf16x8 af[kMaxTiles][kKT32];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    const int row = r0 + 16 * rt;
-    const bool live = seq_ok && row < T;
+  for (int rt = 0; rt < kMaxTiles; ++rt) {
+    const int row = rowj[rt];
+    const int s = blockIdx.x * kSeq + sqj[rt];
+    const bool live = rt < ntile && s < a.S && row < T;
     const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + ((int64_t)s * T + row) * kD;
 #pragma unroll
     for (int kk = 0; kk < kKT32; ++kk)
@@ -108,7 +117,12 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
                                                    : make_uint4(0u, 0u, 0u, 0u));
   }
 
-  const int klen = seq_ok ? (a.key_len ? min(a.key_len[s], T) : T) : 0;
+  int klenj[kSeq];
+#pragma unroll
+  for (int q = 0; q < kSeq; ++q) {
+    const int s = blockIdx.x * kSeq + q;
+    klenj[q] = s < a.S ? (a.key_len ? min(a.key_len[s], T) : T) : 0;
+  }
   const int tr_off = ((4 * lk + (l15 >> 2)) * kVS + 4 * (l15 & 3)) * 2;
   typedef short v4s __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
@@ -125,7 +139,9 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     if (i + 2 < kPieces) issue_piece(i + 2);
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
     const uint16_t* slot = Ws + (i % kNSlot) * kSlot;
-    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    floatx4 acc[kMaxTiles];
+#pragma unroll
+    for (int rt = 0; rt < kMaxTiles; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
     auto wfrag = [&](int kk) {
       const int kc = kk >> 1, cc = (kk & 1) * 4 + lk;
       return *reinterpret_cast<const bf16x8*>(slot + (kc * kPR + l15) * 64 + ((cc ^ (l15 & 7)) * 8));
@@ -139,28 +155,35 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
       if (kk + 1 < kKT32) wnext = wfrag(kk + 1);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
+      if (ntile > 2) acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[2][kk], acc[2], 0, 0, 0);
       asm volatile("" ::: "memory");
       wcur = wnext;
     }
-    // lane holds features 16ft + 4lk + r of token r0 + 16rt
-    uint16_t* dst = c == 0 ? Qs : (c == 1 ? Ks : Vs);
+    // lane holds features 16ft + 4lk + r of token rowj[rt]
     const int ld = c == 2 ? kVS : kQS;
+    const int coff = c * kTP * kQS;                 // Q, K or V image within the sequence's block
     const float scl = c == 0 ? a.scale : 1.f;
     const int n0 = ft * 16 + 4 * lk;
     const float4 bv = *reinterpret_cast<const float4*>(s_bias + c * kD + h * kHD + n0);
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-      *reinterpret_cast<uint2*>(dst + (r0 + 16 * rt) * ld + n0) =
-          make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
-                     pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
+    for (int rt = 0; rt < kMaxTiles; ++rt)
+      if (rt < ntile)
+        *reinterpret_cast<uint2*>(qimg(sqj[rt]) + coff + rowj[rt] * ld + n0) =
+            make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
+                       pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2) continue;
     __syncthreads();   // head h's Q, K, V images complete (both sequences)
-    if (!seq_ok) continue;
 
-    // ---- attention of head h for this wave's two 16-query tiles
+    // ---- attention of head h for this wave's 16-query tiles
 #pragma unroll 1
-    for (int rt = 0; rt < 2; ++rt) {
-      const int row = r0 + 16 * rt;
+    for (int rt = 0; rt < ntile; ++rt) {
+      const int row = rowj[rt];
+      const int s = blockIdx.x * kSeq + sqj[rt];
+      if (s >= a.S) continue;
+      const uint16_t* Qs = qimg(sqj[rt]);
+      const uint16_t* Ks = Qs + kTP * kQS;
+      const uint16_t* Vs = Ks + kTP * kQS;
+      const int klen = klenj[sqj[rt]];
       bf16x8 qf[2];
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(Qs + row * kQS + kc * 32 + lk * 8);
