@@ -239,10 +239,16 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
   add_layernorm(X, y.p, bf, rows, E, L.fin_g, L.fin_b, 1e-5f, false, X, false, st);
 }
 
-void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int T, int E, int nh, int kernel,
-                         const int* key_len, const EncoderWork& w, hipStream_t st) {
-  bool fused = w.bf16 && !Ls.empty();
+bool conformer_stack_fused(const std::vector<ConformerL>& Ls, int E, bool bf16) {
+  bool fused = bf16 && !Ls.empty() && E == 384;
   for (const ConformerL& L : Ls) fused = fused && L.rp_f1 && rowprog_supported(E, L.rp_hidden, true);
+  return fused;
+}
+
+void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int T, int E, int nh, int kernel,
+                         const int* key_len, const EncoderWork& w, hipStream_t st, const SpeakerStreams* io) {
+  const bool fused = conformer_stack_fused(Ls, E, w.bf16);
+  SD_CHECK(!io || fused, kErrInvalid, "run_conformer_stack: speaker streams need the fused stack");
   if (!fused) {
     for (const ConformerL& L : Ls) run_conformer(L, X, S, T, E, nh, kernel, key_len, w, st);
     return;
@@ -264,6 +270,10 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   {
     RowProgArgs r;
     r.X = X; r.Xo = X; r.M = rows;
+    if (io) {
+      r.X = nullptr; r.x_ts = io->ts; r.x_mix = io->mix; r.x_ldmix = io->ldmix; r.x_Tmix = io->Tmix;
+      r.x_NS = io->NS; r.T_seq = T;
+    }
     r.n_ffn = 1; r.ffn[0] = ffn(Ls[0], false);
     r.y = y.p; r.y_g = Ls[0].at_lng; r.y_b = Ls[0].at_lnb;
     rowprog(r, "rowprog_ffn", st);
@@ -313,6 +323,8 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
         const ConformerL& Ln = Ls[li + 1];
         r.n_ffn = 2; r.ffn[1] = ffn(Ln, false);
         r.y = y.p; r.y_g = Ln.at_lng; r.y_b = Ln.at_lnb;
+      } else if (io) {
+        r.Xo = nullptr; r.yt = io->out; r.yt_NS = io->NS; r.T_seq = T;
       }
       rowprog(r, "rowprog_pw2_ffn", st);
     }

@@ -91,7 +91,19 @@ void run_conformer(const ConformerL& L, float* X, int S, int T, int E, int nh, i
                    const int* key_len, const EncoderWork& w, hipStream_t st);
 // All layers of a torchaudio Conformer; runs the per-token parts as rowprog.hip programs when every
 // layer has its pieces (bf16, D 384), else run_conformer per layer.
+// TS-VAD speaker streams around a fused (row-program) conformer stack: the first program builds its input
+// rows [ts | mix] on load (no build_speaker_input pass) and the last writes bf16 rows straight into the
+// speakers-to-channels layout (no speakers_to_channels pass, no fp32 output).  Only with
+// conformer_stack_fused() true.
+struct SpeakerStreams {
+  const float* ts = nullptr;    // (B*NS, 192)
+  const float* mix = nullptr;   // (B, Tmix, ldmix), columns 0..191
+  int ldmix = 0, Tmix = 0, NS = 0;
+  void* out = nullptr;          // bf16 (B, T, NS*E)
+};
+bool conformer_stack_fused(const std::vector<ConformerL>& Ls, int E, bool bf16);
 void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int T, int E, int nh, int kernel,
-                         const int* key_len, const EncoderWork& w, hipStream_t st);
+                         const int* key_len, const EncoderWork& w, hipStream_t st,
+                         const SpeakerStreams* io = nullptr);
 
 }  // namespace sd

@@ -233,6 +233,16 @@ struct RowProgArgs {
   const float* gn_partial = nullptr;
   int gn_nblk = 0, gn_T = 0;
   const float *gn_g = nullptr, *gn_b = nullptr;
+  // optional X source instead of X: the TS-VAD per-speaker input rows [ts_embed | mix] built on load
+  // (build_speaker_input_kernel's layout, no positional encoding): row (s = b*NS + spk, t) of T_seq
+  // rows per sequence = ts[s][0..SE) | mix[b][t][0..SE) (zeros for t >= Tmix), SE = 192
+  const float* x_ts = nullptr;
+  const float* x_mix = nullptr;
+  int x_ldmix = 0, x_Tmix = 0, x_NS = 0, T_seq = 0;
+  // optional output: bf16(acc) in the speakers-to-channels layout (B, T_seq, NS * 384), row (b*NS + spk, t)
+  // -> (b, t) columns spk*384 .. (speakers_to_channels); with Xo == nullptr the fp32 rows are not written
+  void* yt = nullptr;
+  int yt_NS = 0;
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

@@ -234,11 +234,31 @@ void rowprog_kernel(RowProgArgs a) {
     floatx4 acc[kFT][TT];
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
-      const float* xr = a.X + row[tt] * kD + g4;
+      if (a.x_ts) {
+        // [ts_embed | mix] built on load (features 0..191 from the speaker's embedding, 192..383 from
+        // the mixture frame), as build_speaker_input_kernel writes them
+        constexpr int kSE = kD / 2;
+        const int64_t sq = row[tt] / a.T_seq;
+        const int t = (int)(row[tt] - sq * a.T_seq);
+        const float* tsr = a.x_ts + sq * kSE + g4;
+        const bool mv = live[tt] && t < a.x_Tmix;
+        const float* mxr = a.x_mix + ((sq / a.x_NS) * a.x_Tmix + (mv ? t : 0)) * (int64_t)a.x_ldmix + g4 - kSE;
 #pragma unroll
-      for (int ft = 0; ft < kFT; ++ft) {
-        const float4 v = live[tt] ? *reinterpret_cast<const float4*>(xr + 16 * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
-        acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
+        for (int ft = 0; ft < kFT; ++ft) {
+          const bool ts_half = 16 * ft < kSE;
+          const float4 v = !live[tt] ? make_float4(0.f, 0.f, 0.f, 0.f)
+                           : ts_half ? *reinterpret_cast<const float4*>(tsr + 16 * ft)
+                           : mv      ? *reinterpret_cast<const float4*>(mxr + 16 * ft)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+          acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
+        }
+      } else {
+        const float* xr = a.X + row[tt] * kD + g4;
+#pragma unroll
+        for (int ft = 0; ft < kFT; ++ft) {
+          const float4 v = live[tt] ? *reinterpret_cast<const float4*>(xr + 16 * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
+          acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
+        }
       }
     }
 
@@ -412,7 +432,17 @@ void rowprog_kernel(RowProgArgs a) {
     // ---- epilogue: Xo = acc; y = LN_y(acc)
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
-      if (live[tt]) {
+      if (a.yt && live[tt]) {
+        const int64_t sq = row[tt] / a.T_seq;
+        const int64_t t = row[tt] - sq * a.T_seq;
+        const int64_t b = sq / a.yt_NS, spk = sq - b * a.yt_NS;
+        uint16_t* yo = static_cast<uint16_t*>(a.yt) + ((b * a.T_seq + t) * a.yt_NS + spk) * kD + g4;
+#pragma unroll
+        for (int ft = 0; ft < kFT; ++ft)
+          *reinterpret_cast<uint2*>(yo + 16 * ft) = make_uint2(pack_bf16x2(acc[ft][tt][0], acc[ft][tt][1]),
+                                                              pack_bf16x2(acc[ft][tt][2], acc[ft][tt][3]));
+      }
+      if (a.Xo && live[tt]) {
         float* xo = a.Xo + row[tt] * kD + g4;
 #pragma unroll
         for (int ft = 0; ft < kFT; ++ft)
@@ -514,7 +544,10 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
              kErrInvalid, "rowprog: ffn arguments");
   SD_CHECK(!a.w0 || (a.A && a.b0), kErrInvalid, "rowprog: pre-GEMM arguments");
   SD_CHECK(!a.y || (a.y_g && a.y_b), kErrInvalid, "rowprog: y LayerNorm arguments");
-  SD_CHECK(a.X && a.Xo && (a.w0 || a.n_ffn > 0 || a.y), kErrInvalid, "rowprog: empty program");
+  SD_CHECK((a.X || a.x_ts) && (a.Xo || a.yt) && (a.w0 || a.n_ffn > 0 || a.y), kErrInvalid, "rowprog: empty program");
+  SD_CHECK(!a.x_ts || (a.x_mix && a.x_NS > 0 && a.T_seq > 0 && a.x_Tmix > 0 && a.x_ldmix % 4 == 0), kErrInvalid,
+           "rowprog: speaker-input source arguments");
+  SD_CHECK(!a.yt || (a.yt_NS > 0 && a.T_seq > 0), kErrInvalid, "rowprog: channel-layout output arguments");
   if (a.M <= 0) return;
   static int grid_max = 0;
   if (!grid_max) {
@@ -537,7 +570,8 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
     flops += 4.0 * rows * kD * a.ffn[i].hidden;
     wbytes += 4.0 * kD * a.ffn[i].hidden;
   }
-  const double bytes = rows * kD * (8.0 + (a.w0 ? 2.0 : 0.0) + (a.y ? 2.0 : 0.0)) + wbytes;
+  const double bytes =
+      rows * kD * (4.0 + (a.Xo ? 4.0 : 0.0) + (a.w0 ? 2.0 : 0.0) + (a.y ? 2.0 : 0.0) + (a.yt ? 2.0 : 0.0)) + wbytes;
   ProfScope prof(name, flops, bytes, st);
   const dim3 g3(grid);
   {

@@ -148,9 +148,17 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape,
              "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
     gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
-    build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
-    run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
-    speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
+    if (SE == 192 && E == 2 * SE && conformer_stack_fused(conf_, E, bf)) {
+      // the row programs build [ts | mix] on load and write the bf16 speakers-to-channels rows directly
+      SpeakerStreams io;
+      io.ts = ts; io.mix = mixg_; io.ldmix = SE; io.Tmix = T3; io.NS = NS; io.out = X2_;
+      run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st,
+                          &io);
+    } else {
+      build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
+      run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
+      speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
+    }
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
