@@ -111,6 +111,10 @@ __device__ __forceinline__ float warp_max(float v) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// Sigmoid with the hardware reciprocal (v_rcp_f32, <= 1 ulp) instead of an IEEE division (about ten
+// instructions: div_scale / rcp / fma chain / div_fmas / div_fixup) - for the GLU / SiLU epilogues of
+// the hot GEMM and conv kernels.  sigmoid_rcp(-inf) = 0, (+inf) = 1, NaN stays NaN.
+__device__ __forceinline__ float sigmoid_rcp(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // XCD-aware tile order (cdna_hip_programming.md T1, bijective form): workgroups
 // are dealt round-robin over the 8 XCDs, so remap the linear id such that

@@ -17,6 +17,8 @@
 //
 // LDS (one array): W ring [3][K/64][64][64] bf16 (16-B chunk c of row r at c ^ (r & 7)),
 // then alpha / beta for all N columns.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -41,11 +43,18 @@ __device__ __forceinline__ void wait_vm() {
 // pieces are, in order, the previous step's A reloads and stores (s > 0), this step's
 // chunk-(s+2) pieces (more), its A reloads and its stores.  A reloads happen in at most one
 // of the two steps (rl).
+// vmcnt at the end of step s ("chunk s+1 landed"; its DMA went out at the start of step s-1).  Chunk c's
+// epilogue runs during step c+1's k-steps 1.., after that step's chunk DMA, so the ops younger than chunk
+// s+1's DMA are: step s-1's stores (of chunk s-2, s >= 2) and A reloads, then step s's chunk-(s+2) DMA
+// (more), its stores (of chunk s-1, s >= 1) and its A reloads (rl: reloads in either step).
 template <int P, int ST, int AL>
-__device__ __forceinline__ void wait_chunk(bool first, bool more, bool rl) {
-  if (first) {
-    if (more) { if (rl) wait_vm<P + AL + ST>(); else wait_vm<P + ST>(); }
-    else { if (rl) wait_vm<AL + ST>(); else wait_vm<ST>(); }
+__device__ __forceinline__ void wait_chunk(int s, bool more, bool rl) {
+  if (s == 0) {
+    if (more) { if (rl) wait_vm<P + AL>(); else wait_vm<P>(); }
+    else { if (rl) wait_vm<AL>(); else wait_vm<0>(); }
+  } else if (s == 1) {
+    if (more) { if (rl) wait_vm<P + ST + AL>(); else wait_vm<P + ST>(); }
+    else { if (rl) wait_vm<ST + AL>(); else wait_vm<ST>(); }
   } else {
     if (more) { if (rl) wait_vm<2 * ST + P + AL>(); else wait_vm<2 * ST + P>(); }
     else { if (rl) wait_vm<2 * ST + AL>(); else wait_vm<2 * ST>(); }
@@ -132,19 +141,69 @@ __global__ __launch_bounds__(512) void gemm_areg_kernel(ConvGemmArgs p) {
   if (total > 1) wait_vm<PIECES>(); else wait_vm<0>();
   __syncthreads();   // chunk 0 and alpha/beta visible to every wave
 
-  floatx4 acc[MT][NT];
+  // Two accumulator sets: chunk s accumulates into set s & 1 while chunk s-1's epilogue (GLU / act,
+  // stores) is interleaved with its k-steps — the epilogue's VALU work issues in the MFMAs' shadow
+  // instead of after a barrier where every wave of the CU would run it at once with the MFMA pipe idle.
+  floatx4 acc[2][MT][NT];
+  constexpr int G = ACT == kGlu ? MT * NT / 2 : MT * NT;   // epilogue groups (one 8/16-B store each)
+  // epilogue group gi of set SET: chunk column block ccol of tile ptile
+  auto epi_group = [&](auto SETC, int ptile, int ccol, int gi) {
+    constexpr int SET = decltype(SETC)::value;
+    const int mb = ptile * RB + wid * 32 + l15;
+    const int n0 = ccol * NB;
+    if constexpr (ACT == kGlu) {
+      const int mt = gi / (NT / 2), nt = (gi % (NT / 2)) * 2;
+      float o[4];
 #pragma unroll
-  for (int a = 0; a < MT; ++a)
+      for (int r = 0; r < 4; ++r) {
+        const int nv = n0 + nt * 16 + lk * 4 + r, ng = nv + 16;
+        const float av = fmaf(acc[SET][mt][nt][r], s_al[nv], s_be[nv]);
+        const float gt = fmaf(acc[SET][mt][nt + 1][r], s_al[ng], s_be[ng]);
+        o[r] = av * sigmoid_rcp(gt);
+      }
+      const int m = mb + mt * 16;
+      const int ch = ((n0 + nt * 16) >> 5) * 16 + lk * 4;
+      const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + ch) * 2) : kOOB;
+      const u32x2_t v = {pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+    } else {
+      const int mt = gi / NT, nt = gi % NT;
+      const int n = n0 + nt * 16 + lk * 4;
+      float x[4];
 #pragma unroll
-    for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) {
+        x[r] = fmaf(acc[SET][mt][nt][r], s_al[n + r], s_be[n + r]);
+        if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
+        if constexpr (ACT == kActSigmoid) x[r] = sigmoid_rcp(x[r]);
+        if constexpr (ACT == kActSilu) x[r] = x[r] * sigmoid_rcp(x[r]);
+      }
+      const int m = mb + mt * 16;
+      if (out_bf) {
+        const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + n) * 2) : kOOB;
+        const u32x2_t v = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+        __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
+      } else {
+        const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + n) * 4) : kOOB;
+        const u32x4_t v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 0);
+      }
+    }
+  };
 
   bool rl_prev = false;
-  for (int s = 0; s < total; ++s) {
+  int p_tile = 0, p_col = 0;   // the chunk whose epilogue is pending (set (s - 1) & 1)
+  auto step = [&](auto CURC, int s) {
+    constexpr int CUR = decltype(CURC)::value, PRV = 1 - CUR;
     const int j = s / n_chunks, c = s - j * n_chunks;
     const int tile = tile0 + j * grid;
     const bool reload = c == n_chunks - 1 && j + 1 < my_tiles;   // next tile's A during the last chunk
     const bool more = s + 2 < total;
+    const bool pend = s > 0;
     const uint16_t* Wst = Ws + (size_t)(s % NSLOT) * SLOT;
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[CUR][a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
     // W fragments of step kk+1 are read while the MFMAs of step kk run (double-buffered).
     auto read_w = [&](int kk, bf16x8* bfr) {
       const int sb = kk >> 1;
@@ -165,7 +224,7 @@ __global__ __launch_bounds__(512) void gemm_areg_kernel(ConvGemmArgs p) {
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nt], af[mt][kk], acc[mt][nt], 0, 0, 0);
+          acc[CUR][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nt], af[mt][kk], acc[CUR][mt][nt], 0, 0, 0);
       if (kk == 0) {
         // The chunk-(s+2) DMA goes out after the first MFMAs: on a tile's first chunk those wait
         // for the A fragments loaded during the previous chunk, and a DMA issued before them
@@ -178,66 +237,35 @@ __global__ __launch_bounds__(512) void gemm_areg_kernel(ConvGemmArgs p) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) load_a(tile + grid, mt, kk);
       }
+      // the pending epilogue's groups over k-steps 1 .. KT32-1 (after this step's chunk DMA)
+      if (pend && kk >= 1) {
+#pragma unroll
+        for (int gi = 0; gi < G; ++gi)
+          if (1 + gi * (KT32 - 1) / G == kk) epi_group(std::integral_constant<int, PRV>{}, p_tile, p_col, gi);
+      }
     }
-    // ---- epilogue of the 256 x 64 block: lane holds row mb + 16*mt, columns n0 + 16*nt + 4*lk + r
-    const int mb = tile * RB + wid * 32 + l15;
-    const int n0 = chunk_of(s) * NB;
-    if constexpr (ACT == kGlu) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; nt += 2) {
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int nv = n0 + nt * 16 + lk * 4 + r, ng = nv + 16;
-            const float a = fmaf(acc[mt][nt][r], s_al[nv], s_be[nv]);
-            const float gt = fmaf(acc[mt][nt + 1][r], s_al[ng], s_be[ng]);
-            o[r] = a / (1.f + __expf(-gt));
-          }
-          const int m = mb + mt * 16;
-          const int ch = ((n0 + nt * 16) >> 5) * 16 + lk * 4;
-          const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + ch) * 2) : kOOB;
-          const u32x2_t v = {pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
-        }
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const int n = n0 + nt * 16 + lk * 4;
-          float x[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            x[r] = fmaf(acc[mt][nt][r], s_al[n + r], s_be[n + r]);
-            if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
-            if constexpr (ACT == kActSigmoid) x[r] = 1.f / (1.f + __expf(-x[r]));
-            if constexpr (ACT == kActSilu) x[r] = x[r] / (1.f + __expf(-x[r]));
-          }
-          const int m = mb + mt * 16;
-          if (out_bf) {
-            const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + n) * 2) : kOOB;
-            const u32x2_t v = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
-            __builtin_amdgcn_raw_buffer_store_b64(v, ro, off, 0, 0);
-          } else {
-            const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.o_sw + n) * 4) : kOOB;
-            const u32x4_t v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]),
-                               __float_as_uint(x[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 0);
-          }
-        }
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    p_tile = tile;
+    p_col = chunk_of(s);
     if (s + 1 < total) {
-      wait_chunk<PIECES, ST, AL>(s == 0, more, reload || rl_prev);
+      wait_chunk<PIECES, ST, AL>(s, more, reload || rl_prev);
       // plain s_barrier: __syncthreads()' fence would add vmcnt(0) and drain the ring
       asm volatile("s_barrier" ::: "memory");
     }
     rl_prev = reload;
+  };
+  int s = 0;
+  for (; s + 1 < total; s += 2) {
+    step(std::integral_constant<int, 0>{}, s);
+    step(std::integral_constant<int, 1>{}, s + 1);
+  }
+  if (s < total) step(std::integral_constant<int, 0>{}, s);
+  // the last chunk's epilogue (set (total - 1) & 1)
+  if ((total - 1) & 1) {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) epi_group(std::integral_constant<int, 1>{}, p_tile, p_col, gi);
+  } else {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) epi_group(std::integral_constant<int, 0>{}, p_tile, p_col, gi);
   }
 }
 

@@ -232,8 +232,8 @@ __global__ __launch_bounds__(kRingThreads) void gemm_ring_kernel(ConvGemmArgs p)
       for (int r = 0; r < 4; ++r) {
         x[r] = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
         if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
-        if constexpr (ACT == kActSigmoid) x[r] = 1.f / (1.f + __expf(-x[r]));
-        if constexpr (ACT == kActSilu) x[r] = x[r] / (1.f + __expf(-x[r]));
+        if constexpr (ACT == kActSigmoid) x[r] = sigmoid_rcp(x[r]);
+        if constexpr (ACT == kActSilu) x[r] = x[r] * sigmoid_rcp(x[r]);
       }
       const int m = m0 + wm * TM + mt * 16 + l15;
       const int n = n0 + wn * TN + nt * 16 + lk * 4;
@@ -428,8 +428,8 @@ __global__ __launch_bounds__(kRingThreads) void gemm_ring_persist_kernel(ConvGem
             for (int r = 0; r < 4; ++r) {
               x[r] = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
               if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
-              if constexpr (ACT == kActSigmoid) x[r] = 1.f / (1.f + __expf(-x[r]));
-              if constexpr (ACT == kActSilu) x[r] = x[r] / (1.f + __expf(-x[r]));
+              if constexpr (ACT == kActSigmoid) x[r] = sigmoid_rcp(x[r]);
+              if constexpr (ACT == kActSilu) x[r] = x[r] * sigmoid_rcp(x[r]);
             }
             const int m = m0 + wm * TM + mt * 16 + l15;
             const int n = wn * TN + nt * 16 + lk * 4;

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
           for (int r = 0; r < 4; ++r) {
             const float a = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
             const float gt = fmaf(acc[mt][nt + 1][r], al[nt + 1][r], be[nt + 1][r]);
-            o[r] = a / (1.f + __expf(-gt));
+            o[r] = a * sigmoid_rcp(gt);
           }
           const int m = mb + mt * 16;
           const int ch = ((n0 + wn * TN + nt * 16) >> 5) * 16 + lk * 4;
@@ -213,8 +213,8 @@ __global__ __launch_bounds__(kStreamThreads) void gemm_stream_kernel(ConvGemmArg
           for (int r = 0; r < 4; ++r) {
             x[r] = fmaf(acc[mt][nt][r], al[nt][r], be[nt][r]);
             if constexpr (ACT == kActRelu) x[r] = fmaxf(x[r], 0.f);
-            if constexpr (ACT == kActSigmoid) x[r] = 1.f / (1.f + __expf(-x[r]));
-            if constexpr (ACT == kActSilu) x[r] = x[r] / (1.f + __expf(-x[r]));
+            if constexpr (ACT == kActSigmoid) x[r] = sigmoid_rcp(x[r]);
+            if constexpr (ACT == kActSilu) x[r] = x[r] * sigmoid_rcp(x[r]);
           }
           const int m = mb + mt * 16, n = nb + nt * 16;
           const bool ok = m < M && n < p.N;

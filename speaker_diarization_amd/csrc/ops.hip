@@ -685,7 +685,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
           for (int u = 0; u < 4; ++u) {
             const float a0 = __uint_as_float(aw[u] << 16), a1 = __uint_as_float(aw[u] & 0xffff0000u);
             const float g0 = __uint_as_float(gw[u] << 16), g1 = __uint_as_float(gw[u] & 0xffff0000u);
-            o[u] = pack_bf16x2(a0 / (1.f + __expf(-g0)), a1 / (1.f + __expf(-g1)));
+            o[u] = pack_bf16x2(a0 * sigmoid_rcp(g0), a1 * sigmoid_rcp(g1));
           }
           out = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
         float acc = bv;
 #pragma unroll
         for (int j = 0; j < kDwMaxK; ++j) acc = fmaf(wr[j], win[r + j], acc);
-        if (fused_silu) acc = acc / (1.f + __expf(-acc));
+        if (fused_silu) acc = acc * sigmoid_rcp(acc);
         const int t = t0 + r0 + r;
         if constexpr (BF) {
           otile[wv][r * kDwCB + lane] = f2bf_bits(acc);
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256) void groupnorm_silu_kernel(act_t<BF>* __restri
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float t = (x[i] - fm) * rstd * gg[i] + bb[i];
-      x[i] = t / (1.f + __expf(-t));
+      x[i] = t * sigmoid_rcp(t);
     }
     if constexpr (BF) {
       const uint4 u = {pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),

@@ -72,7 +72,7 @@ __device__ __forceinline__ void wait_piece(int younger) {
   else wait_vm<3 * DPW>();
 }
 
-__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+__device__ __forceinline__ float silu(float v) { return v * sigmoid_rcp(v); }
 
 // TT 16-token MFMA column tiles per wave; 8 / TT waves per 128-token tile.
 template <int TT>
@@ -306,8 +306,8 @@ void rowprog_kernel(RowProgArgs a) {
             for (int h = 0; h < 4; ++h) {
               float x0 = (__uint_as_float(w4[h] << 16) - fm) * rstd * gg[2 * h] + bb[2 * h];
               float x1 = (__uint_as_float(w4[h] & 0xffff0000u) - fm) * rstd * gg[2 * h + 1] + bb[2 * h + 1];
-              x0 = x0 / (1.f + __expf(-x0));
-              x1 = x1 / (1.f + __expf(-x1));
+              x0 = x0 * sigmoid_rcp(x0);
+              x1 = x1 * sigmoid_rcp(x1);
               pk[h] = pack_bf16x2(x0, x1);
             }
             af[tt][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
