@@ -148,16 +148,18 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
     };
     // The fragment of k-step kk + 1 is read while kk's two MFMAs run; the empty asm keeps the
     // compiler from hoisting every step's reads to the top.
-    bf16x8 wcur = wfrag(0);
+    constexpr int kWPD = 3;   // weight fragment reads in flight ahead of their MFMAs
+    bf16x8 wq[kWPD];
+#pragma unroll
+    for (int q = 0; q < kWPD; ++q) wq[q] = wfrag(q);
 #pragma unroll
     for (int kk = 0; kk < kKT32; ++kk) {
-      bf16x8 wnext = wcur;
-      if (kk + 1 < kKT32) wnext = wfrag(kk + 1);
+      const bf16x8 wcur = wq[kk % kWPD];
+      if (kk + kWPD < kKT32) wq[kk % kWPD] = wfrag(kk + kWPD);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
       if (ntile > 2) acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[2][kk], acc[2], 0, 0, 0);
       asm volatile("" ::: "memory");
-      wcur = wnext;
     }
     // lane holds features 16ft + 4lk + r of token rowj[rt]
     const int ld = c == 2 ? kVS : kQS;
