@@ -747,6 +747,151 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
 }
 
 
+// bf16 depthwise conv with the tap count K and the run length R fixed at compile time (the conformer
+// kernels 15 and 31): a lane owns a channel PAIR and produces R consecutive output rows, so every tap is
+// one packed FMA (v_pk_fma_f32) over the pair, the window element arrives as one 4-B LDS read (the pair's
+// bf16x2) + two bit ops, and nothing in the unrolled body branches (the runtime-k kernel above predicates
+// every window element).  A wave is two half-waves of 32 pairs = the block's 64 channels; the 8 half-waves
+// of the block take runs 0..7 of an 8R-row tile, rows of 128 B so the halves (R odd) read opposite bank
+// halves.  The tile's staged rows are all requested before the first LDS store (one HBM latency per
+// tile).  Per output element and tap the FMA order is the runtime kernel's (bias, then taps in order),
+// so the conv values are bit-identical to it; only the GroupNorm partial sums' summation order differs.
+template <int K, int R>
+__global__ __launch_bounds__(256) void dwconv_pk_kernel(const uint16_t* __restrict__ x, int T, int C,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        uint16_t* __restrict__ y, float* __restrict__ partial,
+                                                        int fused_silu, int glu_in) {
+  constexpr int kRows = 8 * R + K - 1;                  // staged rows per tile
+  constexpr int kItems = kRows * 8;                     // 16-B chunks (8 channels) per tile
+  constexpr int kIters = (kItems + 255) / 256;
+  constexpr int pad = (K - 1) / 2;
+  __shared__ uint32_t g[kRows * 32];                    // [row][32 channel pairs] bf16x2
+  __shared__ float red[2][256];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int s = blockIdx.y, c0 = blockIdx.x * kDwCB, nblk = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cp = lane & 31, slot = wv * 2 + (lane >> 5);
+  const int c = c0 + 2 * cp;                            // C % 64 == 0 (host check): both channels exist
+  f2 wr[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) wr[j] = f2{w[(int64_t)c * K + j], w[(int64_t)(c + 1) * K + j]};
+  const f2 bv = bias ? f2{bias[c], bias[c + 1]} : f2{0.f, 0.f};
+  const uint16_t* xs = x + (int64_t)s * T * (glu_in ? 2 : 1) * C;
+  uint16_t* ys = y + (int64_t)s * T * C;
+  float lsum = 0.f, lsq = 0.f;
+  for (int t0 = 0; t0 < T; t0 += 8 * R) {
+    uint4 va[kIters], vg[kIters];
+#pragma unroll
+    for (int u = 0; u < kIters; ++u) {
+      const int i = tid + u * 256, tt = i >> 3, ch = (i & 7) * 8, t = t0 - pad + tt;
+      va[u] = vg[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < kItems && t >= 0 && t < T) {
+        if (!glu_in) {
+          va[u] = *reinterpret_cast<const uint4*>(xs + (int64_t)t * C + c0 + ch);
+        } else {
+          const int cc = c0 + ch;   // pw1 rows interleaved in 32-column groups [16 values | 16 gates]
+          const uint16_t* ra = xs + (int64_t)t * 2 * C + (cc / 16) * 32 + cc % 16;
+          va[u] = *reinterpret_cast<const uint4*>(ra);
+          vg[u] = *reinterpret_cast<const uint4*>(ra + 16);
+        }
+      }
+    }
+    __syncthreads();   // the previous tile's reads of g are done
+#pragma unroll
+    for (int u = 0; u < kIters; ++u) {
+      const int i = tid + u * 256;
+      if (i >= kItems) break;
+      uint4 o = va[u];
+      if (glu_in) {
+        const uint32_t aw[4] = {va[u].x, va[u].y, va[u].z, va[u].w}, gw[4] = {vg[u].x, vg[u].y, vg[u].z, vg[u].w};
+        uint32_t r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a0 = __uint_as_float(aw[q] << 16), a1 = __uint_as_float(aw[q] & 0xffff0000u);
+          const float g0 = __uint_as_float(gw[q] << 16), g1 = __uint_as_float(gw[q] & 0xffff0000u);
+          r[q] = pack_bf16x2(a0 * sigmoid_rcp(g0), a1 * sigmoid_rcp(g1));
+        }
+        o = make_uint4(r[0], r[1], r[2], r[3]);
+      }
+      *reinterpret_cast<uint4*>(g + (i >> 3) * 32 + (i & 7) * 4) = o;
+    }
+    __syncthreads();
+    const int r0 = slot * R, nout = min(8 * R, T - t0) - r0;   // valid rows of this run
+    if (nout > 0) {
+      f2 acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = bv;
+      constexpr int kN = R + K - 1, kPf = 4;   // window elements; LDS reads issued kPf elements ahead
+      uint32_t uw[kN];
+#pragma unroll
+      for (int i = 0; i < kPf; ++i) uw[i] = g[(r0 + i) * 32 + cp];
+#pragma unroll
+      for (int i = 0; i < kN; ++i) {
+        if (i + kPf < kN) uw[i + kPf] = g[(r0 + i + kPf) * 32 + cp];
+        const uint32_t u = uw[i];
+        const f2 xv = f2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = i - r;
+          if (j >= 0 && j < K) acc[r] = __builtin_elementwise_fma(wr[j], xv, acc[r]);
+        }
+        // keep the FMAs of one window element together: left alone the scheduler emits each
+        // accumulator's 31-FMA dependent chain back to back (a dependency stall per FMA)
+#pragma unroll
+        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        f2 v = acc[r];
+        if (fused_silu) v = f2{v.x * sigmoid_rcp(v.x), v.y * sigmoid_rcp(v.y)};
+        if (r < nout) {
+          *reinterpret_cast<uint32_t*>(ys + (int64_t)(t0 + r0 + r) * C + c) = pack_bf16x2(v.x, v.y);
+          lsum += v.x + v.y;
+          lsq = fmaf(v.x, v.x, lsq);
+          lsq = fmaf(v.y, v.y, lsq);
+        }
+      }
+    }
+  }
+  if (fused_silu) return;   // uniform across the block
+  red[0][tid] = lsum;
+  red[1][tid] = lsq;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 0] = red[0][0];
+    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 1] = red[1][0];
+  }
+}
+
+// run length for the packed kernel: the R in {9, 13, 19} that stages the fewest rows over the sequence
+static int dwconv_pk_runlen(int T, int K) {
+  int best = 0;
+  long cost = 0;
+  for (int R : {9, 13, 19}) {
+    const long c = (long)cdiv(T, 8 * R) * (8 * R + K - 1);
+    if (!best || c < cost) best = R, cost = c;
+  }
+  return best;
+}
+
+template <int K>
+static void launch_dwconv_pk(int R, dim3 grid, hipStream_t st, const uint16_t* x, int T, int C, const float* w,
+                             const float* bias, uint16_t* y, float* partial, int fused_silu, int glu_in) {
+  if (R == 9)
+    hipLaunchKernelGGL((dwconv_pk_kernel<K, 9>), grid, dim3(256), 0, st, x, T, C, w, bias, y, partial, fused_silu, glu_in);
+  else if (R == 13)
+    hipLaunchKernelGGL((dwconv_pk_kernel<K, 13>), grid, dim3(256), 0, st, x, T, C, w, bias, y, partial, fused_silu, glu_in);
+  else
+    hipLaunchKernelGGL((dwconv_pk_kernel<K, 19>), grid, dim3(256), 0, st, x, T, C, w, bias, y, partial, fused_silu, glu_in);
+}
+
 void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
                 void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st) {
   SD_CHECK(fused_silu || partial, kErrInvalid, "glu_dwconv: GroupNorm partials buffer required");
@@ -755,8 +900,14 @@ void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
   dim3 grid(cdiv(C, kDwCB), S);
   const double eb = io_bf16 ? 2.0 : 4.0;
   ProfScope prof(glu_in ? "glu_dwconv" : "dwconv", 2.0 * S * T * C * k, eb * S * T * (glu_in ? 3.0 : 2.0) * C, st);
-  // (a channel-pair packed-f32 variant measured slower on C2 — 1.65 vs 1.52 ms for 6 launches — and was removed)
-  if (io_bf16)
+  static const bool no_pk = getenv("SDIAR_NO_DWCONV_PK") != nullptr;   // A/B switch: the runtime-k kernel
+  if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk) {
+    const int R = dwconv_pk_runlen(T, k);
+    auto xp = reinterpret_cast<const uint16_t*>(x);
+    auto yp = reinterpret_cast<uint16_t*>(y);
+    if (k == 31) launch_dwconv_pk<31>(R, grid, st, xp, T, C, w, bias, yp, partial, (int)fused_silu, (int)glu_in);
+    else launch_dwconv_pk<15>(R, grid, st, xp, T, C, w, bias, yp, partial, (int)fused_silu, (int)glu_in);
+  } else if (io_bf16)
     hipLaunchKernelGGL(glu_dwconv_kernel<true>, grid, dim3(256), 0, st, reinterpret_cast<const uint16_t*>(x), T,
                        C, w, bias, k, reinterpret_cast<uint16_t*>(y), partial, (int)fused_silu, (int)glu_in);
   else
