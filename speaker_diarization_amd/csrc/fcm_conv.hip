@@ -449,6 +449,185 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
   }
 }
 
+int g_fcm_cu = 0;
+
+// ---------------------------------------------------------------------------------
+// Ring variant of the stride-1 band conv (the production path for FCM's stride-1 3x3 convs, bf16 NHWC
+// in and out).  The band kernel above keeps ONE band's rows in flight (register prefetch, drained by the
+// band-end barrier), so every band paid an HBM latency that its 2-3 us of MFMA work did not cover, and
+// the residual load of each output tile waited behind the next band's prefetch (in-order vmcnt).  Here
+// bands are small (4 output rows x 64 frames) and arrive by LDS-DMA through a 3-slot ring, two bands
+// ahead of the one being computed; the band's residual tile rides in the same slot, so the epilogue
+// reads it from LDS.  Conv zero padding, the frames past W and the unused DMA lanes are out-of-range
+// buffer offsets (the DMA writes zeros, no memory traffic).  The 16-B chunks of a pixel are rotated by
+// (frame >> 2) in LDS so the 16 frames of an MFMA B fragment hit 16 distinct bank slots.  Same MFMA
+// and epilogue arithmetic, in the same order, as the band kernel: bit-identical outputs.
+constexpr int kRR = 4;                                   // output rows per band
+constexpr int kRB = 4;                                   // 16-frame blocks per band
+constexpr int kRPx = kRB * 16 + 2;                       // staged frames per input row
+constexpr int kRInChunks = (kRR + 2) * kRPx * 4;         // 16-B chunks of staged input (1584)
+constexpr int kRInInstr = (kRInChunks + 63) / 64;        // DMA instructions for them (25)
+constexpr int kRResChunks = kRR * kRB * 16 * 4;          // residual tile chunks (1024)
+constexpr int kRResBase = kRInInstr * 64;                // slot position of the residual tile
+template <bool RES>
+constexpr int ring_dma_per_wave() { return (kRInInstr + (RES ? kRResChunks / 64 : 0) + 7) / 8; }
+constexpr int kRNSlot = 3;
+template <bool RES>
+constexpr int ring_slot_bytes() { return ring_dma_per_wave<RES>() * 8 * 64 * 16; }
+
+__device__ __forceinline__ int ring_pos(int row, int px, int q, int row_px) {
+  return (row * row_px + px) * 4 + ((q + (px >> 2)) & 3);
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_ring_kernel(ConvGemmArgs p, int n_bands, int n_tt) {
+  constexpr int kDma = ring_dma_per_wave<RES>();
+  constexpr int kSlot = ring_slot_bytes<RES>();
+  extern __shared__ __attribute__((aligned(1024))) uint16_t xs[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, q = lane >> 4;
+  const int H = p.H, W = p.W;
+  const int n_rb = (p.Ho + kRR - 1) / kRR;
+  bf16x8 wf[9][2];
+  {
+    const uint16_t* Wt = reinterpret_cast<const uint16_t*>(p.Wt);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        wf[t][nt] = *reinterpret_cast<const bf16x8*>(Wt + band_channel(l15, nt) * 288 + t * 32 + q * 8);
+  }
+  float al[2][4], be[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = band_channel(4 * q + r, nt);
+      al[nt][r] = p.alpha ? p.alpha[c] : 1.f;
+      be[nt][r] = p.beta ? p.beta[c] : 0.f;
+    }
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), (short)0,
+                                                                      (int)kFcmOOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(RES ? p.res : p.A), (short)0,
+                                                                      (int)kFcmOOB, 0x00020000);
+  // this lane's chunk of each of the wave's DMAs: DMA k writes slot positions (k * 8 + wv) * 64 + lane
+  int d_row[kDma], d_px[kDma], d_q[kDma];
+#pragma unroll
+  for (int k = 0; k < kDma; ++k) {
+    const int gi = k * 8 + wv;
+    int pos = gi * 64 + lane, row_px = kRPx;
+    if (gi >= kRInInstr) pos -= kRResBase, row_px = kRB * 16;
+    const int row = pos / (row_px * 4), rem = pos - row * row_px * 4, px = rem >> 2;
+    d_row[k] = row;
+    d_px[k] = px;
+    d_q[k] = ((rem & 3) - (px >> 2)) & 3;
+  }
+  // XCD-aware band order: the workgroups of one XCD (blockIdx % 8) take consecutive bands, so a band and
+  // its row neighbours (which re-read two of its input rows) are served by the same L2
+  const int G = gridDim.x;
+  const int vb = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  auto issue = [&](int band, int slot) {
+    const int tt = band % n_tt, bh = band / n_tt;
+    const int b = bh / n_rb, ho0 = (bh % n_rb) * kRR, w0 = tt * kRB * 16;
+#pragma unroll
+    for (int k = 0; k < kDma; ++k) {
+      const int gi = k * 8 + wv;
+      const auto* lds = (const __attribute__((address_space(3))) void*)(xs + (slot * kSlot + gi * 1024) / 2);
+      if (gi < kRInInstr) {
+        const int h = ho0 - 1 + d_row[k], w = w0 - 1 + d_px[k];
+        const bool ok = gi * 64 + lane < kRInChunks && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const uint32_t off =
+            ok ? (uint32_t)(((((int64_t)b * H + h) * W + w) * p.lda + p.a_coff + d_q[k] * 8) * 2) : kFcmOOB;
+        dma_lds16_buf(ra, off, lds);
+      } else {
+        const int ho = ho0 + d_row[k], wo = w0 + d_px[k];
+        const bool ok = RES && gi * 64 + lane - kRResBase < kRResChunks && ho < p.Ho && wo < p.Wo;
+        const uint32_t off =
+            ok ? (uint32_t)(((((int64_t)b * p.Ho + ho) * p.Wo + wo) * p.res_ld + d_q[k] * 8) * 2) : kFcmOOB;
+        dma_lds16_buf(rr, off, lds);
+      }
+    }
+  };
+  auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  const int nb_mine = n_bands > vb ? (n_bands - vb + G - 1) / G : 0;   // bands of this workgroup
+  if (nb_mine > 0) issue(vb, 0);
+  if (nb_mine > 1) issue(vb + G, 1);
+  for (int i = 0; i < nb_mine; ++i) {
+    // band i landed: only band i + 1's DMAs (and this wave's stores) are younger; outstanding <= kDma
+    // then implies all of band i's DMAs are done (loads complete in order)
+    if (i + 1 < nb_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();   // every wave's part of band i is in LDS; every wave is done with band i - 1's slot
+    if (i + 2 < nb_mine) issue(vb + (i + 2) * G, (i + 2) % kRNSlot);
+    const int band = vb + i * G;
+    const int tt = band % n_tt, bh = band / n_tt;
+    const int b = bh / n_rb, ho0 = (bh % n_rb) * kRR, w0 = tt * kRB * 16;
+    const uint16_t* sx = xs + (i % kRNSlot) * (kSlot / 2);
+#pragma unroll
+    for (int j = 0; j < kRR * kRB / 8; ++j) {
+      const int it = wv + 8 * j, r = it / kRB, blk = it % kRB;
+      const int ho = ho0 + r;
+      if (ho >= p.Ho) break;
+      floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(sx + ring_pos(r + dh, blk * 16 + l15 + dw, q, kRPx) * 8);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[dh * 3 + dw][nt], af, acc[nt], 0, 0, 0);
+        }
+      const int wo = w0 + blk * 16 + l15;
+      float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) {
+        const u32x4_t r4 = *reinterpret_cast<const u32x4_t*>(sx + (kRResBase + ring_pos(r, blk * 16 + l15, q, kRB * 16)) * 8);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          rv[2 * u] = __uint_as_float(r4[u] << 16);
+          rv[2 * u + 1] = __uint_as_float(r4[u] & 0xffff0000u);
+        }
+      }
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = fmaf(acc[u >> 2][u & 3], al[u >> 2][u & 3], be[u >> 2][u & 3]) + rv[u];
+        if (RELU) v[u] = fmaxf(v[u], 0.f);   // apply_act(., kActRelu)
+      }
+      if (wo < p.Wo)
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.out) + (((int64_t)b * p.Ho + ho) * p.Wo + wo) * 32 +
+                                  q * 8) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                      pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+  }
+}
+
+bool ring_ok(const ConvGemmArgs& p) {
+  const int64_t in_bytes = (int64_t)p.B * p.H * p.W * p.lda * 2;
+  const int64_t res_bytes = p.res ? (int64_t)p.B * p.Ho * p.Wo * p.res_ld * 2 : 0;
+  return p.sh == 1 && (p.act == kActRelu || p.act == kActNone) && p.out_bf16 && p.o_sn == 1 && p.o_sw == 32 && p.o_sh == (int64_t)p.Wo * 32 &&
+         p.o_sb == (int64_t)p.Ho * p.o_sh && (!p.res || (p.res_bf16 && p.res_ld % 8 == 0)) &&
+         in_bytes < (int64_t)kFcmOOB && res_bytes < (int64_t)kFcmOOB;
+}
+
+template <bool RES, bool RELU>
+void launch_ring(const ConvGemmArgs& p, hipStream_t st) {
+  const int n_tt = cdiv(p.Wo, kRB * 16);
+  const int64_t bands = (int64_t)p.B * cdiv(p.Ho, kRR) * n_tt;
+  SD_CHECK(bands < (1ll << 31), kErrInvalid, "fcm conv: too many bands");
+  constexpr size_t smem = (size_t)kRNSlot * ring_slot_bytes<RES>();
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_ring_kernel<RES, RELU>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    attr = true;
+  }
+  const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
+  hipLaunchKernelGGL((fcm_conv3x3_ring_kernel<RES, RELU>), dim3(grid), dim3(kBandThreads), smem, st, p, (int)bands, n_tt);
+}
+
 // Time tiling: the fewest tiles whose 16-frame blocks (at most kBandMaxBlk, so a
 // staged row stays <= 306 frames) cover W, blocks spread evenly over them.
 constexpr int kBandMaxBlk = 19;
@@ -476,8 +655,6 @@ bool band_fits(const ConvGemmArgs& p) {
          (int64_t)p.B * p.H * p.W * p.lda * 2 < (int64_t)kFcmOOB &&
          (!p.res || (p.res_ld % 8 == 0)) && (p.o_sn != 1 || p.o_sw % 8 == 0);
 }
-
-int g_fcm_cu = 0;
 
 template <int R, int SH, bool STEM = false, bool SC = false>
 void launch_band(const ConvGemmArgs& p, hipStream_t st, const FcmFuse& f = FcmFuse{}) {
@@ -512,6 +689,14 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
     SD_HIP(hipDeviceGetAttribute(&g_fcm_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
   static const bool no_band = getenv("SDIAR_NO_FCM_BAND") != nullptr;
+  static const bool no_ring = getenv("SDIAR_NO_FCM_RING") != nullptr;   // A/B switch: the band kernel
+  if (!no_band && !no_ring && ring_ok(p)) {
+    const bool relu = p.act == kActRelu;
+    if (p.res) relu ? launch_ring<true, true>(p, st) : launch_ring<true, false>(p, st);
+    else relu ? launch_ring<false, true>(p, st) : launch_ring<false, false>(p, st);
+    SD_LAUNCH_CHECK();
+    return;
+  }
   if (!no_band && p.sh == 1 && band_fits<4, 1>(p)) {
     launch_band<4, 1>(p, st);
     SD_LAUNCH_CHECK();

@@ -103,3 +103,39 @@ def test_switch_group_matches_goldens(gpu, group):
     bad = {k: v for k, v in res.items() if not v[0] < v[1]}
     print(group, {k: round(v[0], 5) for k, v in res.items()})
     assert not bad, bad
+
+
+BITS_CHILD = r"""
+import hashlib, os, sys
+import numpy as np, torch
+sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests", "golden"))
+from make_golden import campp_inputs
+from speaker_diarization_amd.ts_vad.embedding import CAMPPlus
+from speaker_diarization_amd.weights import campplus_state_dict, to_torch
+dev = torch.device("cuda", 0)
+m = CAMPPlus(feat_dim=80, embedding_size=192, device=dev, precision="bf16", max_batch=6, max_frames=600)
+m.load_state_dict(to_torch(campplus_state_dict(5, 192)))
+h = hashlib.sha256()
+for B, T, seed in ((6, 600, 1), (1, 333, 2), (3, 97, 3)):
+    x = torch.from_numpy(campp_inputs(B, T, seed)).to(dev)
+    h.update(m(x, get_time_out=True).float().cpu().numpy().tobytes())
+print("HASH " + h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("switch", ["SDIAR_NO_FCM_RING"])
+def test_switch_is_bit_identical(gpu, switch):
+    """Kernels documented as bit-identical to the path their switch restores (same MFMA and epilogue
+    arithmetic in the same order): the CAM++ trunk's output bits with and without the switch."""
+    hashes = []
+    for on in (False, True):
+        env = dict(os.environ)
+        env.pop(switch, None)
+        if on:
+            env[switch] = "1"
+        r = subprocess.run([sys.executable, "-c", BITS_CHILD.format(repo=REPO)], capture_output=True, text=True,
+                           timeout=110, env=env)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
+        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
+        hashes.append(line[0])
+    assert hashes[0] == hashes[1], hashes
