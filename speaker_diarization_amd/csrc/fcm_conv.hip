@@ -192,13 +192,21 @@ __host__ __device__ inline int band_channel(int i, int nt) { return 8 * (i >> 2)
 //   STEM  the staged input rows are head.conv1 (1 -> 32, 3x3, pad 1) + BN + ReLU computed in LDS from the
 //         fbank rows they need (cam_pplus_wespeaker.py:277-301), so the 80-bin 32-channel stem map (1.84 GB
 //         for a 10-min C2 meeting) is never written.  Same fmaf order as fcm_conv1_kernel (bit-identical).
-template <int R, int SH, bool STEM = false, bool SC = false>
+// TOUT: FCM head.conv2, whose output is the TDNN input (B, T, 32 * Ho) with channel c * Ho + h: a band is
+// ALL Ho = R output rows of kToutBlk 16-frame blocks, so its output is one contiguous run of whole
+// 640-B frame rows.  The epilogue scatters into an LDS image of those rows and the band leaves as 16-B
+// stores (per-element stores of R-row bands left every frame row to be assembled from 2-B pieces by
+// five different bands).
+constexpr int kToutBlk = 4;
+constexpr int kToutRow = 328;   // LDS frame-row stride in bf16 (656 B: 16-B aligned, rows 36 banks apart)
+
+template <int R, int SH, bool STEM = false, bool SC = false, bool TOUT = false>
 __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, FcmFuse f, int n_bands,
                                                                        int n_blk) {
   // A band: (image b, R output rows from ho0, time tile tt of n_blk 16-frame blocks).
   constexpr int NR = (R - 1) * SH + 3;
   // staged 16-B vectors per thread: NR rows x (at most 19 x 16 + 2 = 306 frames) x 4 (band_fits checks it)
-  constexpr int kVP = (NR * 306 * 4 + kBandThreads - 1) / kBandThreads;
+  constexpr int kVP = (NR * (TOUT ? kToutBlk * 16 + 2 : 306) * 4 + kBandThreads - 1) / kBandThreads;
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];   // [NR][TW+2][kPS] (+ STEM: fbank tile)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l15 = lane & 15, q = lane >> 4;
@@ -266,7 +274,12 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
       v[k] = make_uint4(x.x, x.y, x.z, x.w);
       px += 128;
-      if (px >= Wp) {
+      if constexpr (TOUT) {   // Wp < 128: the frame index can wrap twice
+        while (px >= Wp) {
+          px -= Wp;
+          ++rr;
+        }
+      } else if (px >= Wp) {
         px -= Wp;
         ++rr;
       }
@@ -431,7 +444,11 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         v[u] = apply_act(fmaf(acc[u >> 2][u & 3], al[u >> 2][u & 3], be[u >> 2][u & 3]) + rv[u], p.act);
-      if (nhwc && p.out_bf16) {
+      if constexpr (TOUT) {   // output row r of frame wo -> its LDS frame row, channel c at c * R + r
+        uint16_t* so = xs + NR * Wp * kPS + (blk * 16 + l15) * kToutRow + r;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) so[(c0 + u) * R] = f2bf_bits(v[u]);
+      } else if (nhwc && p.out_bf16) {
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.out) + pix * 32 + c0) =
             make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                        pack_bf16x2(v[6], v[7]));
@@ -443,6 +460,17 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
           if (p.out_bf16) reinterpret_cast<uint16_t*>(p.out)[o] = f2bf_bits(v[u]);
           else reinterpret_cast<float*>(p.out)[o] = v[u];
         }
+      }
+    }
+    if constexpr (TOUT) {   // the band's frame rows are contiguous in the output: 16-B copies
+      __syncthreads();
+      const int nfr = min(n_blk * 16, p.Wo - wo0), cpr = R * 4;
+      uint16_t* ob = reinterpret_cast<uint16_t*>(p.out) + ((int64_t)b * p.Wo + wo0) * 32 * R;
+      const uint16_t* so = xs + NR * Wp * kPS;
+      for (int i = tid; i < nfr * cpr; i += kBandThreads) {
+        const int fr = i / cpr, ck = i - fr * cpr;
+        *reinterpret_cast<uint4*>(ob + (int64_t)fr * 32 * R + ck * 8) =
+            *reinterpret_cast<const uint4*>(so + fr * kToutRow + ck * 8);
       }
     }
     __syncthreads();   // xs free for the next band
@@ -675,6 +703,32 @@ void launch_band(const ConvGemmArgs& p, hipStream_t st, const FcmFuse& f = FcmFu
 
 }  // namespace
 
+// FCM head.conv2 (stride 2 to Ho = 10 rows) into the TDNN's (B, T, 32 * Ho) layout: see TOUT above
+bool tout_ok(const ConvGemmArgs& p) {
+  return p.sh == 2 && p.Ho == 10 && p.out_bf16 && !p.res && p.o_sn == p.Ho && p.o_sh == 1 &&
+         p.o_sw == 32 * p.Ho && p.o_sb == (int64_t)p.Wo * 32 * p.Ho &&
+         (int64_t)p.B * p.H * p.W * p.lda * 2 < (int64_t)kFcmOOB;
+}
+
+void launch_tout(const ConvGemmArgs& p, hipStream_t st) {
+  constexpr int R = 10, NR = (R - 1) * 2 + 3;
+  const int n_tt = cdiv(p.Wo, kToutBlk * 16);
+  const int64_t bands = (int64_t)p.B * n_tt;
+  SD_CHECK(bands < (1ll << 31), kErrInvalid, "fcm conv: too many bands");
+  const size_t smem = (size_t)NR * (kToutBlk * 16 + 2) * kPS * 2 + (size_t)kToutBlk * 16 * kToutRow * 2;
+  static_assert((size_t)NR * (kToutBlk * 16 + 2) * kPS * 2 + (size_t)kToutBlk * 16 * kToutRow * 2 <= 160 * 1024,
+                "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, 2, false, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    attr = true;
+  }
+  const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
+  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, 2, false, false, true>), dim3(grid), dim3(kBandThreads), smem, st,
+                     p, FcmFuse{}, (int)bands, kToutBlk);
+}
+
 bool fcm_conv_supported(const ConvGemmArgs& p) {
   return p.a_bf16 && !p.pre_scale && !p.gate && p.kh == 3 && p.kw == 3 && p.Cin == 32 && p.N == 32 &&
          p.K == 288 && p.ph == 1 && p.pw == 1 && p.sw == 1 && (p.sh == 1 || p.sh == 2) && p.dh == 1 &&
@@ -699,6 +753,12 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
   }
   if (!no_band && p.sh == 1 && band_fits<4, 1>(p)) {
     launch_band<4, 1>(p, st);
+    SD_LAUNCH_CHECK();
+    return;
+  }
+  static const bool no_tout = getenv("SDIAR_NO_FCM_TOUT") != nullptr;   // A/B switch: per-element stores
+  if (!no_band && !no_tout && tout_ok(p)) {
+    launch_tout(p, st);
     SD_LAUNCH_CHECK();
     return;
   }

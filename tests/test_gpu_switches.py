@@ -123,7 +123,7 @@ print("HASH " + h.hexdigest())
 """
 
 
-@pytest.mark.parametrize("switch", ["SDIAR_NO_FCM_RING"])
+@pytest.mark.parametrize("switch", ["SDIAR_NO_FCM_RING", "SDIAR_NO_FCM_TOUT"])
 def test_switch_is_bit_identical(gpu, switch):
     """Kernels documented as bit-identical to the path their switch restores (same MFMA and epilogue
     arithmetic in the same order): the CAM++ trunk's output bits with and without the switch."""
