@@ -9,8 +9,10 @@
 //   stored at chunk c ^ (r & 7) (swizzle applied on the SOURCE address, the
 //   DMA destination stays lane-linear), which makes the MFMA fragment reads
 //   (ds_read_b128, 16 rows x one chunk) bank-conflict free.
-// * 2 LDS stages: the DMA of tile k+1 is in flight while tile k is consumed;
-//   one vmcnt(0) + barrier per k-tile.
+// * NS-stage LDS ring: the DMAs of k-tiles k+1 .. k+NS-1 are in flight while tile k is consumed; the
+//   DMAs are inline asm (invisible to the compiler's wait-count pass), so each k-tile costs one counted
+//   vmcnt wait + one barrier.  The BN-ReLU prologue's per-channel scale / shift live in LDS, so no
+//   compiler-visible global load sits in the loop either (its wait would drain the ring).
 // * Epilogue identical to gemm_bf16.hip (LDS-staged, coalesced, bf16/fp32 out).
 // Handles taps == 1 (linear / 1x1 conv) and multi-tap convs with Cin % 64 == 0.
 #include <string>
@@ -30,7 +32,9 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
   return (uint32_t)f2bf_bits(a) | ((uint32_t)f2bf_bits(b) << 16);
 }
 
-template <int BM, int BN>
+constexpr int kPreMax = 1024;   // prologue channels staged in LDS
+
+template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   constexpr int TM = BM / 2, TN = BN / 2;
   constexpr int MT = TM / 16, NT = TN / 16;
@@ -39,8 +43,10 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   constexpr int STAGE = (BM + BN) * BK;   // bf16 elements per stage
   constexpr int CLD = BN + 4;
   constexpr int EPI = BM * CLD * 2;
-  constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  constexpr int SMEM = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  constexpr int DPW = AI + BI;       // DMA instructions per wave per k-tile
   __shared__ __attribute__((aligned(1024))) uint16_t sm[SMEM];
+  __shared__ float pre_ss[2 * kPreMax];   // prologue scale | shift per input channel
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -167,10 +173,10 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
     const int c = k - tap * p.Cin;                  // their channel (k itself for one tap)
     float sc[8], sh[8];
     if (k + 8 <= ke) {
-      const float4 s0 = *reinterpret_cast<const float4*>(p.pre_scale + c);
-      const float4 s1 = *reinterpret_cast<const float4*>(p.pre_scale + c + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(p.pre_shift + c);
-      const float4 h1 = *reinterpret_cast<const float4*>(p.pre_shift + c + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(pre_ss + c);
+      const float4 s1 = *reinterpret_cast<const float4*>(pre_ss + c + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(pre_ss + kPreMax + c);
+      const float4 h1 = *reinterpret_cast<const float4*>(pre_ss + kPreMax + c + 4);
       sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
       sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
     } else {
@@ -197,17 +203,31 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
     }
   };
   const bool pre = p.pre_scale != nullptr;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (pre) {
+    const int cin = taps > 1 ? p.Cin : p.K;
+    for (int i = tid; i < cin; i += 256) {
+      pre_ss[i] = p.pre_scale[i];
+      pre_ss[kPreMax + i] = p.pre_shift[i];
+    }
+  }
+  // a plain barrier (LDS writes done): a __syncthreads() fence would add vmcnt(0) and drain the ring
+  auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < KT) issue(s, s);
   for (int kt = 0; kt < KT; ++kt) {
-    const int stg = kt & 1;
+    const int stg = kt % NS;
+    // k-tile kt landed: only the tiles issued after it (kt + 1 .. kt + NS - 2, DPW DMAs each) are younger
+    const int younger = min(KT - 1, kt + NS - 2) - kt;
+    if (NS >= 4 && younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+    else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();   // tile kt visible to every wave; every wave is done with tile kt - 1's stage
     if (pre) {
       prologue(kt, stg);
-      // LDS writes done, then a plain barrier (a __syncthreads() fence would add vmcnt(0))
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      barrier();
     }
-    if (kt + 1 < KT) issue(kt + 1, stg ^ 1);
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const uint16_t* As = sm + stg * STAGE;
     const uint16_t* Bs = As + BM * BK;
 #pragma unroll
@@ -229,9 +249,8 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  barrier();   // every wave is done with the ring: the epilogue tile takes over its LDS
 
   // ---- epilogue (LDS-staged, row-contiguous 4-column groups)
   float* Cs = reinterpret_cast<float*>(sm);
@@ -378,11 +397,18 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   }
 }
 
+// ring depth 2: two 64-KiB workgroups per CU overlap one's BN-ReLU prologue pass with the other's MFMAs;
+// a 4-stage ring at one workgroup per CU measured slower (C2 gemm_dma 0.60 -> 0.90 ms; 2 stages: 0.56)
+template <int BM, int BN>
+constexpr int dma_stages() {
+  return 2;
+}
+
 template <int BM, int BN>
 void launch(const ConvGemmArgs& p, hipStream_t st) {
   const int M = p.B * p.Ho * p.Wo;
   dim3 grid(cdiv(p.N, BN) * cdiv(M, BM), p.ksplit > 1 ? p.ksplit : 1);
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, dma_stages<BM, BN>()>), grid, dim3(256), 0, st, p);
 }
 
 }  // namespace
@@ -391,7 +417,8 @@ bool gemm_dma_supported(const ConvGemmArgs& p) {
   const int taps = p.kh * p.kw;
   const int64_t a_bytes = ((int64_t)p.B * p.H * p.W) * p.lda * 2;
   const int64_t w_bytes = (int64_t)p.N * p.K * 2;
-  return p.a_bf16 && (!p.pre_scale || (p.pre_shift && (taps == 1 || p.Cin % BK == 0))) && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
+  return p.a_bf16 && (!p.pre_scale || (p.pre_shift && (taps == 1 || p.Cin % BK == 0) &&
+                                       (taps > 1 ? p.Cin : p.K) <= kPreMax)) && (taps == 1 || p.Cin % BK == 0) && p.K % 8 == 0 && p.lda % 8 == 0 &&
          p.a_coff % 8 == 0 && a_bytes < (int64_t)kOOB && w_bytes < (int64_t)kOOB;
 }
 
