@@ -110,7 +110,10 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   // Linear + LayerNorm
   conv_gemm(lin(Tens{const_cast<float*>(feats), false}, rows, ld_in, in_.w, in_.beta, Tens{Y_, false}, E), bf, st);
   layernorm(Y_, rows, E, E, norm_g_, norm_b_, 1e-5f, X_, E, false, st);
-  for (size_t i = 0; i < tfm_.size(); ++i) run_transformer(tfm_[i], X_, S, T, E, cfg_.n_heads, key_len, w, st, 0, 0, i > 0);
+  // bf16(X) for the first layer's in-projection (later layers get it from the LayerNorms): see tsvad.cpp
+  if (bf && !tfm_.empty()) f32_to_bf16(X_, (int64_t)rows * E, AO_, st);
+  for (size_t i = 0; i < tfm_.size(); ++i)
+    run_transformer(tfm_[i], X_, S, T, E, cfg_.n_heads, key_len, w, st, 0, 0, bf || i > 0);
   run_conformer_stack(conf_, X_, S, T, E, cfg_.n_heads, 31, key_len, w, st);
   if (plain) {   // eend/models.py:97-99: decoder Linear, activation=sigmoid (eend_infer.py:69)
     ConvGemmArgs p = lin(Tens{X_, false}, rows, E, dec_.w, dec_.beta, Tens{act, false}, cfg_.n_speakers);

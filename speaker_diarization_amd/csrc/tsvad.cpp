@@ -132,15 +132,19 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_CHECK(Tl <= pe_len_, kErrShape, "label length exceeds positional-encoding max_len");
     // Per-speaker encoder over S = B*NS sequences (model.py:869-879).
     build_speaker_input(ts, mix_, SE, T3, B, NS, Tl, SE, pe_, X_, st);
+    // bf16(X) for the first layer's in-projection too (every later layer gets it from the LayerNorms): an
+    // fp32 A operand would send that GEMM to the register-staged kernel (C4: 1.5 ms per 640 windows vs 0.3)
+    if (bf) f32_to_bf16(X_, (int64_t)S * Tl * E, enc_work().AO, st);
     for (size_t i = 0; i < single_.size(); ++i)
-      run_transformer(single_[i], X_, S, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, i > 0);
+      run_transformer(single_[i], X_, S, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, bf || i > 0);
     speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     ConvGemmArgs p = cam_conv1d(Tens{X2_, bf}, B, Tl, NS * E, backend_down_, 1, 2, 1, Tens{X_, false}, E);
     p.act = kActRelu;
     conv_gemm(p, bf, st);
     add_pe(X_, B * Tl, Tl, E, E, pe_, st);
+    if (bf) f32_to_bf16(X_, (int64_t)B * Tl * E, enc_work().AO, st);
     for (size_t i = 0; i < multi_.size(); ++i)
-      run_transformer(multi_[i], X_, B, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, i > 0);
+      run_transformer(multi_[i], X_, B, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, bf || i > 0);
     ConvGemmArgs f = cam_conv1d(Tens{X_, false}, B, Tl, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
