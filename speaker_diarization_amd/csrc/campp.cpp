@@ -146,9 +146,25 @@ void CamTrunk::alloc(DeviceArena& a, int max_batch, int max_frames) {
   gate_ = ws(a, Bm * ((T2 + 99) / 100) * 32);
 }
 
-Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
+Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0) const {
   const bool bf = bf16_;   // bf16 mode: CAM++ activations stored as bf16
   const int F = 80;
+  // Windows [b0, b0 + B) of a larger batch: every workspace map is addressed from its window-b0 slice (the
+  // FCM buffers with their largest row count as the per-window stride), so two slices of one batch can run
+  // concurrently on two streams and leave the full-batch layout behind.
+  const int64_t esz = bf ? 2 : 4, T2w = out_frames(Tf);
+  auto sl = [&](float* p, int64_t per, int64_t bytes) {
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(p) + b0 * per * bytes);
+  };
+  const float* ref = fbank + (int64_t)b0 * Tf * F;
+  float* const fcmA = sl(fcmA_, 80LL * Tf * 32, esz);
+  float* const fcmB = sl(fcmB_, 80LL * Tf * 32, esz);
+  float* const fcmC = sl(fcmC_, 40LL * Tf * 32, esz);
+  float* const x0 = sl(x0_, (int64_t)Tf * 320, esz);
+  float* const dd[3] = {sl(d_[0], T2w * 512, esz), sl(d_[1], T2w * 1024, esz), sl(d_[2], T2w * 1024, esz)};
+  float* const x4 = sl(x4_, T2w * kChannels, esz);
+  float* const tmp = sl(tmp_, T2w * 128, esz);
+  float* const gate = sl(gate_, ((T2w + 99) / 100) * 32, 4);
   // ---------------- FCM head (cam_pplus_wespeaker.py:271-308), NHWC (B, F, T, 32)
   // layer1.0: A(80) -> B(40); shortcut A -> C(40); conv2 B -> A(40) + C
   // layer1.1: A -> B; conv2 B -> C + A
@@ -156,9 +172,9 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
   // layer2.1: C -> A; conv2 A -> B + C
   // bf16: layer1.0's conv1 computes the stem (head.conv1 + bn1 + relu) from the fbank in LDS, and the two
   // strided blocks' shortcuts ride on their conv1's centre tap (fcm_conv.hip FcmFuse).
-  float* cur = fcmA_;
+  float* cur = fcmA;
   int H = F;
-  float* bufs[3] = {fcmA_, fcmB_, fcmC_};
+  float* bufs[3] = {fcmA, fcmB, fcmC};
   bool stem_done = false;
   for (size_t i = 0; i < fcm_blocks_.size(); ++i) {
     const ResBlock& rb = fcm_blocks_[i];
@@ -179,7 +195,7 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
     }
     const bool fused = bf && !no_fused_ && rb.has_sc && rb.sc.w.N == 32 && rb.sc.w.K == 32 && fcm_fused_supported(p, fu);
     if (i == 0 && !fused) {
-      fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA_, bf, st);
+      fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA, bf, st);
       stem_done = true;
     }
     SD_CHECK(i != 0 || fused || stem_done, kErrInvalid, "FCM stem not computed");
@@ -204,7 +220,7 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
   }
   {
     // head.conv2 (stride (2,1)) + bn2 + relu, stored as (B, T, C*F') with channel c*F'+f.
-    ConvGemmArgs p = conv2d(Tens{cur, bf}, B, H, Tf, fcm_conv2_, 2, 1, 1, 1, Tens{x0_, bf});
+    ConvGemmArgs p = conv2d(Tens{cur, bf}, B, H, Tf, fcm_conv2_, 2, 1, 1, 1, Tens{x0, bf});
     p.act = kActRelu;
     const int Fo = p.Ho;
     SD_CHECK(Fo * 32 == 320, kErrShape, "FCM output width mismatch");
@@ -215,14 +231,14 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
   const int T2 = out_frames(Tf);
   const int ctot[3] = {512, 1024, 1024};
   {
-    ConvGemmArgs p = cam_conv1d(Tens{x0_, bf}, B, Tf, 320, tdnn_, 2, 2, 1, Tens{d_[0], bf}, ctot[0]);
+    ConvGemmArgs p = cam_conv1d(Tens{x0, bf}, B, Tf, 320, tdnn_, 2, 2, 1, Tens{dd[0], bf}, ctot[0]);
     p.act = kActRelu;
     SD_CHECK(p.Wo == T2, kErrShape, "tdnn output length");
     conv_gemm(p, bf, st);
   }
   int cin = 128;
   for (int b = 0; b < 3; ++b) {
-    const Tens D{d_[b], bf};
+    const Tens D{dd[b], bf};
     const int ld = ctot[b];
     for (const DenseL& L : dense_[b]) {
       SD_CHECK(L.bottleneck.w.Cin == cin, kErrParam, "dense layer input width");
@@ -235,7 +251,7 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
         cin += L.local.w.N;
         continue;
       }
-      ConvGemmArgs p = cam_conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp_, bf}, 128);
+      ConvGemmArgs p = cam_conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp, bf}, 128);
       p.act = kActRelu;
       conv_gemm(p, bf, st);
       if (!no_fused_ && cam_local_fused_supported(128, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil, 100, ld, bf)) {
@@ -243,27 +259,27 @@ Tens CamTrunk::forward(const float* ref, int B, int Tf, hipStream_t st) const {
         // computes the gate.  Large batches: the context kernel, then the conv kernel reading
         // only each segment's window rows (fewer bytes per workgroup, higher occupancy).
         if (B * ((T2 + 99) / 100) < 1024) {
-          cam_local_fused(tmp_, B, T2, L.dil, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
+          cam_local_fused(tmp, B, T2, L.dil, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
                           act_at(D, cin).p, ld, st);
         } else {
-          cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
-          cam_local_conv(tmp_, B, T2, L.dil, L.local.w.w, L.local.beta, gate_, act_at(D, cin).p, ld, st);
+          cam_context(tmp, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate, st);
+          cam_local_conv(tmp, B, T2, L.dil, L.local.w.w, L.local.beta, gate, act_at(D, cin).p, ld, st);
         }
       } else {
-        cam_context(tmp_, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate_, st);
-        ConvGemmArgs q = cam_conv1d(Tens{tmp_, bf}, B, T2, 128, L.local, 1, L.dil, L.dil, act_at(D, cin), ld);
-        q.gate = gate_; q.gate_seg = 100; q.gate_nseg = (T2 + 99) / 100;
+        cam_context(tmp, bf, B, T2, 128, 128, 100, L.c1w, L.c1b, L.c1, L.c2w, L.c2b, L.c2, gate, st);
+        ConvGemmArgs q = cam_conv1d(Tens{tmp, bf}, B, T2, 128, L.local, 1, L.dil, L.dil, act_at(D, cin), ld);
+        q.gate = gate; q.gate_seg = 100; q.gate_nseg = (T2 + 99) / 100;
         conv_gemm(q, bf, st);
       }
       cin += L.local.w.N;
     }
     SD_CHECK(cin == ld, kErrShape, "dense block width");
-    const Tens dst{b < 2 ? d_[b + 1] : x4_, bf};
+    const Tens dst{b < 2 ? dd[b + 1] : x4, bf};
     const int ldo = b < 2 ? ctot[b + 1] : kChannels;
     conv_gemm(cam_conv1d(D, B, T2, ld, transit_[b], 1, 0, 1, dst, ldo), bf, st);
     cin = transit_[b].w.N;
   }
-  return Tens{x4_, bf};
+  return Tens{x4, bf};
 }
 
 // ------------------------------------------------------------------------------ CamppModel

@@ -36,7 +36,9 @@ class CamTrunk {
   void alloc(DeviceArena& arena, int max_batch, int max_frames);
   static int out_frames(int Tf) { return (Tf - 1) / 2 + 1; }
   // fbank (B, Tf, 80) fp32 -> transit3 output (B, out_frames(Tf), 512), before out_nonlinear.
-  Tens forward(const float* fbank, int B, int Tf, hipStream_t st) const;
+  // b0: the call covers windows [b0, b0 + B) of a batch (fbank = the batch's base; the result is the
+  // batch's output map with this slice filled in), so disjoint slices may run on different streams.
+  Tens forward(const float* fbank, int B, int Tf, hipStream_t st, int b0 = 0) const;
   // Folded out_nonlinear BatchNorm (the ReLU follows it).
   const float* out_s() const { return out_s_; }
   const float* out_h() const { return out_h_; }

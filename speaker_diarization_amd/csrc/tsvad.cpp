@@ -103,7 +103,11 @@ void TsvadModel::alloc_workspace() {
   lstm_work_ = ws(lstm_work_floats((int)Bm, cfg_.lstm_hidden, 2));
 }
 
-TsvadModel::~TsvadModel() = default;
+TsvadModel::~TsvadModel() {
+  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+  if (ev_join_) (void)hipEventDestroy(ev_join_);
+  if (side_) (void)hipStreamDestroy(side_);
+}
 
 // Direct launches only.  A hipGraph replay of this forward was tried (round 2-3) and dropped: it measured no
 // faster on C2 (34.3 vs 34.4 ms per 10-min step: ~150 launches against a 34-ms GPU span) and its replays did
@@ -117,7 +121,27 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   // an earlier forward's LSTM report nobody collected with sd_tsvad_status
   lstm_err_.raise_if_set();
   const bool bf = cfg_.bf16;
-  const Tens x4 = cam_.forward(ref, B, Tf, st);   // CAM++ up to transit3, (B, T2, 512)
+  // CAM++ up to transit3, (B, T2, 512).  Batches of more than one round of CUs run as two window slices on
+  // two streams (bit-identical per window: every CAM++ kernel computes a window independently of the rest
+  // of the batch).  SDIAR_CAM_ONE_STREAM: one launch sequence over the whole batch.
+  static const bool one_stream = getenv("SDIAR_CAM_ONE_STREAM") != nullptr;
+  Tens x4;
+  if (!one_stream && B >= 384) {
+    if (!side_) {
+      SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+      SD_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+      SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    }
+    const int B1 = B / 2;
+    SD_HIP(hipEventRecord(ev_fork_, st));
+    SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+    x4 = cam_.forward(ref, B1, Tf, st, 0);
+    (void)cam_.forward(ref, B - B1, Tf, side_, B1);
+    SD_HIP(hipEventRecord(ev_join_, side_));
+    SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
+  } else {
+    x4 = cam_.forward(ref, B, Tf, st);
+  }
   const int T2 = CamTrunk::out_frames(Tf);
   // ---------------- speech_down_or_up (out_nonlinear BN-ReLU fused as prologue), fp32 out
   const int E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim, NS = cfg_.max_num_speaker;

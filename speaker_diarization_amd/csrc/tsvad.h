@@ -64,6 +64,12 @@ class TsvadModel {
   const void* lstm_hh_bf_ = nullptr;   // bf16 copy of W_hh (bf16 mode)
   ConvL fc_;
 
+  // CAM++ trunk of a large batch as two window slices, the second on side_ (fork / join events on the
+  // caller's stream): the per-layer launches of one slice fill the CUs the other slice's last round of
+  // workgroups leaves idle (cam_dense: 600 items on 256 CUs = 2.34 rounds of 3).
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+
   // Workspace.
   float *mix_ = nullptr, *mixg_ = nullptr;
   float *X_ = nullptr, *Y_ = nullptr, *QKV_ = nullptr, *AO_ = nullptr, *H_ = nullptr;

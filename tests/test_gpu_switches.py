@@ -139,3 +139,41 @@ def test_switch_is_bit_identical(gpu, switch):
         assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
         hashes.append(line[0])
     assert hashes[0] == hashes[1], hashes
+
+
+TSVAD_BITS_CHILD = r"""
+import hashlib, os, sys
+import numpy as np, torch
+sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests", "golden"))
+from make_golden import tsvad_inputs
+from speaker_diarization_amd.ts_vad.model import TSVADModel
+from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
+dev = torch.device("cuda", 0)
+h = hashlib.sha256()
+for v in (1, 0):
+    cfg = TSVADConfig(rs_len=4) if v == 0 else TSVADConfig.ots_vad_v1(rs_len=4)
+    B = 400
+    m = TSVADModel(cfg, device=dev, precision="bf16", max_batch=B)
+    m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=11)))
+    x, ts = tsvad_inputs(B, 398, 100, seed=5)
+    out = m.forward(torch.from_numpy(x).to(dev), torch.from_numpy(ts).to(dev), 100)
+    h.update(out.float().cpu().numpy().tobytes())
+print("HASH " + h.hexdigest())
+"""
+
+
+def test_cam_two_stream_slices_bit_identical(gpu):
+    """TS-VAD batches of >= 384 windows run the CAM++ trunk as two window slices on two streams
+    (tsvad.cpp); the logits must be bit-identical to one launch sequence over the whole batch."""
+    hashes = []
+    for one in (False, True):
+        env = dict(os.environ)
+        env.pop("SDIAR_CAM_ONE_STREAM", None)
+        if one:
+            env["SDIAR_CAM_ONE_STREAM"] = "1"
+        r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
+                           text=True, timeout=110, env=env)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
+        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
+        hashes.append(line[0])
+    assert hashes[0] == hashes[1], hashes
