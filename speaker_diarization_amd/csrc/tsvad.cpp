@@ -123,8 +123,12 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   const bool bf = cfg_.bf16;
   // CAM++ up to transit3, (B, T2, 512).  Batches of more than one round of CUs run as two window slices on
   // two streams (bit-identical per window: every CAM++ kernel computes a window independently of the rest
-  // of the batch).  SDIAR_CAM_ONE_STREAM: one launch sequence over the whole batch.
-  static const bool one_stream = getenv("SDIAR_CAM_ONE_STREAM") != nullptr;
+  // of the batch); so does the fused conformer stack below.  SDIAR_CAM_ONE_STREAM: one launch sequence over
+  // the whole batch.
+  // Under the libsdiar kernel timer (bench.py's extra profiled step) the forward stays on one stream, so
+  // each kernel's HIP-event time is its own and not shared with the other slice's kernels.
+  static const bool one_stream_env = getenv("SDIAR_CAM_ONE_STREAM") != nullptr;
+  const bool one_stream = one_stream_env || prof_enabled();
   Tens x4;
   if (!one_stream && B >= 384) {
     if (!side_) {
@@ -178,10 +182,35 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
     if (SE == 192 && E == 2 * SE && conformer_stack_fused(conf_, E, bf)) {
       // the row programs build [ts | mix] on load and write the bf16 speakers-to-channels rows directly
-      SpeakerStreams io;
-      io.ts = ts; io.mix = mixg_; io.ldmix = SE; io.Tmix = T3; io.NS = NS; io.out = X2_;
-      run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st,
-                          &io);
+      // windows [b0, b0 + Bh): every buffer of the fused stack is addressed from the slice's first row
+      // (bf16 y / qkv / ao / h, fp32 X, per-sequence GroupNorm partials, the speaker streams)
+      auto run_slice = [&](int b0, int Bh, hipStream_t s) {
+        const int64_t s0 = (int64_t)b0 * NS, r0 = s0 * Tl;
+        auto at = [](float* p, int64_t bytes) { return reinterpret_cast<float*>(reinterpret_cast<char*>(p) + bytes); };
+        EncoderWork w = enc_work();
+        w.Y = at(Y_, r0 * E * 2);
+        w.QKV = at(QKV_, r0 * 3 * E * 2);
+        w.AO = at(AO_, r0 * E * 2);
+        w.H = at(H_, r0 * 2 * E * 2);
+        w.partial = partial_ + s0 * ((E + 63) / 64) * 2;
+        SpeakerStreams io;
+        io.ts = ts + s0 * SE; io.mix = mixg_ + (int64_t)b0 * T3 * SE; io.ldmix = SE; io.Tmix = T3; io.NS = NS;
+        io.out = at(X2_, (int64_t)b0 * Tl * NS * E * 2);
+        run_conformer_stack(conf_, X_ + r0 * E, Bh * NS, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr,
+                            w, s, &io);
+      };
+      // like the CAM++ trunk above: two window slices on two streams fill each other's idle CUs
+      if (!one_stream && B >= 384) {
+        const int B1 = B / 2;
+        SD_HIP(hipEventRecord(ev_fork_, st));
+        SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+        run_slice(0, B1, st);
+        run_slice(B1, B - B1, side_);
+        SD_HIP(hipEventRecord(ev_join_, side_));
+        SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
+      } else {
+        run_slice(0, B, st);
+      }
     } else {
       build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
       run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);

@@ -12,6 +12,9 @@ MFMA_PMC=${MFMA_PMC:-"SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_B
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 BENCH="bench.py --workload $WL --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-c4-ref"
+# per-kernel evidence on ONE stream (the TS-VAD forward otherwise runs the CAM++ trunk and the conformer stack
+# as two concurrent window slices, whose kernels share the GPU): matches bench.py's single-stream profiled step
+export SDIAR_CAM_ONE_STREAM=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.log" 2>&1
 echo "trace ok"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.log" 2>&1
