@@ -14,7 +14,8 @@ for WL in "$@"; do
   else
     timeout -k 10 240 python3 $BENCH > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
   fi
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$WL" -o run -- python3 $BENCH \
+  # kernel stats on one stream (see tools/profile_c2.sh)
+  SDIAR_CAM_ONE_STREAM=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$WL" -o run -- python3 $BENCH \
     > "$OUT/trace_$WL.log" 2>&1
   cp "$(find "$OUT/trace_$WL" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats_$WL.csv"
   rm -rf "$OUT/trace_$WL"   # the full traces exceed what gpurun copies back
