@@ -30,10 +30,10 @@ CATEGORIES = {
     "gemm_areg": r"gemm_areg_kernel",
     "gemm_dma": r"gemm_dma_kernel",
     "gemm_bf16_reg": r"gemm_bf16_kernel",
-    "fcm_conv3x3_band": r"fcm_conv3x3_kernel|fcm_conv3x3_band_kernel<(4, 1|2, 2), false",
+    "fcm_conv3x3_band": r"fcm_conv3x3_kernel|fcm_conv3x3_band_kernel<(4, 1|2, 2|10, 2), false|fcm_conv3x3_ring_kernel",
     "attention_bf16": r"attn_\w*kernel|attention\w*kernel",
     "lstm_recurrence": r"lstm\w*kernel",
-    "dwconv": r"glu_dwconv_kernel",
+    "dwconv": r"glu_dwconv_kernel|dwconv_pk_kernel",
     "groupnorm_silu": r"groupnorm\w*kernel",
     "cam_context": r"cam_context\w*kernel",
     "cam_dense": r"cam_dense_kernel",
