@@ -243,6 +243,9 @@ struct RowProgArgs {
   // -> (b, t) columns spk*384 .. (speakers_to_channels); with Xo == nullptr the fp32 rows are not written
   void* yt = nullptr;
   int yt_NS = 0;
+  // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog(); SDIAR_RP_STAGGER overrides):
+  // half the CUs run their epilogue store burst while the other half streams MFMAs
+  int stagger = 0;
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

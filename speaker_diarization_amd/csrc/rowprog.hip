@@ -175,6 +175,10 @@ void rowprog_kernel(RowProgArgs a) {
   constexpr bool do_mfma = !(PROBE & 1), do_lds = !(PROBE & 4);
   const bool has_pre = PROG >= 0 ? (PROG & 1) != 0 : a.w0 != nullptr;
   const int nffn = PROG >= 0 ? (PROG >> 1) : a.n_ffn;
+  // odd workgroups start late, so their epilogue store bursts fall into the even ones' MFMA streaming
+  // (delaying only the workgroups with a tile fewer, which have a tile of slack, measured no gain)
+  if (blockIdx.x & 1)
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(64);
 
   // parameters -> LDS (before the first DMA, so the compiler's waits for these loads do not drain the ring)
   auto cp = [&](int off, const float* p, int n) {
@@ -575,12 +579,17 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   ProfScope prof(name, flops, bytes, st);
   const dim3 g3(grid);
   {
+    // A/B (C2, 3 rounds on one box): rowprog_pw2_ffn 5.95 -> 5.76 ms per step at 20 (12: 5.83); the short
+    // programs (out_proj: one 12-piece GEMM per tile) only lose the offset, so they start together
+    static const int stagger = getenv("SDIAR_RP_STAGGER") ? atoi(getenv("SDIAR_RP_STAGGER")) : 20;
+    RowProgArgs b = a;
     const int prog = (a.w0 ? 1 : 0) | (a.n_ffn << 1);
-    if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, a);
-    else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, a);
-    else if (prog == 3) hipLaunchKernelGGL((rowprog_kernel<1, 0, 3>), g3, dim3(512), kSmemBytes, st, a);
-    else if (prog == 5) hipLaunchKernelGGL((rowprog_kernel<1, 0, 5>), g3, dim3(512), kSmemBytes, st, a);
-    else hipLaunchKernelGGL((rowprog_kernel<1, 0>), g3, dim3(512), kSmemBytes, st, a);
+    b.stagger = prog == 5 && stagger > 0 && stagger < 256 && ntiles > grid ? stagger : 0;
+    if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, b);
+    else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, b);
+    else if (prog == 3) hipLaunchKernelGGL((rowprog_kernel<1, 0, 3>), g3, dim3(512), kSmemBytes, st, b);
+    else if (prog == 5) hipLaunchKernelGGL((rowprog_kernel<1, 0, 5>), g3, dim3(512), kSmemBytes, st, b);
+    else hipLaunchKernelGGL((rowprog_kernel<1, 0>), g3, dim3(512), kSmemBytes, st, b);
   }
   SD_LAUNCH_CHECK();
 }

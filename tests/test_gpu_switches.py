@@ -26,7 +26,7 @@ GROUPS = {
                                                "SDIAR_NO_CAM_FUSED": "1", "SDIAR_NO_DWCONV_PK": "1"},
     "fcmband_off+areg_off+ringpersist_off+xremap_off": {
         "SDIAR_NO_FCM_BAND": "1", "SDIAR_NO_AREG_GEMM": "1", "SDIAR_NO_RING_PERSIST": "1",
-        "SDIAR_ATTN_NO_XREMAP": "1"},
+        "SDIAR_ATTN_NO_XREMAP": "1", "SDIAR_RP_STAGGER": "0"},
     "fcmfuse_off+ring_off+stream_off+lstmseq_off": {"SDIAR_NO_FCM_FUSE": "1", "SDIAR_NO_RING_GEMM": "1",
                                                      "SDIAR_NO_STREAM_GEMM": "1", "SDIAR_NO_LSTM_SEQ": "1"},
 }
