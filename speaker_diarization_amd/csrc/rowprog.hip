@@ -579,7 +579,8 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   ProfScope prof(name, flops, bytes, st);
   const dim3 g3(grid);
   {
-    // A/B (C2, 3 rounds on one box): rowprog_pw2_ffn 5.95 -> 5.76 ms per step at 20 (12: 5.83); the short
+    // A/B (C2, 4 rounds on one box): rowprog_pw2_ffn 6.06 -> 5.85 ms per step at 20 (12 less, 32 / 48 no
+    // better; the step time is unchanged within noise); the short
     // programs (out_proj: one 12-piece GEMM per tile) only lose the offset, so they start together
     static const int stagger = getenv("SDIAR_RP_STAGGER") ? atoi(getenv("SDIAR_RP_STAGGER")) : 20;
     RowProgArgs b = a;
