@@ -12,8 +12,9 @@
 // [pw2 + ffn2 + final LN + next layer's ffn1 + attn-LN].  HBM sees X, the bf16 A rows and y once each;
 // the 512-wide FFN hidden layer, the sub-block outputs and every LN input stay on chip.
 //
-// Layout (transposed MFMA, v_mfma_f32_16x16x32_bf16 with weights as the A operand): a workgroup is 4 waves
-// (one per SIMD, ~350 VGPRs), a wave owns 32 tokens as two 16-token column tiles.  acc[ft][tt] holds
+// Layout (transposed MFMA, v_mfma_f32_16x16x32_bf16 with weights as the A operand): a workgroup is 8 waves
+// (two per SIMD, <= 256 VGPRs each), a wave owns 16 tokens as one 16-token column tile (TT = 1; the
+// template keeps TT for the 2-tile layout, which measured slower at one wave per SIMD).  acc[ft][tt] holds
 // features 16 ft + 4 g + r (g = lane / 16) of token 16 tt + lane % 16, i.e. a token's 384 features over the
 // 4 lanes that share lane % 16 (LN statistics = 2 shuffles).  The B operand of the next GEMM is built from
 // that layout without any data movement: k-step kk of a lane holds features 32 kk + 4 g + {0..3} (tile 2kk)
@@ -25,7 +26,7 @@
 // ds_read_b128 is conflict-free) through a 5-slot LDS ring (global_load_lds, 4 pieces in flight, counted
 // vmcnt waits, one barrier per piece).  The workgroups are persistent over tiles; the ring runs across tile
 // boundaries, so the next tile's first weights are in flight during the current tile's epilogue.
-// MFMA accumulators in the VGPR form: with the default AGPR form the 2-tile variant spills to scratch
+// MFMA accumulators in the VGPR form (the 2-tile layout spilled to scratch with the default AGPR form)
 // sdiar-build: -mllvm -amdgpu-mfma-vgpr-form=1
 #include <cstring>
 #include <vector>
