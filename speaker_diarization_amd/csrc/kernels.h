@@ -243,7 +243,7 @@ struct RowProgArgs {
   // -> (b, t) columns spk*384 .. (speakers_to_channels); with Xo == nullptr the fp32 rows are not written
   void* yt = nullptr;
   int yt_NS = 0;
-  // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog(); SDIAR_RP_STAGGER overrides):
+  // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog(); SDIAR_RP_STAGGER scales it):
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
 };

@@ -580,13 +580,17 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   ProfScope prof(name, flops, bytes, st);
   const dim3 g3(grid);
   {
-    // A/B (C2, 4 rounds on one box): rowprog_pw2_ffn 6.06 -> 5.85 ms per step at 20 (12 less, 32 / 48 no
-    // better; the step time is unchanged within noise); the short
-    // programs (out_proj: one 12-piece GEMM per tile) only lose the offset, so they start together
-    static const int stagger = getenv("SDIAR_RP_STAGGER") ? atoi(getenv("SDIAR_RP_STAGGER")) : 20;
-    RowProgArgs b = a;
+    // Start offset of the odd workgroups per program, in s_sleep(64) units, scaled by SDIAR_RP_STAGGER (percent,
+    // default 100; 0 = all workgroups start together).  A/B on one box (C2, 3-4 rounds each, every round the
+    // same way): pw2+FFN (prog 5, 76 pieces per tile) 6.06 -> 5.85 ms per step at 20 (12 less, 32 / 48 no
+    // better); out_proj (prog 1, 12 pieces, HBM-bound) 2.53 -> 2.42 at 8 (4: 2.45; 16: 2.53); the one-launch
+    // FFN programs (2, 3) get offsets in proportion to their tile length.
+    static const int scale = getenv("SDIAR_RP_STAGGER") ? atoi(getenv("SDIAR_RP_STAGGER")) : 100;
     const int prog = (a.w0 ? 1 : 0) | (a.n_ffn << 1);
-    b.stagger = prog == 5 && stagger > 0 && stagger < 256 && ntiles > grid ? stagger : 0;
+    RowProgArgs b = a;
+    const int base = prog == 5 ? 20 : prog == 3 ? 12 : 8;
+    const int sv = (base * scale + 50) / 100;
+    b.stagger = sv > 0 && sv < 256 && ntiles > grid ? sv : 0;
     if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, b);
     else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, b);
     else if (prog == 3) hipLaunchKernelGGL((rowprog_kernel<1, 0, 3>), g3, dim3(512), kSmemBytes, st, b);
