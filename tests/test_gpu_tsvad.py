@@ -10,9 +10,10 @@ from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_to
 pytestmark = pytest.mark.gpu
 
 # fp32: exact-f32 MFMA, the north_star bound.  bf16: bf16 operands / fp32
-# accumulate through ~70 layers; bound on the logits measured on the goldens.
+# accumulate through ~70 layers; bound on the logits measured on the goldens (MI355X, round 3:
+# 6.4e-3 v1 rs6, 7.0-7.4e-3 v0 rs4, 7.8e-3 for the B = 40 batch; the kernels are deterministic).
 FP32_ATOL = 1e-3
-BF16_ATOL = 2e-2
+BF16_ATOL = 1.5e-2
 
 
 def _cfg(v, rs):
