@@ -203,13 +203,46 @@ def live_kernels(step):
     return kernels
 
 
+def lstm_handoff_floor_us(steps=4000):
+    """Measured exchange floor of the persistent LSTM recurrence: sd_probe_lstm_handoff runs the
+    recurrence's own 4-workgroup hand-off protocol (poll, h-fragment loads, publish) with no gate
+    arithmetic; us per step (median of 3 launches)."""
+    import ctypes
+    import torch
+    from speaker_diarization_amd import _lib
+    v = ctypes.c_float()
+    runs = []
+    for _ in range(3):
+        _lib.call("sd_probe_lstm_handoff", steps, ctypes.byref(v), _lib.stream_ptr())
+        runs.append(v.value)
+    torch.cuda.synchronize()
+    return float(np.median(runs))
+
+
+def latency_roofline_of(name, st, floor_us):
+    """Latency-model roofline of a sequential kernel: `achieved` = its time per dependent
+    step (live HIP-event time / steps it counted), `peak` = the measured per-step floor of the mechanism
+    the steps wait on; frac = peak / achieved (1.0 = at the floor)."""
+    us = st["ms"] * 1000.0 / st["steps"]
+    r = roofline_of(name, st)
+    return dict(bound="latency", achieved=round(us, 4), peak=round(floor_us, 4), unit="us/step",
+                frac=round(floor_us / us, 4), traffic=None, kernel=name, launches=st["launches"],
+                steps_per_launch=round(st["steps"] / st["launches"], 1), avg_launch_ms=round(st["ms"] / st["launches"], 4),
+                floor="sd_probe_lstm_handoff: the recurrence's 4-workgroup h exchange alone, us per step",
+                mfma_frac=r["mfma_frac"], hbm_frac=r["hbm_frac"])
+
+
 def kernel_report(kernels, workload, ms_per_step, precision):
     """roofline (dominant single kernel), attention_roofline, whole-step work and a
-    per-kernel table, all from the live timer."""
+    per-kernel table, all from the live timer.  A dominant kernel that counts sequential steps (the
+    LSTM recurrence of C1 / C3) gets the latency model instead of a flop / byte roof."""
     if not kernels:
         return {}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
-    out = {"roofline": roofline_of(dom, kernels[dom], pmc_traffic(workload, dom))}
+    if kernels[dom].get("steps", 0) > 0 and dom == "lstm_recurrence":
+        out = {"roofline": latency_roofline_of(dom, kernels[dom], lstm_handoff_floor_us())}
+    else:
+        out = {"roofline": roofline_of(dom, kernels[dom], pmc_traffic(workload, dom))}
     att = [k for k in ATTN_KERNELS if k in kernels]
     if att:
         out["attention_roofline"] = roofline_of(att[0], kernels[att[0]], pmc_traffic(workload, att[0]))
@@ -929,8 +962,19 @@ def main_stream(a, wl):
         torch.cuda.synchronize()
         assert out + cnt.value == T, (out, cnt.value, T)
 
-    elapsed, _ = timed(lambda: step(True), a.warmup, a.steps, world, dev)
-    lat[:] = lat[-(len(lat) // (a.warmup + a.steps)) * a.steps:]   # timed steps only
+    def stats():
+        e, d, ne, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+        _lib.call("sd_fseend_stream_stats", s, ctypes.byref(e), ctypes.byref(d), ctypes.byref(ne), ctypes.byref(nd))
+        return e.value, d.value, ne.value, nd.value
+
+    for _ in range(a.warmup):
+        step(False)
+    st0 = stats()
+    elapsed, _ = timed(lambda: step(True), 0, a.steps, world, dev)
+    st1 = stats()
+    lat[:] = lat[-(len(lat) // a.steps) * a.steps:]   # timed steps only
+    latency_model = stream_latency_model(sd_np, st0, st1, len(lat), float(np.percentile(np.array(lat) * 1e6, 50)),
+                                         audio, a.precision) if a.steps else None
     # parity of this very run: against the whole-recording GPU test() on the same features, and against
     # the fp32 CPU oracle (oracle/fseend_ref.py test() on oracle/eend_ref.py features) over the first frames
     Tc = min(T, 2000)
@@ -965,6 +1009,7 @@ def main_stream(a, wl):
                                "p99": round(float(np.percentile(L, 99)), 4),
                                "max": round(float(L.max()), 4), "mean": round(float(L.mean()), 4)},
                 "real_time_factor": round(float(L.mean()) / unit_ms, 5),
+                "roofline": latency_model,
                 "max_abs_diff_vs_test": err, "parity": parity}
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = fseend_cpu_baseline(meeting, sd_np, a.cpu_seconds)
@@ -973,6 +1018,64 @@ def main_stream(a, wl):
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def kernel_boundary_us(n=200, reps=20):
+    """Measured cost of one dependent kernel boundary inside a replayed hipGraph: a captured chain of n
+    trivial dependent kernels (1-element in-place adds), replayed `reps` times; device time per kernel."""
+    import torch
+    x = torch.zeros(1, device="cuda")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            x.add_(1.0)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(n):
+                x.add_(1.0)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / (n * reps)
+
+
+def stream_latency_model(sd_np, st0, st1, pushes, p50_us, audio, precision):
+    """C5 latency roofline (SURVEY §8(d) latency model): a push cannot finish faster than its chain of
+    dependent device operations: (graph nodes run per push + the per-push copies) x the measured kernel
+    boundary, plus the weight bytes those chunk runs stream / HBM peak.  achieved = p50 per push (host
+    wall, incl. the graph launch and the synchronisation); frac = floor / achieved."""
+    enc_runs, dec_runs = st1[0] - st0[0], st1[1] - st0[1]
+    ne, nd = st1[2], st1[3]
+    esz = 2 if precision == "bf16" else 4
+    groups = {}
+    for k, v in sd_np.items():
+        if k.endswith("num_batches_tracked"):
+            continue
+        groups[k.split(".")[0]] = groups.get(k.split(".")[0], 0) + int(np.asarray(v).size)
+    enc_bytes = groups.get("enc", 0) * esz
+    dec_bytes = (groups.get("cnn", 0) + 2 * groups.get("dec", 0)) * esz   # the fusion layer runs twice
+    per_push_nodes = (enc_runs * ne + dec_runs * nd) / max(pushes, 1)
+    per_push_copies = 1.0 + dec_runs / max(pushes, 1)     # the samples' copy, each emitted frame's copy
+    b_us = kernel_boundary_us()
+    bytes_per_push = (enc_runs * enc_bytes + dec_runs * dec_bytes) / max(pushes, 1)
+    floor = (per_push_nodes + per_push_copies) * b_us + bytes_per_push / (HBM_PEAK * 1e9) * 1e6
+    return dict(bound="latency", achieved=round(p50_us, 2), peak=round(floor, 2), unit="us/push",
+                frac=round(floor / p50_us, 4), traffic=None,
+                model={"encoder_runs_per_push": round(enc_runs / max(pushes, 1), 4),
+                       "decoder_runs_per_push": round(dec_runs / max(pushes, 1), 4),
+                       "encoder_graph_nodes": ne, "decoder_graph_nodes": nd,
+                       "device_ops_per_push": round(per_push_nodes + per_push_copies, 2),
+                       "kernel_boundary_us": round(b_us, 3),
+                       "weight_bytes_per_push": int(bytes_per_push),
+                       "input": "audio" if audio else "feature rows",
+                       "floor": "(graph nodes + copies per push) x measured dependent-kernel boundary "
+                                "(replayed hipGraph of trivial kernels) + weight bytes per push / 8 TB/s"})
 
 
 def fseend_oracle_parity(meeting, sd_np, gpu_scores, frames=1000):

@@ -38,6 +38,12 @@ void sd_prof_enable(int on);
 void sd_prof_reset(void);
 int sd_prof_query(int i, char* name, int name_len, int64_t* launches, double* flops, double* bytes,
                   double* ms);
+/* Sequential steps family i accumulated (latency-bound kernels: the LSTM recurrence counts its time steps). */
+double sd_prof_query_steps(int i);
+/* The persistent LSTM's exchange floor: one launch of the recurrence's 4-workgroup h hand-off protocol with
+ * no gate arithmetic (same publish / poll / payload loads as lstm_group_bf16_kernel, batch 16) over `steps`
+ * steps, timed with HIP events on `stream`; *us_per_step = its time / steps. */
+int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream);
 
 /* ------------------------------------------------------------------ TS-VAD
  * Replaces TSVADModel (egs/alimeeting/ts_vad2/model.py:179-1142):
@@ -79,6 +85,11 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_s
  * calls it after forward(), so the failing forward itself raises (RuntimeError); an
  * uncollected report is raised by the handle's next forward at the latest. */
 int sd_tsvad_status(sd_tsvad* h, void* stream);
+/* Windows per reference forward call (the collater's batch, e.g. infer.py's batch of 64) when one device
+ * forward covers several of them: the scope of BatchNorm1D's NaN bypass (ts_vad2/model.py:161-171) — a window
+ * with a non-finite input makes the reference skip speech_down_or_up's (and, variant 0, backend_down's)
+ * BatchNorm for every window of ITS batch.  0 (default): the whole sd_tsvad_forward call is one batch. */
+int sd_tsvad_set_forward_batch(sd_tsvad* h, int windows);
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 int sd_tsvad_destroy(sd_tsvad* h);
 
@@ -302,8 +313,14 @@ int sd_fseend_stream_set_audio(sd_fseend_stream* s, const float* mel_fb, int n_m
 int sd_fseend_stream_push_audio(sd_fseend_stream* s, const float* samples, int64_t n, float* preds, int cap,
                                 int* n_out, void* stream);
 int sd_fseend_stream_flush(sd_fseend_stream* s, float* preds, int cap, int* n_out, void* stream);
+/* reset: enqueues the cursor reset on `stream` and waits for it (and every chunk enqueued before it), so a
+ * following set_audio() on any stream sees no chunk of the previous utterance still in flight. */
 int sd_fseend_stream_reset(sd_fseend_stream* s, void* stream);
 int64_t sd_fseend_stream_device_bytes(const sd_fseend_stream* s);
+/* Counters for the latency model of bench.py's C5 line: encoder / decoder chunks run since creation and the
+ * node count of each captured chunk graph (0 before the capture). */
+int sd_fseend_stream_stats(const sd_fseend_stream* s, int64_t* enc_runs, int64_t* dec_runs, int* enc_nodes,
+                           int* dec_nodes);
 int sd_fseend_stream_destroy(sd_fseend_stream* s);
 
 /* feature.stft + feature.transform('logmel23_mn' | 'logmel23') + feature.splice + [::subsampling]
@@ -382,6 +399,20 @@ int sd_op_linear(const float* x, int M, int K, const float* w, const float* b, i
 int sd_op_gemm_bf16(const void* x, int M, int K, int lda, int a_coff, const float* w, int N,
                     const float* pre_scale, const float* pre_shift, const float* alpha, const float* beta,
                     int act, void* out, int ldo, void* stream);
+/* One CAM++ dense layer, bf16 (CAMDenseTDNNLayer + CAMLayer, egs/alimeeting/ts_vad2/cam_pplus_wespeaker.py:
+ * 79-168) as the TS-VAD / embedding trunk runs it (cam_dense.hip): x bf16 bits (B, T, ld), input channels
+ * [0, cin); out: bf16 bits at x's channels [cin, cin + 32) (out may alias x + cin).  s1/h1: nonlinear1
+ * folded [cin]; wb: linear1 weight fp32 (128, cin); a2/b2: nonlinear2 folded [128]; wl: linear_local weight
+ * fp32 (32, 128, 3); bl: its bias [32] or NULL; w1/c1: cam_layer.linear1 (64, 128)/(64); w2/c2:
+ * cam_layer.linear2 (32, 64)/(32).  T <= 320, dil 1 or 2, cin % 32 == 0, cin <= 992.  repeats: run the
+ * launch that many times on the same exchange records / counters (each must give the same bits). */
+int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
+                    const float* wb, const float* a2, const float* b2, const float* wl, const float* bl,
+                    const float* w1, const float* c1, const float* w2, const float* c2, void* out, int repeats,
+                    void* stream);
+/* Diagnostics: while `stamps` (device, >= 16 u64 per workgroup of a launch) is non-NULL, every cam_dense
+ * launch records its workgroups' phase-boundary s_memrealtime stamps there (tools/cam_dense_probe.py). */
+int sd_debug_cam_dense_probe(void* stamps);
 /* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);

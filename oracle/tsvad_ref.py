@@ -22,6 +22,12 @@ def _bn(x, sd, p, eps=1e-5):
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], w, b, False, 0.0, eps)
 
 
+def _bn1d_nan_bypass(x, sd, p):
+    """BatchNorm1D (model.py:161-171): the wrapped eval BatchNorm1d runs only when the WHOLE input tensor
+    (the forward's batch) holds no NaN; otherwise the input passes through unchanged for every window."""
+    return _bn(x, sd, p) if int(torch.isnan(x).sum()) == 0 else x
+
+
 # ----------------------------------------------------------------------------- CAM++
 def fcm(sd, x, pre="speech_encoder.head."):
     """FCM.forward (cam_pplus_wespeaker.py:299-308). x: (B, F, T) -> (B, 320, T)."""
@@ -224,7 +230,7 @@ def speech_encoder_out(sd, ref_speech):
     """CAM++ time output + speech_down_or_up (model.py:844-848 / 683-687) -> (B, 192, T')."""
     x = campplus_time_out(sd, ref_speech)
     x = F.conv1d(x, sd["speech_down_or_up.0.weight"], sd["speech_down_or_up.0.bias"], stride=2, padding=2)
-    return F.relu(_bn(x, sd, "speech_down_or_up.1.bn"))
+    return F.relu(_bn1d_nan_bypass(x, sd, "speech_down_or_up.1.bn"))
 
 
 @torch.no_grad()
@@ -270,8 +276,8 @@ def tsvad_forward(sd, cfg, ref_speech, target_speech, max_len):
             cat = transformer_layer(cat, sd, f"single_backend.layers.{l}.", nh)
         outs.append(cat.transpose(0, 1))
     cat = torch.stack(outs).permute(1, 0, 3, 2).reshape(B, -1, T)
-    cat = F.relu(_bn(F.conv1d(cat, sd["backend_down.0.weight"], sd["backend_down.0.bias"], padding=2), sd,
-                     "backend_down.1.bn"))
+    cat = F.relu(_bn1d_nan_bypass(F.conv1d(cat, sd["backend_down.0.weight"], sd["backend_down.0.bias"], padding=2),
+                                  sd, "backend_down.1.bn"))
     cat = positional_encoding(cat.permute(2, 0, 1), sd)
     for l in range(cfg.num_transformer_layer):
         cat = transformer_layer(cat, sd, f"multi_backend.layers.{l}.", nh)

@@ -113,11 +113,14 @@ _SIGS = {
     "sd_prof_reset": (None, []),
     "sd_prof_query": (c_int, [c_int, c_char_p, c_int, POINTER(c_int64), POINTER(ctypes.c_double),
                               POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
+    "sd_prof_query_steps": (ctypes.c_double, [c_int]),
+    "sd_probe_lstm_handoff": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_tsvad_create": (c_int, [POINTER(TsvadConfig), POINTER(c_void_p)]),
     "sd_tsvad_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
     "sd_tsvad_finalize": (c_int, [c_void_p]),
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_status": (c_int, [c_void_p, c_void_p]),
+    "sd_tsvad_set_forward_batch": (c_int, [c_void_p, c_int]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
     "sd_tsvad_stream_create": (c_int, [POINTER(TsvadStreamConfig), POINTER(c_void_p)]),
@@ -164,6 +167,7 @@ _SIGS = {
     "sd_fseend_stream_flush": (c_int, [c_void_p, c_void_p, c_int, POINTER(c_int), c_void_p]),
     "sd_fseend_stream_reset": (c_int, [c_void_p, c_void_p]),
     "sd_fseend_stream_device_bytes": (c_int64, [c_void_p]),
+    "sd_fseend_stream_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int), POINTER(c_int)]),
     "sd_fseend_stream_destroy": (c_int, [c_void_p]),
     "sd_eend_features": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p, c_int, c_void_p]),
@@ -181,6 +185,10 @@ _SIGS = {
     "sd_op_linear": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_gemm_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "sd_debug_cam_dense_probe": (c_int, [c_void_p]),
+    "sd_op_cam_dense": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_int, c_void_p]),
     "sd_op_conv1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_void_p, c_int, c_void_p]),
     "sd_op_conv2d": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
@@ -213,7 +221,12 @@ def load():
             f"libsdiar.so not found at {LIB_PATH}; build it with "
             "`python -m speaker_diarization_amd.build` (HIP extension is required)")
     lib = ctypes.CDLL(LIB_PATH)
+    # SDIAR_LIB (A/B runs against an older build) may lack entry points added since; the in-tree build
+    # must export every one of them
+    ab = os.environ.get("SDIAR_LIB") is not None
     for name, (res, args) in _SIGS.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -284,7 +297,8 @@ def prof_stats():
         l, f, b, ms = c_int64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         if not lib.sd_prof_query(i, buf, 128, ctypes.byref(l), ctypes.byref(f), ctypes.byref(b), ctypes.byref(ms)):
             break
-        out[buf.value.decode()] = dict(launches=l.value, flops=f.value, bytes=b.value, ms=ms.value)
+        steps = lib.sd_prof_query_steps(i) if hasattr(lib, "sd_prof_query_steps") else 0.0
+        out[buf.value.decode()] = dict(launches=l.value, flops=f.value, bytes=b.value, ms=ms.value, steps=steps)
         i += 1
     return out
 

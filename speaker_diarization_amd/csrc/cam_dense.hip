@@ -1,32 +1,37 @@
 // One CAM++ dense layer (CAMDenseTDNNLayer, egs/alimeeting/ts_vad2/cam_pplus_wespeaker.py:127-168 with
-// CAMLayer :79-123) per item in ONE launch, bf16, for items of up to kMaxT frames (C2 / C4 windows,
-// the 6-s enrollment chunks):
+// CAMLayer :79-123) in ONE launch, bf16, for items of up to kMaxT frames (C2 / C4 windows, the 6-s
+// enrollment chunks):
 //
 //   h[t, n]   = relu(a2[n] * sum_k W[n][k] relu(s1[k] x[t, k] + h1[k]) + b2[n])   bottleneck (1x1, 128)
 //   ctx[s, n] = mean_t h[t, n] + mean_{t in segment s} h[t, n]                    (seg_len 100, ceil)
 //   gate[s]   = sigmoid(W2 relu(W1 ctx[s] + c1) + c2)
 //   out[t, o] = (sum_{tap, n} Wl[o][tap][n] h[t + (tap - 1) dil, n] + bl[o]) * gate[t / 100, o]
 //
-// written into the dense block's channel slice [cin, cin + 32).  The unfused path ran the bottleneck as
-// a ring GEMM into a (B, T, 128) HBM buffer that the context kernel and the local conv then read back
-// (three launches, 128 channels written and read twice per frame); here the workgroup of an item keeps
-// h in LDS, so HBM sees the item's input rows once and the 32 new channels.
+// written into the dense block's channel slice [cin, cin + 32).  h never touches HBM.
 //
-// Workgroup = one item, 8 waves, one workgroup per CU (121 KiB LDS).
-// Phase 1 (HBM-bound): per 32-deep k-step the item's input rows (one 1-KiB MFMA B-operand fragment per
-// 16-frame tile) and the bottleneck weights (8 fragments, L2-resident, shared by every item) stream
-// HBM/L2 -> LDS by LDS-DMA, lane-linear (conflict-free ds_read_b128), through a 4-slot ring with three
-// k-steps (81 KiB) in flight; the fragments of k-step s + 1 are read from LDS while the MFMAs of k-step s
-// run; BN-ReLU is applied on the way from LDS to the MFMA.  Transposed MFMA (weights as the A operand): a
-// lane ends with 4 consecutive bottleneck channels of one frame -> BN2 + ReLU -> 8-B bf16 stores into the
-// LDS image of h (rows XOR-swizzled by 16-B chunk, zero halo rows for the conv), which takes over the
-// ring's LDS.  The layer weights of phases 2-3 are requested at the end of the GEMM and stay in flight
-// through the epilogue (plain barriers, see below).
-// Phase 2: per-segment channel sums of h (16-B LDS reads, wave shuffles), the k-3 local conv on MFMA from
-// the h image (independent of the gate, so it runs here), then the context and the gate MLP with one
-// output per 8 / 16 lanes.  Phase 3: (conv + bias) x gate, 8-B stores of the new channels.
-// Measured per item (C2, T = 299, s_memrealtime probes): GEMM 13 us (cin 128) .. 40 us (cin 896), epilogue
-// 2.6 us, phase 2 5.8 us, phase 3 0.9 us.
+// Round 4: TWO workgroups per CU.  A workgroup (4 waves, 80 KiB of LDS) owns one PART of an item: items
+// of more than 10 frame tiles (T > 160: the 299-frame TS-VAD windows) are cut into two parts of <= 10
+// tiles, so 600 windows make 1200 workgroups over 512 slots, and while one workgroup of a CU runs its
+// fixed per-part phases (epilogue, channel sums, conv, gate) the other keeps the CU's HBM stream busy
+// (round 3 ran one 121-KiB workgroup per item and per CU: HBM idle through ~9 us of those phases per
+// item, 600 items = 3 rounds over 256 CUs).
+//
+// Phase 1 (HBM-bound): per 32-deep k-step the part's input rows (one 1-KiB MFMA B-operand fragment per
+// 16-frame tile) and the bottleneck weights (8 fragments, L2-resident) stream HBM/L2 -> LDS by LDS-DMA,
+// lane-linear (conflict-free ds_read_b128), through a 4-slot ring with three k-steps in flight; BN-ReLU
+// on the way from LDS to the transposed MFMA (weights as the A operand), whose lane ends with 4
+// consecutive bottleneck channels of one frame -> BN2 + ReLU -> the part's bf16 h image in LDS (16-B
+// chunks XOR-swizzled by row, zero halo rows), which takes over the ring's LDS.
+// Phase 2: per-segment channel sums of the part's h, the k-3 local conv on MFMA from the h image.
+// Parts exchange what the layer couples across them through a per-item record (write-through `sc1`
+// stores, an agent-scope arrival counter; MI355X_MICROARCH.md hand-off table, row 1): their segment sums
+// and the kMaxDil h rows next to the cut.  The LAST part to arrive (told by the value its add returned)
+// finishes the item: context -> gate MLP -> the conv's missing cross-cut taps for the <= 2 kMaxDil frames
+// next to the cut -> (conv + bias) x gate for its own frames and for the first part's, whose pre-gate
+// conv (fp32) that part published after arriving.  The first part never waits; the last part waits only
+// for a part that has already arrived (and so is running), so no placement or dispatch order is assumed.
+// Every value is computed from the same operands in the same order whichever part arrives last, so the
+// output is deterministic (and independent of the batch: items never interact).
 #include <algorithm>
 #include <type_traits>
 
@@ -40,26 +45,40 @@ namespace {
 constexpr int kC = 128, kC1 = 64, kC2 = 32;   // bn_channels, reduction 2, growth rate
 constexpr int kSeg = 100;
 constexpr int kMaxDil = 2;
-constexpr int kMaxT = 320;                    // frames per item held in LDS
+constexpr int kPartTT = 10;                   // 16-frame tiles per workgroup
+constexpr int kPartT = 16 * kPartTT;
+constexpr int kMaxT = 2 * kPartT;             // frames per item (two parts)
 constexpr int kMaxSegs = (kMaxT + kSeg - 1) / kSeg;
-constexpr int kHR = kMaxT + 2 * kMaxDil;      // h image rows (halo rows at both ends)
-constexpr int kMaxCin = 1024;
-constexpr int kWaves = 8, kThreads = 64 * kWaves;
+constexpr int kHR = kPartT + 2 * kMaxDil;     // h image rows of a part (halo rows at both ends)
+constexpr int kMaxCin = 992;                  // widest dense-layer input (512 + 15 x 32, 256 + 23 x 32)
+constexpr int kWaves = 4, kThreads = 64 * kWaves;
 constexpr int kFrag = 512;                    // bf16 per MFMA fragment (1 KiB)
-constexpr int kMaxTT = kMaxT / 16;            // 16-frame tiles
-// ring slot of one k-step: 8 weight fragments (out tiles of 16 channels) then kMaxTT input fragments
-constexpr int kSlot = (8 + kMaxTT) * kFrag;
+// ring slot of one k-step: 8 weight fragments (out tiles of 16 channels) then kPartTT input fragments
+constexpr int kSlot = (8 + kPartTT) * kFrag;
 constexpr int kNSlot = 4;
-constexpr int kDmaPerWave = 4;
-                // per k-step: the wave's weight fragment + its 3 frame tiles
+constexpr int kDmaPerWave = 5;                // per k-step: the wave's 2 weight fragments + its 3 frame tiles
 constexpr int kRingBytes = kNSlot * kSlot * 2;
 constexpr int kHBytes = kHR * kC * 2;         // h image (after the GEMM, in the ring's LDS)
-// phase-2 scratch after the h image: per wave x segment channel sums, then ctx / hid / gate
-constexpr int kScratchBytes = (kWaves * kMaxSegs * kC + kMaxSegs * (kC + kC1 + kC2)) * 4;
-constexpr int kSshBytes = (2 * kMaxCin + 2 * kC) * 4;   // BN1 scale | shift, BN2 scale | shift
+constexpr int kSshStride = 1024;              // floats: BN1 scale at [0, cin), shift at [1024, 1024 + cin)
+constexpr int kSshBytes = 2 * kSshStride * 4;
 constexpr size_t kSmemBytes = (size_t)kRingBytes + kSshBytes;
+// phase-2 scratch after the h image (floats unless noted)
+constexpr int kRedF = kWaves * kMaxSegs * kC;        // per wave x segment channel sums
+constexpr int kAbF = 2 * kC;                         // BN2 scale | shift
+constexpr int kCtxF = kMaxSegs * kC, kHidF = kMaxSegs * kC1, kGateF = kMaxSegs * kC2;
+constexpr int kFixF = 2 * kMaxDil * kC2;             // cross-cut conv taps of the frames next to the cut
+constexpr int kEdgeH = 2 * kMaxDil * kC;             // bf16 [part][row][c]: the h rows next to the cut
+constexpr int kScratchBytes = (kRedF + kAbF + kCtxF + kHidF + kGateF + kFixF) * 4 + kEdgeH * 2 + 16;
 static_assert(kHBytes + kScratchBytes <= kRingBytes, "h image + phase-2 scratch inside the ring");
-static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
+static_assert(kSmemBytes <= 80 * 1024, "two workgroups per CU");
+
+// per-item exchange record (bytes): segment sums, the h rows next to the cut, the first part's pre-gate conv
+constexpr int kXSums = 0;                                   // [2][kMaxSegs][kC] f32
+constexpr int kXRows = kXSums + 2 * kMaxSegs * kC * 4;      // [2][kMaxDil][kC] bf16
+constexpr int kXPre = kXRows + 2 * kMaxDil * kC * 2;        // [2][kPartT][kC2] f32
+constexpr int kXBytes = kXPre + 2 * kPartT * kC2 * 4;
+constexpr int kCnt = 4;                                     // u32 per item: arrivals, first part's decision
+constexpr int kSc1 = 16;                                    // cache-policy bits: write-through / L1 bypass
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <int N>
@@ -67,12 +86,12 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// h image: row r = frame r - kMaxDil, 128 channels (one 256-B bank row), 16-B chunk q at q ^ (r & 15)
+// h image: row r = part frame r - kMaxDil, 128 channels (one 256-B bank row), 16-B chunk q at q ^ (r & 15)
 __device__ __forceinline__ int h_off(int r, int c) { return r * kC + ((((c >> 3) ^ (r & 15)) << 3) | (c & 7)); }
 
 struct CamDenseArgs {
   const uint16_t* x;        // (B, T, ld) bf16 dense-block map; input channels [0, cin)
-  int ld, cin, T, dil;
+  int ld, cin, T, dil, B;
   const float *s1, *h1;     // BN1 (nonlinear1) folded scale / shift, [cin]
   const uint16_t* wb;       // bottleneck weights bf16 [128][cin]
   const float *a2, *b2;     // BN2 (nonlinear2) folded, [128]
@@ -80,41 +99,75 @@ struct CamDenseArgs {
   const float* bl;          // linear_local bias [32] or null
   const float *w1, *c1, *w2, *c2;   // CAMLayer linear1 (64 x 128) / linear2 (32 x 64) + biases, fp32
   uint16_t* out;            // channel slice [cin, cin + 32) of the same map (stride ld)
+  uint8_t* xr;              // [B][kXBytes] exchange records
+  unsigned* cnt;            // [B][kCnt] counters (zeroed once at allocation, monotonic)
+  unsigned long long* stamps;   // PROBE: [grid][16] s_memrealtime stamps of the phase boundaries
+  int meet_ticks;           // the first part's wait for the other (100 MHz ticks; 0 forces the hand-over)
 };
 
-__global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
+template <bool PROBE>
+__global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) {
+  // diagnostic phase stamps (100 MHz real-time counter) kept in scalar registers and stored once at the exit
+  // (a store per stamp would sit in the in-order vmcnt queue and move the kernel's own waits)
+  unsigned long long stv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  auto stamp = [&](int k) {
+    if (PROBE) stv[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto stamp_out = [&] {
+    if (PROBE && threadIdx.x == 0)
+      for (int k = 0; k < 10; ++k) a.stamps[(size_t)blockIdx.x * 16 + k] = stv[k];
+  };
+  stamp(0);
   extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
-  uint16_t* ring = sm;                                            // phase 1: [kNSlot][8 + kMaxTT][kFrag]
+  uint16_t* ring = sm;                                            // phase 1: [kNSlot][8 + kPartTT][kFrag]
   uint16_t* hs = sm;                                              // after it: [kHR][kC] h image
   float* ssh = reinterpret_cast<float*>(sm + kRingBytes / 2);     // s1 | h1
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x;
   const int T = a.T, cin = a.cin, nk = cin / 32;
   const int n_tt = (T + 15) / 16;
+  const bool split = n_tt > kPartTT;
+  const int tt_cut = (n_tt + 1) / 2;                              // tiles of part 0 when split
+  const int S = 16 * tt_cut;                                      // first frame of part 1
+  // parts of an item: ids (16 k + j, 16 k + j + r) of a group of r <= 8 items, i.e. b and b + 8 (one XCD
+  // under round-robin dealing; speed only, the protocol assumes no placement)
+  int b = blockIdx.x, part = 0;
+  if (split) {
+    const int grp = (int)blockIdx.x >> 4, j = (int)blockIdx.x & 15, r = min(8, a.B - 8 * grp);
+    part = j >= r ? 1 : 0;
+    b = 8 * grp + j - part * r;
+  }
+  const int ntt = split ? (part ? n_tt - tt_cut : tt_cut) : n_tt;
+  const int f0 = part ? S : 0;                                    // first frame of this part
+  const int f1 = min(T, f0 + 16 * ntt);
   const uint16_t* xb = a.x + (int64_t)b * T * a.ld;
 
-  for (int i = tid; i < cin; i += kThreads) {
-    ssh[i] = a.s1[i];
-    ssh[kMaxCin + i] = a.h1[i];
-  }
-  float* ab2 = ssh + 2 * kMaxCin;                                  // BN2 for the epilogue
+  // BN2 goes to registers now: loaded at the end of the GEMM they would queue behind the conv
+  // weights' loads (vmcnt is in order) and stall the epilogue on them
+  float a2v = 0.f, b2v = 0.f;
   if (tid < kC) {
-    ab2[tid] = a.a2[tid];
-    ab2[kC + tid] = a.b2[tid];
+    a2v = a.a2[tid];
+    b2v = a.b2[tid];
+  }
+  // BN1 scale / shift -> LDS by LDS-DMA ahead of the ring's first k-steps (bounds-checked: lanes past cin land
+  // as zeros), so the first k-step does not wait for a load -> store round trip
+  {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.s1), (short)0, cin * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.h1), (short)0, cin * 4, 0x00020000);
+    dma_lds16_buf(rs, (uint32_t)(w * 1024 + lane * 16), (lds_ptr_t)(ssh + w * 256));
+    dma_lds16_buf(rh, (uint32_t)(w * 1024 + lane * 16), (lds_ptr_t)(ssh + kSshStride + w * 256));
   }
 
-  // ---- phase 1: bottleneck GEMM.  Wave w owns frame tiles w, w + 8, w + 16 (the third only when
-  // w + 16 < n_tt; its DMA is then a repeat of the second tile's, so every wave issues kDmaPerWave per k-step
-  // and the vmcnt counts are uniform).
-  const bool has3 = w + 16 < n_tt;
-  const int tt2 = has3 ? w + 16 : w + 8;
-  const int tts[3] = {w, w + 8, tt2};
+  // ---- phase 1: bottleneck GEMM.  Wave w owns the part's frame tiles w, w + 4, w + 8 (the third only when
+  // w + 8 < ntt; its DMA is then a repeat of the second tile's, so every wave issues kDmaPerWave per k-step
+  // and the vmcnt counts are uniform) and out tiles 2w, 2w + 1 of the weights' DMA.
+  const bool has3 = w + 8 < ntt;
+  const int tts[3] = {w, w + 4, has3 ? w + 8 : w + 4};
   const uint16_t* xsrc[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) xsrc[j] = xb + (int64_t)min(tts[j] * 16 + l15, T - 1) * a.ld + 8 * g;
-  const uint16_t* wsrc = a.wb + (int64_t)(w * 16 + l15) * cin + 8 * g;       // weight fragment w
+  for (int j = 0; j < 3; ++j) xsrc[j] = xb + (int64_t)min(f0 + tts[j] * 16 + l15, T - 1) * a.ld + 8 * g;
+  const uint16_t* wsrc = a.wb + (int64_t)(2 * w * 16 + l15) * cin + 8 * g;   // weight fragments 2w, 2w + 1
   // LDS byte addresses for the inline-asm reads below: a compiler-visible ds_read of LDS that an LDS-DMA
   // writes gets an s_waitcnt vmcnt(0) in front of it (the compiler cannot rule out the alias), which would
   // drain the whole DMA pipeline every k-step
@@ -127,7 +180,8 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
     for (int ot = 0; ot < 8; ++ot) acc[j][ot] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto issue = [&](int s) {
     uint16_t* slot = ring + (s % kNSlot) * kSlot;
-    dma_lds16(wsrc + s * 32, (lds_ptr_t)(slot + w * kFrag));
+    dma_lds16(wsrc + s * 32, (lds_ptr_t)(slot + 2 * w * kFrag));
+    dma_lds16(wsrc + (int64_t)16 * cin + s * 32, (lds_ptr_t)(slot + (2 * w + 1) * kFrag));
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       dma_lds16(xsrc[j] + s * 32, (lds_ptr_t)(slot + (8 + tts[j]) * kFrag));
@@ -161,8 +215,8 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
           "=&v"(f.wf[6]), "=&v"(f.wf[7]), "=&v"(f.xv[0]), "=&v"(f.xv[1]), "=&v"(f.xv[2]), "=&v"(f.sc4[0]),
           "=&v"(f.sc4[1]), "=&v"(f.sh4[0]), "=&v"(f.sh4[1])
         : "v"(sb), "v"(sb + (uint32_t)((8 + tts[0]) * kFrag * 2)), "v"(sb + (uint32_t)((8 + tts[1]) * kFrag * 2)),
-          "v"(sb + (uint32_t)((8 + tts[2]) * kFrag * 2)), "v"(ssh_lds + (uint32_t)s * 128u), "i"(kMaxCin * 4),
-          "i"(kMaxCin * 4 + 16)
+          "v"(sb + (uint32_t)((8 + tts[2]) * kFrag * 2)), "v"(ssh_lds + (uint32_t)s * 128u), "i"(kSshStride * 4),
+          "i"(kSshStride * 4 + 16)
         : "memory");
   };
   // the reads above have landed; the "+v" ties keep every use of f behind this wait
@@ -227,7 +281,8 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
   else if (npro == 3) wait_vm<2 * kDmaPerWave>();
   else if (npro == 2) wait_vm<kDmaPerWave>();
   else wait_vm<0>();
-  barrier();                      // k-step 0 (and the staged BN1 / BN2 parameters) visible
+  barrier();                      // k-step 0 and BN1 (the oldest DMAs) visible
+  stamp(1);
   Frags fa, fb;
   read_issue(fa, 0);
   read_wait(fa);
@@ -235,32 +290,35 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
     step(fa, fb, s);
     if (s + 1 < nk) step(fb, fa, s + 1);
   }
-  // the L2-resident weights of the rest of the layer are requested here, in one batch, so their latency
-  // hides behind the epilogue and the channel sums: the conv's fragments, this thread's 16-wide slice of linear1 (row tid / 8) and 4-wide slice of linear2 (row tid / 16)
+  // the conv's L2-resident fragments are requested here so their latency hides behind the epilogue and the
+  // channel sums; BN2 goes to LDS (the ring is free after the barrier below)
   bf16x8 wl[2][12];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk)
       wl[nt][kk] = *reinterpret_cast<const bf16x8*>(a.wl + (nt * 16 + l15) * (3 * kC) + kk * 32 + g * 8);
-  const int j1 = tid >> 3, k1 = (tid & 7) * 16, j2 = tid >> 4, k2 = (tid & 15) * 4;
-  float4 w1v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) w1v[u] = *reinterpret_cast<const float4*>(a.w1 + j1 * kC + k1 + 4 * u);
-  const float4 w2v = *reinterpret_cast<const float4*>(a.w2 + j2 * kC1 + k2);
-  const float c1v = a.c1[j1], c2v = a.c2[j2];
-  float bl4[2][4];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bl4[nt][r] = a.bl ? a.bl[nt * 16 + 4 * g + r] : 0.f;
-  barrier();   // every wave is done with the ring: its LDS becomes the h image
+  float* red = reinterpret_cast<float*>(sm + kHBytes / 2);         // [kWaves][kMaxSegs][kC]
+  float* ab2 = red + kRedF;                                         // BN2 scale | shift
+  float* ctx = ab2 + kAbF;                                          // [kMaxSegs][kC]
+  float* hid = ctx + kCtxF;                                         // [kMaxSegs][kC1]
+  float* gate = hid + kHidF;                                        // [kMaxSegs][kC2]
+  float* fix = gate + kGateF;                                       // [2 kMaxDil][kC2]
+  uint16_t* edge = reinterpret_cast<uint16_t*>(fix + kFixF);        // [2][kMaxDil][kC] bf16
+  int* bcast = reinterpret_cast<int*>(edge + kEdgeH);
+  barrier();   // every wave is done with the ring: its LDS becomes the h image + scratch
+  stamp(2);
+  if (tid < kC) {
+    ab2[tid] = a2v;
+    ab2[kC + tid] = b2v;
+  }
+  barrier();
   // epilogue: BN2 + ReLU -> bf16 into the h image (frames >= T: zero rows, the conv's padding)
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int tt = w + 8 * j;
-    if (tt >= n_tt) continue;
-    const int t = tt * 16 + l15;
+    const int lt = w + 4 * j;
+    if ((j == 2 && !has3) || lt >= ntt) continue;
+    const int t = f0 + lt * 16 + l15;
 #pragma unroll
     for (int ot = 0; ot < 8; ++ot) {
       const int n = ot * 16 + 4 * g;
@@ -270,38 +328,41 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
       if (t < T)
         v = make_uint2(pack_bf16x2(fmaxf(fmaf(acc[j][ot][0], al.x, be.x), 0.f), fmaxf(fmaf(acc[j][ot][1], al.y, be.y), 0.f)),
                        pack_bf16x2(fmaxf(fmaf(acc[j][ot][2], al.z, be.z), 0.f), fmaxf(fmaf(acc[j][ot][3], al.w, be.w), 0.f)));
-      *reinterpret_cast<uint2*>(hs + h_off(t + kMaxDil, n)) = v;
+      *reinterpret_cast<uint2*>(hs + h_off(lt * 16 + l15 + kMaxDil, n)) = v;
     }
   }
-  // halo rows: kMaxDil before frame 0, and from the last tile's end up to what the conv reads
+  // halo rows: kMaxDil before the part's first frame and after its last tile (zeros: the item's padding, or
+  // the other part's rows, whose taps the finishing part adds across the cut)
   for (int i = tid; i < kMaxDil * (kC / 4); i += kThreads) {
     const int r = i / (kC / 4), c = (i % (kC / 4)) * 4;
     *reinterpret_cast<uint2*>(hs + h_off(r, c)) = make_uint2(0u, 0u);
-    *reinterpret_cast<uint2*>(hs + h_off(n_tt * 16 + kMaxDil + r, c)) = make_uint2(0u, 0u);
+    *reinterpret_cast<uint2*>(hs + h_off(ntt * 16 + kMaxDil + r, c)) = make_uint2(0u, 0u);
   }
+  // the gate MLP's weights: linear1 row tid / 4 (32 k per lane), linear2 row tid / 8 (8 k per lane)
+  const int j1 = tid >> 2, k1 = (tid & 3) * 32, j2 = tid >> 3, k2 = (tid & 7) * 8;
+  float4 w1v[8], w2v[2];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) w1v[u] = *reinterpret_cast<const float4*>(a.w1 + j1 * kC + k1 + 4 * u);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) w2v[u] = *reinterpret_cast<const float4*>(a.w2 + j2 * kC1 + k2 + 4 * u);
+  const float c1v = a.c1[j1], c2v = a.c2[j2];
   barrier();   // h complete
+  stamp(3);
 
-  // ---- phase 2: per-segment channel sums of h, the context (mean + segment mean), the gate MLP
-  float* red = reinterpret_cast<float*>(sm + kHBytes / 2);         // [kWaves][kMaxSegs][kC]
-  float* ctx = red + kWaves * kMaxSegs * kC;                       // [kMaxSegs][kC]
-  float* hid = ctx + kMaxSegs * kC;                                // [kMaxSegs][kC1]
-  float* gate = hid + kMaxSegs * kC1;                              // [kMaxSegs][kC2]
-  const int nseg = (T + kSeg - 1) / kSeg;
+  // ---- phase 2: per-segment channel sums of the part's h
   {
-    // lane (cg, rg): channels 8cg .. 8cg + 7 of frames rg, rg + 4, ... of the wave's frame stripe
-    const int cg = lane & 15, rg = (lane >> 4) + 4 * w;            // 32 row groups over the block
+    // lane (cg, rg): channels 8cg .. 8cg + 7 of the frames = rg (mod 16) of each segment's span in the part
+    const int cg = lane & 15, rg = (lane >> 4) + 4 * w;             // 16 row groups over the workgroup
 #pragma unroll
     for (int q = 0; q < kMaxSegs; ++q) {
       float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (q < nseg) {
-        const int t1 = min(T, (q + 1) * kSeg);
-        for (int t = q * kSeg + ((rg - q * kSeg) & 31); t < t1; t += 32) {
-          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(t + kMaxDil, 8 * cg));
+      const int ta = max(q * kSeg, f0), tb = min((q + 1) * kSeg, f1);
+      for (int t = ta + ((rg - ta) & 15); t < tb; t += 16) {
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(t - f0 + kMaxDil, 8 * cg));
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            sv[2 * u] += __uint_as_float(v[u] << 16);
-            sv[2 * u + 1] += __uint_as_float(v[u] & 0xffff0000u);
-          }
+        for (int u = 0; u < 4; ++u) {
+          sv[2 * u] += __uint_as_float(v[u] << 16);
+          sv[2 * u + 1] += __uint_as_float(v[u] & 0xffff0000u);
         }
       }
 #pragma unroll
@@ -311,89 +372,314 @@ __global__ __launch_bounds__(kThreads) void cam_dense_kernel(CamDenseArgs a) {
         const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sv[u]), __float_as_uint(sv[u]), false, false);
         sv[u] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
       }
-      if (lane < 16 && q < nseg) {
+      if (lane < 16) {
         float4* d = reinterpret_cast<float4*>(red + (w * kMaxSegs + q) * kC + 8 * cg);
         d[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         d[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
       }
     }
   }
-  // local conv (k 3, dilation dil, zero padding) of the wave's frame tiles w, w + 8, w + 16: it only needs
-  // h, so its MFMAs run here; the gate is applied once the MLP below has produced it
+  // local conv (k 3, dilation dil, zero padding) of the wave's frame tiles: it only needs h, so its MFMAs run
+  // here; the gate (and, next to a cut, the other part's taps) is applied once the MLP has produced it
   floatx4 cacc[3][2];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     cacc[j][0] = floatx4{0.f, 0.f, 0.f, 0.f};
     cacc[j][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (w + 8 * j < n_tt) {
-      const int t = (w + 8 * j) * 16 + l15;
+    const int lt = w + 4 * j;
+    if (!(j == 2 && !has3) && lt < ntt) {
+      const int r = lt * 16 + l15 + kMaxDil;
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         const int tap = kk >> 2, c = (kk & 3) * 32 + g * 8;
-        const bf16x8 hf = *reinterpret_cast<const bf16x8*>(hs + h_off(t + kMaxDil + (tap - 1) * a.dil, c));
+        const bf16x8 hf = *reinterpret_cast<const bf16x8*>(hs + h_off(r + (tap - 1) * a.dil, c));
         cacc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[0][kk], hf, cacc[j][0], 0, 0, 0);
         cacc[j][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[1][kk], hf, cacc[j][1], 0, 0, 0);
       }
     }
   }
+  float bl4[2][4];                       // the conv bias of the lane's output channels (used at the end)
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bl4[nt][r] = a.bl ? a.bl[nt * 16 + 4 * g + r] : 0.f;
   barrier();
-  if (tid < kC) {                        // ctx[q][c] = mean over all frames + mean over segment q
-    float sq[kMaxSegs], tot = 0.f;
+  stamp(4);
+  const int nseg = (T + kSeg - 1) / kSeg;
+  float sq[kMaxSegs];                    // thread c < 128: this part's segment sums of channel c
 #pragma unroll
-    for (int q = 0; q < kMaxSegs; ++q) {
-      sq[q] = 0.f;
-      if (q < nseg)
+  for (int q = 0; q < kMaxSegs; ++q) {
+    sq[q] = 0.f;
+    if (tid < kC)
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) sq[q] += red[(ww * kMaxSegs + q) * kC + tid];
-      tot += sq[q];
-    }
+      for (int ww = 0; ww < kWaves; ++ww) sq[q] += red[(ww * kMaxSegs + q) * kC + tid];
+  }
+  // ctx[q][c] = mean over all frames + mean over segment q, from the item's segment sums s (both parts')
+  auto context = [&](const float* s) {
+    float tot = 0.f;
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q) tot += s[q];
 #pragma unroll
     for (int q = 0; q < kMaxSegs; ++q)
-      if (q < nseg) ctx[q * kC + tid] = tot / (float)T + sq[q] / (float)(min(T, (q + 1) * kSeg) - q * kSeg);
-  }
-  barrier();
-  for (int q = 0; q < nseg; ++q) {       // hid = relu(W1 ctx + c1): 8 lanes per output, 16 k each
-    const float4* cq = reinterpret_cast<const float4*>(ctx + q * kC + k1);
-    float p = 0.f;
+      if (q < nseg) ctx[q * kC + tid] = tot / (float)T + s[q] / (float)(min(T, (q + 1) * kSeg) - q * kSeg);
+  };
+  auto mlp_gate = [&] {
+    for (int q = 0; q < nseg; ++q) {       // hid = relu(W1 ctx + c1): 4 lanes per output, 32 k each
+      const float4* cq = reinterpret_cast<const float4*>(ctx + q * kC + k1);
+      float p = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float4 c4 = cq[u];
-      p = fmaf(w1v[u].x, c4.x, p); p = fmaf(w1v[u].y, c4.y, p);
-      p = fmaf(w1v[u].z, c4.z, p); p = fmaf(w1v[u].w, c4.w, p);
+      for (int u = 0; u < 8; ++u) {
+        const float4 c4 = cq[u];
+        p = fmaf(w1v[u].x, c4.x, p); p = fmaf(w1v[u].y, c4.y, p);
+        p = fmaf(w1v[u].z, c4.z, p); p = fmaf(w1v[u].w, c4.w, p);
+      }
+      p += __shfl_xor(p, 1); p += __shfl_xor(p, 2);
+      if ((tid & 3) == 0) hid[q * kC1 + j1] = fmaxf(p + c1v, 0.f);
     }
-    p += __shfl_xor(p, 1); p += __shfl_xor(p, 2); p += __shfl_xor(p, 4);
-    if ((tid & 7) == 0) hid[q * kC1 + j1] = fmaxf(p + c1v, 0.f);
-  }
-  barrier();
-  for (int q = 0; q < nseg; ++q) {       // gate = sigmoid(W2 hid + c2): 16 lanes per output, 4 k each
-    const float4 h4 = *reinterpret_cast<const float4*>(hid + q * kC1 + k2);
-    float p = w2v.x * h4.x;
-    p = fmaf(w2v.y, h4.y, p); p = fmaf(w2v.z, h4.z, p); p = fmaf(w2v.w, h4.w, p);
-    p += __shfl_xor(p, 1); p += __shfl_xor(p, 2); p += __shfl_xor(p, 4); p += __shfl_xor(p, 8);
-    if ((tid & 15) == 0) gate[q * kC2 + j2] = 1.f / (1.f + expf(-(p + c2v)));
-  }
-  barrier();
-
-  // ---- phase 3: (conv + bias) x gate -> the new 32 channels
-  uint16_t* ob = a.out + (int64_t)b * T * a.ld;
+    barrier();
+    for (int q = 0; q < nseg; ++q) {       // gate = sigmoid(W2 hid + c2): 8 lanes per output, 8 k each
+      const float4* hq = reinterpret_cast<const float4*>(hid + q * kC1 + k2);
+      float p = 0.f;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int t = (w + 8 * j) * 16 + l15;
-    if (w + 8 * j < n_tt && t < T) {
+      for (int u = 0; u < 2; ++u) {
+        const float4 h4 = hq[u];
+        p = fmaf(w2v[u].x, h4.x, p); p = fmaf(w2v[u].y, h4.y, p);
+        p = fmaf(w2v[u].z, h4.z, p); p = fmaf(w2v[u].w, h4.w, p);
+      }
+      p += __shfl_xor(p, 1); p += __shfl_xor(p, 2); p += __shfl_xor(p, 4);
+      if ((tid & 7) == 0) gate[q * kC2 + j2] = 1.f / (1.f + expf(-(p + c2v)));
+    }
+  };
+  uint16_t* ob = a.out + (int64_t)b * T * a.ld;
+  // (conv + cross-cut taps + bias) x gate -> the new 32 channels of the part's own frames
+  auto emit_own = [&](bool cut) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int lt = w + 4 * j;
+      const int t = f0 + lt * 16 + l15;
+      if ((j == 2 && !has3) || lt >= ntt || t >= T) continue;
       const float* gq = gate + (t / kSeg) * kC2;
+      const int fi = t - (S - kMaxDil);
+      const bool near = cut && fi >= 0 && fi < 2 * kMaxDil;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int n = nt * 16 + 4 * g;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (cacc[j][nt][r] + bl4[nt][r]) * gq[n + r];
+        for (int r = 0; r < 4; ++r) {
+          const float c = near ? cacc[j][nt][r] + fix[fi * kC2 + n + r] : cacc[j][nt][r];
+          v[r] = (c + bl4[nt][r]) * gq[n + r];
+        }
         *reinterpret_cast<uint2*>(ob + (int64_t)t * a.ld + n) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
     }
+  };
+
+  if (!split) {
+    if (tid < kC) context(sq);
+    barrier();
+    mlp_gate();
+    barrier();
+    stamp(6);
+    emit_own(false);
+    stamp(9);
+    stamp_out();
+    return;
   }
+
+  // ---- the two parts of a split item meet through the record (hand-off table row 1: write-through stores,
+  // every storing wave's vmcnt(0), a workgroup barrier, one lane's agent-scope add; the reader loads sc1 only
+  // after its own add (or poll) has returned and a barrier)
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(a.xr + (int64_t)b * kXBytes, (short)0, kXBytes, 0x00020000);
+  unsigned* cnt = a.cnt + (int64_t)b * kCnt;
+  if (tid < kC)
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq[q]), xr, kXSums + ((part * kMaxSegs + q) * kC + tid) * 4, 0, kSc1);
+  if (tid < kMaxDil * (kC / 8)) {   // the kMaxDil h rows next to the cut, un-swizzled, also into `edge`
+    const int i = tid / (kC / 8), c = (tid % (kC / 8)) * 8;
+    const int row = part ? kMaxDil + i : ntt * 16 + i;           // part 0: frames S - kMaxDil + i, part 1: S + i
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(row, c));
+    *reinterpret_cast<u32x4_t*>(edge + (part * kMaxDil + i) * kC + c) = v;
+    __builtin_amdgcn_raw_buffer_store_b128(v, xr, kXRows + ((part * kMaxDil + i) * kC + c) * 2, 0, kSc1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+  if (tid == 0) bcast[0] = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  barrier();
+  stamp(5);
+  const unsigned arrived = (unsigned)bcast[0];
+  const unsigned epoch = (arrived >> 1) + 1u;          // 1-based index of this launch for the item
+  const bool first = !(arrived & 1u);
+  if (first) {
+    // First to arrive: wait a bounded time (10 us) for the other part, which was dispatched next to this one
+    // and has the same work, so it nearly always arrives within a few us; then each part finishes its own
+    // frames.  Past the deadline (the other part may not even be resident), hand over instead: publish this
+    // part's pre-gate conv and let the last part finish it.  The decision word tells the last part which.
+    if (tid == 0) {
+      const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + (unsigned long long)a.meet_ticks;
+      int met = 0;
+      for (;;) {
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= arrived + 2u) {
+          met = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() > deadline) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (met) __hip_atomic_store(cnt + 1, 2u * epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // self
+      bcast[1] = met;
+    }
+    barrier();
+    if (!bcast[1]) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int lt = w + 4 * j;
+        if ((j == 2 && !has3) || lt >= ntt || f0 + lt * 16 + l15 >= T) continue;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, cacc[j][nt]), xr,
+                                                 kXPre + ((part * kPartT + lt * 16 + l15) * kC2 + nt * 16 + 4 * g) * 4, 0, kSc1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier();
+      stamp(6);
+      if (tid == 0) __hip_atomic_store(cnt + 1, 2u * epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // handed over
+      stamp(9);
+      stamp_out();
+      return;
+    }
+  }
+  stamp(5);
+  // Finish this part's frames (both parts when they met; the last part also finishes a handed-over part).
+  // The cross-cut taps' weight rows are requested first (used after the MLP): frame S - kMaxDil + fi (part 0,
+  // fi < kMaxDil) misses tap 2 at part 1's row fi + dil - kMaxDil; frame S + i (part 1, i = fi - kMaxDil < dil)
+  // misses tap 0 at part 0's row kMaxDil - dil + i
+  const int other = 1 - part;
+  int fsrc = -1, ftap = 0;
+  u32x4_t fw[kC / 8];
+  if (tid < 2 * kMaxDil * kC2) {
+    const int fi = tid / kC2, o = tid % kC2;
+    if (fi < kMaxDil) {
+      if (fi + a.dil >= kMaxDil) { fsrc = fi + a.dil; ftap = 2; }      // edge row kMaxDil + (fi + dil - kMaxDil)
+    } else if (fi - kMaxDil < a.dil) {
+      fsrc = kMaxDil - a.dil + (fi - kMaxDil);
+      ftap = 0;
+    }
+    if (fsrc >= 0)
+#pragma unroll
+      for (int c = 0; c < kC / 8; ++c) fw[c] = *reinterpret_cast<const u32x4_t*>(a.wl + o * (3 * kC) + ftap * kC + 8 * c);
+  }
+  if (tid < kC) {
+    float so[kMaxSegs], s[kMaxSegs];
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q)
+      so[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, kXSums + ((other * kMaxSegs + q) * kC + tid) * 4, 0, kSc1));
+#pragma unroll
+    for (int q = 0; q < kMaxSegs; ++q) s[q] = part ? so[q] + sq[q] : sq[q] + so[q];   // part 0's sum first
+    context(s);
+  }
+  if (tid < kMaxDil * (kC / 8)) {
+    const int i = tid / (kC / 8), c = (tid % (kC / 8)) * 8;
+    *reinterpret_cast<u32x4_t*>(edge + (other * kMaxDil + i) * kC + c) =
+        __builtin_amdgcn_raw_buffer_load_b128(xr, kXRows + ((other * kMaxDil + i) * kC + c) * 2, 0, kSc1);
+  }
+  barrier();
+  mlp_gate();
+  // the conv taps across the cut
+  if (tid < 2 * kMaxDil * kC2) {
+    float s = 0.f;
+    if (fsrc >= 0) {
+      const uint16_t* e = edge + fsrc * kC;    // rows [part 0: 0, kMaxDil) | [part 1: kMaxDil, 2 kMaxDil)
+#pragma unroll
+      for (int c = 0; c < kC / 8; ++c) {
+        const u32x4_t ev = *reinterpret_cast<const u32x4_t*>(e + 8 * c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s = fmaf(__uint_as_float(fw[c][u] << 16), __uint_as_float(ev[u] << 16), s);
+          s = fmaf(__uint_as_float(fw[c][u] & 0xffff0000u), __uint_as_float(ev[u] & 0xffff0000u), s);
+        }
+      }
+    }
+    fix[tid] = s;                                 // [fi][o]
+  }
+  barrier();
+  stamp(6);
+  emit_own(true);
+  stamp(7);
+  if (first) {
+    stamp(9);
+    stamp_out();
+    return;
+  }
+  // last to arrive: the first part's decision.  It has arrived, so it is running, and it decides within its
+  // 10-us deadline (plus the pre-gate publish when it hands over) without waiting on anything.
+  if (tid == 0) {
+    unsigned spins = 0, d = 0;
+    int lost = 0;
+    while (((d = __hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) < epoch) {
+      if (++spins > (1u << 24)) {   // cannot happen by construction; never hang the GPU on a broken invariant
+        lost = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    bcast[1] = lost ? 2 : (int)(d & 1u);
+  }
+  barrier();
+  stamp(8);
+  if (bcast[1] == 0) {             // the first part finished its own frames
+    stamp(9);
+    stamp_out();
+    return;
+  }
+  const bool lost = bcast[1] == 2;
+  const int of0 = other ? S : 0, on = other ? T - S : S;
+  // the other part's frames: every 16-B chunk of this thread requested before any is used
+  constexpr int kPer = kPartT * (kC2 / 4) / kThreads;
+  static_assert(kPer * kThreads == kPartT * (kC2 / 4), "chunks per thread");
+  u32x4_t pv[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = tid + k * kThreads;
+    const int fl = i / (kC2 / 4), n = (i % (kC2 / 4)) * 4;
+    if (fl < on) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, kXPre + ((other * kPartT + fl) * kC2 + n) * 4, 0, kSc1);
+  }
+  const int nb = (tid % (kC2 / 4)) * 4;           // the thread's 4 channels (the same for every k)
+  float blv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) blv[r] = a.bl ? a.bl[nb + r] : 0.f;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int fl = (tid + k * kThreads) / (kC2 / 4), t = of0 + fl;
+    if (fl >= on) continue;
+    const float* gq = gate + (t / kSeg) * kC2;
+    const int fi = t - (S - kMaxDil);
+    const bool near = fi >= 0 && fi < 2 * kMaxDil;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float c = near ? __uint_as_float(pv[k][r]) + fix[fi * kC2 + nb + r] : __uint_as_float(pv[k][r]);
+      v[r] = lost ? __int_as_float(0x7fc00000) : (c + blv[r]) * gq[nb + r];
+    }
+    *reinterpret_cast<uint2*>(ob + (int64_t)t * a.ld + nb) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+  stamp(9);
+  stamp_out();
 }
 
 }  // namespace
+
+// The first part's wait for the other: 10 us; SDIAR_CAM_DENSE_MEET_TICKS (tests) overrides it, 0 = always hand over.
+static int meet_ticks() {
+  static const int v = getenv("SDIAR_CAM_DENSE_MEET_TICKS") ? atoi(getenv("SDIAR_CAM_DENSE_MEET_TICKS")) : 1000;
+  return v;
+}
+
+// test-only: when set, launches run the stamping instantiation and write [grid][16] stamps here
+static unsigned long long* g_cam_probe = nullptr;
+void cam_dense_set_probe(void* stamps) { g_cam_probe = static_cast<unsigned long long*>(stamps); }
 
 bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, int taps, int dil, int seg_len,
                          bool bf16) {
@@ -403,15 +689,24 @@ bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, 
          seg_len == kSeg;
 }
 
+size_t cam_dense_record_bytes(int B) { return (size_t)B * kXBytes; }
+size_t cam_dense_counter_bytes(int B) { return (size_t)B * kCnt * sizeof(unsigned); }
+
 void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
-               const float* c1, const float* w2, const float* c2, void* out, hipStream_t st) {
+               const float* c1, const float* w2, const float* c2, void* out, void* records, unsigned* counters,
+               hipStream_t st) {
   SD_CHECK(B >= 1 && T >= 1 && T <= kMaxT, kErrInvalid, "cam_dense: bad item shape");
   SD_CHECK((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0, kErrInvalid,
            "cam_dense: misaligned map");
+  const bool split = cdiv(T, 16) > kPartTT;
+  SD_CHECK(!split || (records && counters && (reinterpret_cast<uintptr_t>(records) & 15) == 0), kErrInvalid,
+           "cam_dense: items of more than 160 frames need the exchange records and counters");
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cam_dense_kernel),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cam_dense_kernel<false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cam_dense_kernel<true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     attr = true;
   }
@@ -419,9 +714,13 @@ void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const floa
   ProfScope prof("cam_dense",
                  2.0 * B * T * kC * (double)cin + 2.0 * B * T * kC2 * 3 * kC + 2.0 * B * nseg * (kC * kC1 + kC1 * kC2),
                  2.0 * B * T * ((double)cin + kC2) + 2.0 * kC * cin, st);
-  CamDenseArgs a{static_cast<const uint16_t*>(x), ld, cin, T, dil, s1, h1, static_cast<const uint16_t*>(wb), a2, b2,
-                 static_cast<const uint16_t*>(wl), bl, w1, c1, w2, c2, static_cast<uint16_t*>(out)};
-  hipLaunchKernelGGL(cam_dense_kernel, dim3(B), dim3(kThreads), kSmemBytes, st, a);
+  CamDenseArgs a{static_cast<const uint16_t*>(x), ld, cin, T, dil, B, s1, h1, static_cast<const uint16_t*>(wb), a2, b2,
+                 static_cast<const uint16_t*>(wl), bl, w1, c1, w2, c2, static_cast<uint16_t*>(out),
+                 static_cast<uint8_t*>(records), counters, g_cam_probe, meet_ticks()};
+  if (g_cam_probe)
+    hipLaunchKernelGGL(cam_dense_kernel<true>, dim3(split ? 2 * B : B), dim3(kThreads), kSmemBytes, st, a);
+  else
+    hipLaunchKernelGGL(cam_dense_kernel<false>, dim3(split ? 2 * B : B), dim3(kThreads), kSmemBytes, st, a);
   SD_LAUNCH_CHECK();
 }
 

@@ -144,6 +144,9 @@ void CamTrunk::alloc(DeviceArena& a, int max_batch, int max_frames) {
   x4_ = ws(a, Bm * T2 * 512);
   tmp_ = ws(a, Bm * T2 * 128);
   gate_ = ws(a, Bm * ((T2 + 99) / 100) * 32);
+  dense_rec_ = a.alloc(cam_dense_record_bytes(max_batch));
+  dense_cnt_ = static_cast<unsigned*>(a.alloc(cam_dense_counter_bytes(max_batch)));
+  SD_HIP(hipMemset(dense_cnt_, 0, cam_dense_counter_bytes(max_batch)));
 }
 
 Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0) const {
@@ -165,6 +168,9 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
   float* const x4 = sl(x4_, T2w * kChannels, esz);
   float* const tmp = sl(tmp_, T2w * 128, esz);
   float* const gate = sl(gate_, ((T2w + 99) / 100) * 32, 4);
+  // per-window records / counters: the two slices' launches never share one
+  void* const dense_rec = static_cast<char*>(dense_rec_) + cam_dense_record_bytes(b0);
+  unsigned* const dense_cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(dense_cnt_) + cam_dense_counter_bytes(b0));
   // ---------------- FCM head (cam_pplus_wespeaker.py:271-308), NHWC (B, F, T, 32)
   // layer1.0: A(80) -> B(40); shortcut A -> C(40); conv2 B -> A(40) + C
   // layer1.1: A -> B; conv2 B -> C + A
@@ -247,7 +253,7 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
         // the whole layer per item in one launch, the 128-channel bottleneck kept in LDS (cam_dense.hip)
         cam_dense(D.p, B, T2, ld, cin, L.dil, L.bottleneck.pre_s, L.bottleneck.pre_h, L.bottleneck.w.w,
                   L.bottleneck.alpha, L.bottleneck.beta, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
-                  act_at(D, cin).p, st);
+                  act_at(D, cin).p, dense_rec, dense_cnt, st);
         cin += L.local.w.N;
         continue;
       }

@@ -59,6 +59,8 @@ class CamTrunk {
   // Workspace.
   float *fcmA_ = nullptr, *fcmB_ = nullptr, *fcmC_ = nullptr, *x0_ = nullptr;
   float *d_[3] = {nullptr, nullptr, nullptr}, *x4_ = nullptr, *tmp_ = nullptr, *gate_ = nullptr;
+  void* dense_rec_ = nullptr;          // cam_dense exchange records, one per window
+  unsigned* dense_cnt_ = nullptr;      // cam_dense counters, one set per window (zeroed once)
 };
 
 struct CamppConfig {

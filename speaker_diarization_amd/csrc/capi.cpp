@@ -107,6 +107,15 @@ int sd_prof_query(int i, char* name, int name_len, int64_t* launches, double* fl
   return 1;
 }
 
+double sd_prof_query_steps(int i) { return sd::prof_query_steps(i); }
+
+int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream) {
+  return guard([&] {
+    SD_CHECK(steps >= 1 && us_per_step, sd::kErrInvalid, "probe_lstm_handoff: bad argument");
+    *us_per_step = sd::lstm_handoff_probe(steps, S(stream));
+  });
+}
+
 int sd_tsvad_create(const sd_tsvad_config* c, sd_tsvad** out) {
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
@@ -163,6 +172,13 @@ int sd_tsvad_status(sd_tsvad* h, void* stream) {
   return guard([&] {
     SD_CHECK(h, sd::kErrInvalid, "null argument");
     h->model->status(S(stream));
+  });
+}
+
+int sd_tsvad_set_forward_batch(sd_tsvad* h, int windows) {
+  return guard([&] {
+    SD_CHECK(h && windows >= 0, sd::kErrInvalid, "set_forward_batch: bad argument");
+    h->model->set_forward_batch(windows);
   });
 }
 
@@ -349,6 +365,17 @@ int sd_fseend_stream_reset(sd_fseend_stream* s, void* stream) {
   return guard([&] {
     SD_CHECK(s, sd::kErrInvalid, "null handle");
     s->s->reset(S(stream));
+  });
+}
+
+int sd_fseend_stream_stats(const sd_fseend_stream* s, int64_t* enc_runs, int64_t* dec_runs, int* enc_nodes,
+                           int* dec_nodes) {
+  return guard([&] {
+    SD_CHECK(s && enc_runs && dec_runs && enc_nodes && dec_nodes, sd::kErrInvalid, "null argument");
+    *enc_runs = s->s->runs(0);
+    *dec_runs = s->s->runs(1);
+    *enc_nodes = s->s->graph_nodes(0);
+    *dec_nodes = s->s->graph_nodes(1);
   });
 }
 
@@ -659,6 +686,30 @@ int sd_op_gemm_bf16(const void* x, int M, int K, int lda, int a_coff, const floa
     p.beta = beta;
     p.act = act;
     sd::conv_gemm(p, true, st);
+  });
+}
+
+int sd_debug_cam_dense_probe(void* stamps) {
+  return guard([&] { sd::cam_dense_set_probe(stamps); });
+}
+
+int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
+                    const float* wb, const float* a2, const float* b2, const float* wl, const float* bl,
+                    const float* w1, const float* c1, const float* w2, const float* c2, void* out, int repeats,
+                    void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    SD_CHECK(B >= 1 && repeats >= 1 && ld >= cin + 32 &&
+                 sd::cam_dense_supported(T, cin, ld, 128, 64, 32, 32, 3, dil, 100, true),
+             sd::kErrInvalid, "cam_dense: unsupported shape");
+    Scratch wbt((size_t)128 * cin * 2, st), wlt((size_t)32 * 3 * 128 * 2, st);
+    sd::pack_weight(wb, 128, cin, 1, wbt.p, true, st);
+    sd::pack_weight(wl, 32, 128, 3, wlt.p, true, st);   // Wt[o][tap * 128 + c]
+    Scratch rec(sd::cam_dense_record_bytes(B), st), cnt(sd::cam_dense_counter_bytes(B), st);
+    SD_HIP(hipMemsetAsync(cnt.p, 0, sd::cam_dense_counter_bytes(B), st));
+    for (int r = 0; r < repeats; ++r)
+      sd::cam_dense(x, B, T, ld, cin, dil, s1, h1, wbt.p, a2, b2, wlt.p, bl, w1, c1, w2, c2, out, rec.p,
+                    static_cast<unsigned*>(cnt.p), st);
   });
 }
 

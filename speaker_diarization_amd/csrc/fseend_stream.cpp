@@ -222,7 +222,15 @@ void FsEendStream::dec_chunk(hipStream_t st) {
   stream_dec_finish(ln.x, ln.t, bf_, ln.g, ln.b, 1e-5f, c, C, D, E_, P_, state_ + 2, st);
 }
 
+int FsEendStream::graph_nodes(int which) const {
+  if (!graph_[which]) return 0;
+  size_t n = 0;
+  SD_HIP(hipGraphGetNodes(graph_[which], nullptr, &n));
+  return (int)n;
+}
+
 void FsEendStream::run(int which, hipStream_t st) {
+  ++runs_[which];
   auto body = [&](hipStream_t s) {
     if (which == 0) enc_chunk(s);
     else dec_chunk(s);
@@ -366,6 +374,9 @@ int FsEendStream::flush(float* preds, int cap, hipStream_t st) {
 
 void FsEendStream::reset(hipStream_t st) {
   SD_HIP(hipMemsetAsync(state_, 0, 4 * sizeof(int), st));
+  // wait for the chunks flush() / push*() enqueued: they read bound_ and replay the graphs destroyed below,
+  // and set_audio() rewrites bound_ with a synchronous copy that is not ordered after a non-blocking st
+  SD_HIP(hipStreamSynchronize(st));
   n_enc_ = n_valid_ = n_dec_ = n_out_ = 0;
   closed_ = false;
   if (audio_) {   // back to feature rows until set_audio() again (the next capture rebuilds the encoder graph)

@@ -38,6 +38,9 @@ class FsEendStream {
   int frames_in() const { return n_valid_; }
   int frames_out() const { return n_out_; }
   int chunk() const { return c_; }
+  // chunks run so far (0 encoder, 1 decoder) and the nodes of the captured graph (0 if none yet)
+  int64_t runs(int which) const { return runs_[which]; }
+  int graph_nodes(int which) const;
   size_t device_bytes() const { return arena_.total(); }
 
  private:
@@ -79,6 +82,7 @@ class FsEendStream {
   hipGraph_t graph_[2] = {nullptr, nullptr};
   hipGraphExec_t exec_[2] = {nullptr, nullptr};
   bool ran_direct_[2] = {false, false};
+  int64_t runs_[2] = {0, 0};
 };
 
 }  // namespace sd

@@ -121,14 +121,21 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
                  int C2, float* gate, hipStream_t st);
 // CAM++ dense-layer tail fused (cam_fused.hip): context gate + linear_local k3 conv + gating
 // for one bf16 bottleneck map x (B, T, 128) -> out (B, T, 32) at row stride ldo (bf16).
-// One CAM++ dense layer (bottleneck BN-ReLU-1x1-BN-ReLU, CAMLayer context gate, k-3 local conv x gate) per
-// item in one launch, h kept in LDS (cam_dense.hip); x: (B, T, ld) bf16 map whose channels [0, cin) are the
-// input, out: its channel slice at cin.  bf16, T <= 320.
+// One CAM++ dense layer (bottleneck BN-ReLU-1x1-BN-ReLU, CAMLayer context gate, k-3 local conv x gate) in
+// one launch, h kept in LDS (cam_dense.hip); x: (B, T, ld) bf16 map whose channels [0, cin) are the
+// input, out: its channel slice at cin.  bf16, T <= 320.  Items of more than 160 frames run as two
+// workgroups that meet through `records` (cam_dense_record_bytes(B), 16-B aligned) and `counters`
+// (cam_dense_counter_bytes(B), zeroed ONCE when allocated, then owned by the launches: never shared by
+// launches that may run concurrently).
 bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, int taps, int dil, int seg_len,
                          bool bf16);
+size_t cam_dense_record_bytes(int B);
+void cam_dense_set_probe(void* stamps);   // test-only phase stamps ([grid][16] u64), null = off
+size_t cam_dense_counter_bytes(int B);
 void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
-               const float* c1, const float* w2, const float* c2, void* out, hipStream_t st);
+               const float* c1, const float* w2, const float* c2, void* out, void* records, unsigned* counters,
+               hipStream_t st);
 bool cam_local_fused_supported(int C, int C1, int C2, int N, int taps, int dil, int seg_len, int ldo, bool bf16);
 void cam_local_fused(const void* x, int B, int T, int dil, const void* wt, const float* bias, const float* w1,
                      const float* b1, const float* w2, const float* b2, void* out, int ldo, hipStream_t st);
@@ -278,11 +285,31 @@ void mean_sigmoid_affine(const float* x, int rows, int T, int ldx, const float* 
                          int ldo, hipStream_t st);
 
 // ---------------------------------------------------------------- ts-vad glue
+// BatchNorm1D + ReLU applied by the consumer of a conv output x = conv + bias (model.py:161-171, used at :255
+// and :393): v = relu(a[c] x + b[c]), or v = relu(x) for every window of a reference forward (a group of
+// `group` consecutive windows) whose BN input held a non-finite value: BatchNorm1D skips its BatchNorm for the
+// WHOLE batch then.  a == null: v = x (no BN here).  grp: per-group flags (nonfinite_windows) or null.
+struct BnRelu {
+  const float* a = nullptr;
+  const float* b = nullptr;
+  const int* grp = nullptr;
+  int group = 1;
+};
+// Non-finite scan of per-window inputs x (B windows of per_win floats, 16-B aligned rows): win[w] |= 1 and
+// grp_a[w / group] |= 1, grp_b[w / group] |= 1 (each nullable) for every window holding a NaN / Inf.  The
+// flags must be zeroed before (stream-ordered).  The reference's NaN reaches every BN input value of its
+// window (torch's conv / BN / ReLU / mean propagate it; CAM++'s context mean spreads it over all frames),
+// while these kernels' ReLUs (v_max_f32) drop NaN, so the flag is taken at the source.
+void nonfinite_windows(const float* x, int B, int64_t per_win, int group, int* win, int* grp_a, int* grp_b,
+                       hipStream_t st);
+// rows of `per_win` floats of every window w with win_a[w] | win_b[w] set -> NaN (the reference's logits of a
+// window with a non-finite input are NaN; win_b nullable).
+void poison_windows(float* x, int B, int64_t per_win, const int* win_a, const int* win_b, hipStream_t st);
 // rows (b, spk, t) of a (B*NS*T, 2E) buffer: [ts[b,spk,:] | mix[b,t,:]] (+ pe[t]).
 // mix rows t >= Tmix read as zeros (the pad of model.py:703-710 / :852-854).
 // model.py:862-877 (ts_embeds repeat + cat) and :876 PositionalEncoding.
 void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
-                         int T, int E, const float* pe, float* out, hipStream_t st);
+                         int T, int E, const float* pe, float* out, hipStream_t st, const BnRelu& mix_bn = BnRelu());
 
 // Chunk-streaming speaker input (ts_vad2_streaming/model.py:767-777): row (b, spk, t) =
 // [ts[b, spk] | mix[b, t]] * scale + pe[pos(t)], pos(t) = start(t / C) + t % C with start(c) = 0
@@ -290,11 +317,14 @@ void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix,
 void build_stream_input(const float* ts, const float* mix, int B, int T, int NS, int E, float scale,
                         const float* pe, int C, int left, float* out, hipStream_t st);
 // x[r, :] += pe[r % T, :]  (rows of length D at stride ld)
-void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st);
+// (bn: the rows' BatchNorm1D + ReLU first, window = row / T)
+void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st, const BnRelu& bn = BnRelu());
 
 // Per-frame mean/std over channels then Linear(2 -> E): model.py:689-696.
+// bn: speech_down_or_up's BatchNorm1D + ReLU applied to x first (window = row / rows_per_window).
 void gsp_fc(const float* x, int rows, int C, int ldx, const float* w /*E x 2*/,
-            const float* bias, int E, float* out, int ldo, hipStream_t st);
+            const float* bias, int E, float* out, int ldo, hipStream_t st, const BnRelu& bn = BnRelu(),
+            int rows_per_window = 1);
 
 // (B*NS, T, E) speaker-major rows -> (B, T, NS*E) channel-concatenated rows.
 void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out, bool out_bf16,
@@ -321,11 +351,14 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 // whh_bf16 (optional, same layout in bf16 bits): bf16-MFMA recurrence (bf16 mode); the
 // cell state, gates and h stay fp32, h is rounded to bf16 only as the MFMA operand.
 // work: per-handle device scratch of lstm_work_floats(B, H, ndir) floats (the persistent bf16
-// kernel keeps its h exchange and counters there).  host_err (optional, a pinned slot of the handle's
-// PinnedFlags, one per recurrence of a forward): receives a stream-ordered copy of the persistent
-// kernel's poll-timeout flag; the handle raises kErrHip for a set slot once the stream has completed
-// (sd_tsvad_status / sd_eda_status after the forward), or at the latest on its next call.
+// kernel keeps its h exchange and counters there).  host_err (optional, the DEVICE address of a pinned
+// slot of the handle's PinnedFlags): a persistent launch whose poll timed out sets it to 1 from the
+// kernel itself and nothing ever writes 0 there but the host's take(), so the report is sticky across
+// any number of forwards enqueued before the handle raises kErrHip (sd_tsvad_status / sd_eda_status after
+// the forward, or at the latest its next call).
 int64_t lstm_work_floats(int B, int H, int ndir);
+// Exchange floor of the persistent recurrence (sd_probe_lstm_handoff): us per step of its hand-off alone.
+float lstm_handoff_probe(int steps, hipStream_t st);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr,

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
     float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
     uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err,
-    unsigned spin_limit) {
+    unsigned spin_limit, int* __restrict__ host_err) {
   constexpr int H = LS_H, BB = 16 * MT;
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -368,6 +368,8 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
   // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
   const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  // sticky report into the handle's pinned slot: only ever 1 from here, cleared by the host after a sync
+  if (bad && host_err && tid == 0) __hip_atomic_store(host_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const float qnan = __int_as_float(0x7fc00000);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -386,18 +388,71 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   }
 }
 
-// Poll bound of the persistent kernel's waits: 2^22 polls (~0.1 s).  SDIAR_LSTM_SPIN_LIMIT (tests only)
-// shrinks it so a test can force the co-residency-lost path and check that it is reported.
+// The exchange alone (sd_probe_lstm_handoff): one group of 4 workgroups runs lstm_group_bf16_kernel<1>'s
+// per-step protocol -- bounded poll of the group counter, every h fragment of the step requested in one
+// batch (sc1), publish of the lane's 4 units (sc1 stores, vmcnt(0), barrier, one agent-scope add) -- with
+// no gate arithmetic: its time per step is the floor the recurrence's step can approach.
+__global__ __launch_bounds__(256) void lstm_handoff_probe_kernel(int steps, uint16_t* __restrict__ hx,
+                                                                 unsigned* __restrict__ cnt, int* __restrict__ err,
+                                                                 unsigned spin_limit, float* __restrict__ sink) {
+  constexpr int H = LS_H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int ub = 64 * (int)(blockIdx.x & 3) + 16 * w + 4 * g;
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, 2 * 16 * H * 2, 0x00020000);
+  auto off = [&](int parity, int b, int u) { return (uint32_t)(((parity * 16 + b) * H + u) * 2); };
+  float hr = (float)ub;
+  auto publish = [&](int parity) {
+    const u32x2_t v = {pack_bf16x2(hr, hr), pack_bf16x2(hr, hr)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rh, off(parity, l15, ub), 0, 16);   // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  publish(0);
+  for (int step = 0; step < steps; ++step) {
+    if (tid == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 4u * (step + 1)) {
+        if (spins >= spin_limit) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        ++spins;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u32x4_t f[H / 32];
+#pragma unroll
+    for (int kc = 0; kc < H / 32; ++kc) f[kc] = __builtin_amdgcn_raw_buffer_load_b128(rh, off(step & 1, l15, kc * 32 + 8 * g), 0, 16);
+    uint32_t x = 0;
+#pragma unroll
+    for (int kc = 0; kc < H / 32; ++kc) x ^= f[kc][0] ^ f[kc][3];
+    hr = __uint_as_float((x & 0x007fffffu) | 0x3f800000u);   // the next publish depends on every load
+    publish((step + 1) & 1);
+  }
+  if (tid == 0) sink[blockIdx.x] = hr;
+}
+
+// Poll bound of the persistent kernel's waits: 2^22 polls (~0.1 s).  Tests only: SDIAR_LSTM_SPIN_LIMIT
+// shrinks it so a test can force the co-residency-lost path and check that it is reported;
+// SDIAR_LSTM_SPIN_LIMIT_LAUNCHES=n applies that limit to the first n persistent launches of the process
+// only (a forced timeout followed by clean forwards: the report must survive them).
 unsigned lstm_spin_limit() {
   static const unsigned v = getenv("SDIAR_LSTM_SPIN_LIMIT") ? (unsigned)strtoul(getenv("SDIAR_LSTM_SPIN_LIMIT"), nullptr, 10)
                                                            : (1u << 22);
-  return v;
+  static const long n_forced = getenv("SDIAR_LSTM_SPIN_LIMIT_LAUNCHES") ? atol(getenv("SDIAR_LSTM_SPIN_LIMIT_LAUNCHES")) : -1;
+  static long launches = 0;
+  if (n_forced < 0) return v;
+  return launches++ < n_forced ? v : (1u << 22);
 }
 
 template <int MT>
 void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                        const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
-                       uint16_t* hx, int Bp, unsigned* counters, int* err, hipStream_t st) {
+                       uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
@@ -408,7 +463,7 @@ void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_
   const int groups = ndir * cdiv(B, 16 * MT);
   hipLaunchKernelGGL((lstm_group_bf16_kernel<MT>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
-                     counters, err, lstm_spin_limit());
+                     counters, err, lstm_spin_limit(), host_err);
   SD_LAUNCH_CHECK();
 }
 
@@ -462,6 +517,34 @@ size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * L
 
 }  // namespace
 
+float lstm_handoff_probe(int steps, hipStream_t st) {
+  const size_t hx_bytes = (size_t)2 * 16 * LS_H * 2, ctl = 4 * LS_CNT_STRIDE + 64;
+  void* buf = nullptr;
+  SD_HIP(hipMalloc(&buf, hx_bytes + ctl + 64));
+  SD_HIP(hipMemsetAsync(buf, 0, hx_bytes + ctl + 64, st));
+  uint16_t* hx = static_cast<uint16_t*>(buf);
+  unsigned* cnt = reinterpret_cast<unsigned*>(static_cast<char*>(buf) + hx_bytes);
+  int* err = reinterpret_cast<int*>(cnt + LS_CNT_STRIDE);
+  float* sink = reinterpret_cast<float*>(static_cast<char*>(buf) + hx_bytes + ctl);
+  hipEvent_t a, b;
+  SD_HIP(hipEventCreate(&a));
+  SD_HIP(hipEventCreate(&b));
+  SD_HIP(hipEventRecord(a, st));
+  hipLaunchKernelGGL(lstm_handoff_probe_kernel, dim3(4), dim3(256), 0, st, steps, hx, cnt, err, lstm_spin_limit(), sink);
+  SD_LAUNCH_CHECK();
+  SD_HIP(hipEventRecord(b, st));
+  SD_HIP(hipEventSynchronize(b));
+  float ms = 0.f;
+  SD_HIP(hipEventElapsedTime(&ms, a, b));
+  int e = 0;
+  SD_HIP(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(buf);
+  SD_CHECK(e == 0, kErrHip, "lstm hand-off probe: a poll timed out");
+  return ms * 1000.f / (float)steps;
+}
+
 int64_t lstm_work_floats(int B, int H, int ndir) {
   int64_t step_path = 3LL * ndir * B * H;
   if (H != LS_H) return step_path;
@@ -493,18 +576,18 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
+      prof.set_steps(T);   // sequential steps (an upper bound with packed lengths: the launch runs max(len))
       int* err = reinterpret_cast<int*>(ctl + (size_t)groups * LS_CNT_STRIDE);
       switch (mt) {
-        case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
-        case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
-        case 3: launch_lstm_group<3>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
-        case 4: launch_lstm_group<4>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
-        case 5: launch_lstm_group<5>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
-        default: launch_lstm_group<6>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, st); break;
+        case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
+        case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
+        case 3: launch_lstm_group<3>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
+        case 4: launch_lstm_group<4>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
+        case 5: launch_lstm_group<5>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
+        default: launch_lstm_group<6>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
       }
-      // stream-ordered copy of the err word into this recurrence's own pinned slot; the handle reads
-      // it after the forward's stream completes (sd_*_status) or, at the latest, on its next call
-      if (host_err) SD_HIP(hipMemcpyAsync(host_err, err, sizeof(int), hipMemcpyDeviceToHost, st));
+      // a timed-out launch sets *host_err itself (sticky); the handle reads it after the forward's stream
+      // completes (sd_*_status) or, at the latest, on its next call
       return;
     }
   }

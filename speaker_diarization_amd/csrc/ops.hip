@@ -1,6 +1,8 @@
 // Small fused kernels around the GEMMs: FCM stem, CAMLayer context gate,
 // LayerNorm, GroupNorm+SiLU, GLU+depthwise conv, GSP, layout glue.
 // HBM-bound; written for coalesced 64-lane access, no MFMA.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -508,9 +510,58 @@ void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const 
 }
 
 // ------------------------------------------------------------------ TS-VAD glue
+__device__ __forceinline__ float bn_relu(const BnRelu& p, int window, int c, float x) {
+  if (!p.a) return x;
+  const bool bypass = p.grp && p.grp[window / p.group];
+  return fmaxf(bypass ? x : fmaf(p.a[c], x, p.b[c]), 0.f);
+}
+
+__global__ __launch_bounds__(256) void nonfinite_windows_kernel(const float* __restrict__ x, int64_t per_win, int group,
+                                                                int* win, int* grp_a, int* grp_b) {
+  const int w = blockIdx.x;
+  const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)w * per_win);
+  const int64_t n4 = per_win / 4;
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.y * blockDim.x) {
+    const float4 v = xr[i];
+    bad |= ((__float_as_uint(v.x) | 0x807fffffu) == 0xffffffffu) | ((__float_as_uint(v.y) | 0x807fffffu) == 0xffffffffu) |
+           ((__float_as_uint(v.z) | 0x807fffffu) == 0xffffffffu) | ((__float_as_uint(v.w) | 0x807fffffu) == 0xffffffffu);
+  }
+  if (blockIdx.y == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < per_win; i += blockDim.x)
+      bad |= (__float_as_uint(x[(int64_t)w * per_win + i]) | 0x807fffffu) == 0xffffffffu;
+  if (__any(bad) && (threadIdx.x & 63) == 0) {   // one atomic per wave that saw one
+    atomicOr(win + w, 1);
+    if (grp_a) atomicOr(grp_a + w / group, 1);
+    if (grp_b) atomicOr(grp_b + w / group, 1);
+  }
+}
+
+void nonfinite_windows(const float* x, int B, int64_t per_win, int group, int* win, int* grp_a, int* grp_b,
+                       hipStream_t st) {
+  SD_CHECK(B >= 1 && per_win >= 1 && group >= 1 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && per_win % 4 == 0,
+           kErrInvalid, "nonfinite_windows: bad shape");
+  const int chunks = (int)std::min<int64_t>(64, cdiv((int)std::min<int64_t>(per_win / 4, 1 << 30), 256 * 8));
+  hipLaunchKernelGGL(nonfinite_windows_kernel, dim3(B, std::max(chunks, 1)), dim3(256), 0, st, x, per_win, group, win,
+                     grp_a, grp_b);
+  SD_LAUNCH_CHECK();
+}
+
+__global__ void poison_windows_kernel(float* x, int64_t per_win, const int* __restrict__ win_a,
+                                      const int* __restrict__ win_b) {
+  const int w = blockIdx.x;
+  if (!win_a[w] && !(win_b && win_b[w])) return;
+  for (int64_t i = threadIdx.x; i < per_win; i += blockDim.x) x[(int64_t)w * per_win + i] = __int_as_float(0x7fc00000);
+}
+
+void poison_windows(float* x, int B, int64_t per_win, const int* win_a, const int* win_b, hipStream_t st) {
+  hipLaunchKernelGGL(poison_windows_kernel, dim3(B), dim3(256), 0, st, x, per_win, win_a, win_b);
+  SD_LAUNCH_CHECK();
+}
+
 __global__ void build_speaker_input_kernel(const float* __restrict__ ts, const float* __restrict__ mix,
                                            int ldmix, int Tmix, int B, int NS, int T, int E,
-                                           const float* __restrict__ pe, float* __restrict__ out) {
+                                           const float* __restrict__ pe, float* __restrict__ out, BnRelu bn) {
   const int row = blockIdx.x;  // (b, spk, t)
   const int t = row % T;
   const int bs = row / T;
@@ -521,16 +572,16 @@ __global__ void build_speaker_input_kernel(const float* __restrict__ ts, const f
   const float* mx = mix + ((int64_t)b * Tmix + (mv ? t : 0)) * ldmix;
   const float* pr = pe ? pe + (int64_t)t * 2 * E : nullptr;
   for (int c = threadIdx.x; c < 2 * E; c += blockDim.x) {
-    float v = c < E ? ts_r[c] : (mv ? mx[c - E] : 0.f);
+    float v = c < E ? ts_r[c] : (mv ? bn_relu(bn, b, c - E, mx[c - E]) : 0.f);
     if (pr) v += pr[c];
     o[c] = v;
   }
 }
 
 void build_speaker_input(const float* ts, const float* mix, int ldmix, int Tmix, int B, int NS,
-                         int T, int E, const float* pe, float* out, hipStream_t st) {
+                         int T, int E, const float* pe, float* out, hipStream_t st, const BnRelu& mix_bn) {
   hipLaunchKernelGGL(build_speaker_input_kernel, dim3(B * NS * T), dim3(128), 0, st, ts, mix,
-                     ldmix, Tmix, B, NS, T, E, pe, out);
+                     ldmix, Tmix, B, NS, T, E, pe, out, mix_bn);
   SD_LAUNCH_CHECK();
 }
 
@@ -557,31 +608,43 @@ void build_stream_input(const float* ts, const float* mix, int B, int T, int NS,
 }
 
 __global__ void add_pe_kernel(float* __restrict__ x, int rows, int T, int D, int ld,
-                              const float* __restrict__ pe) {
+                              const float* __restrict__ pe, BnRelu bn) {
   const int row = blockIdx.x;
   const int t = row % T;
-  for (int c = threadIdx.x; c < D; c += blockDim.x) x[(int64_t)row * ld + c] += pe[(int64_t)t * D + c];
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float* p = x + (int64_t)row * ld + c;
+    *p = bn_relu(bn, row / T, c, *p) + pe[(int64_t)t * D + c];
+  }
 }
 
-void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st) {
-  hipLaunchKernelGGL(add_pe_kernel, dim3(rows), dim3(128), 0, st, x, rows, T, D, ld, pe);
+void add_pe(float* x, int rows, int T, int D, int ld, const float* pe, hipStream_t st, const BnRelu& bn) {
+  hipLaunchKernelGGL(add_pe_kernel, dim3(rows), dim3(128), 0, st, x, rows, T, D, ld, pe, bn);
   SD_LAUNCH_CHECK();
 }
 
 __global__ __launch_bounds__(256) void gsp_fc_kernel(const float* __restrict__ x, int rows, int C,
                                                      int ldx, const float* __restrict__ w,
                                                      const float* __restrict__ bias, int E,
-                                                     float* __restrict__ out, int ldo) {
+                                                     float* __restrict__ out, int ldo, BnRelu bn, int rpw) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + (int64_t)row * ldx;
+  constexpr int kMaxPer = 4;                      // C <= 256
+  float v[kMaxPer];
   float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += xr[c];
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int c = lane + 64 * k;
+    v[k] = c < C ? bn_relu(bn, row / rpw, c, xr[c]) : 0.f;
+    s += v[k];
+  }
   s = warp_sum(s);
   const float mean = s / (float)C;
   float q = 0.f;
-  for (int c = lane; c < C; c += 64) { float d = xr[c] - mean; q += d * d; }
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k)
+    if (lane + 64 * k < C) { const float d = v[k] - mean; q += d * d; }
   q = warp_sum(q);
   const float sd = sqrtf(q / (float)(C - 1));   // torch.std default: unbiased
   float* o = out + (int64_t)row * ldo;
@@ -589,9 +652,10 @@ __global__ __launch_bounds__(256) void gsp_fc_kernel(const float* __restrict__ x
 }
 
 void gsp_fc(const float* x, int rows, int C, int ldx, const float* w, const float* bias, int E,
-            float* out, int ldo, hipStream_t st) {
+            float* out, int ldo, hipStream_t st, const BnRelu& bn, int rows_per_window) {
+  SD_CHECK(C >= 2 && C <= 256 && rows_per_window >= 1, kErrInvalid, "gsp_fc: C must be in [2, 256]");
   hipLaunchKernelGGL(gsp_fc_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, C, ldx, w, bias,
-                     E, out, ldo);
+                     E, out, ldo, bn, rows_per_window);
   SD_LAUNCH_CHECK();
 }
 

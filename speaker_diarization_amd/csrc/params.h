@@ -44,20 +44,22 @@ class DeviceArena {
   size_t total_ = 0;
 };
 
-// Pinned host ints per handle, one slot per device-side failure flag of a forward (each persistent
-// LSTM recurrence copies its poll-timeout word into its own slot, stream-ordered).  take() reads and
-// clears every slot: callers use it once the stream has completed (the same call) or on the next call.
+// Pinned, device-mapped host ints per handle, one slot per persistent LSTM recurrence of a forward.  A
+// launch that lost co-residency stores 1 into its slot from the kernel (system scope); nothing on the
+// device ever stores 0, so reports accumulate across forwards until take() reads and clears every slot
+// (callers use it once the stream has completed, in the same call, or on the next call).
 class PinnedFlags {
  public:
   static constexpr int kSlots = 4;
   PinnedFlags() {
-    SD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), kSlots * sizeof(int), hipHostMallocDefault));
+    SD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), kSlots * sizeof(int), hipHostMallocMapped));
     for (int i = 0; i < kSlots; ++i) p_[i] = 0;
+    SD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_), p_, 0));
   }
   ~PinnedFlags() { if (p_) (void)hipHostFree(p_); }
   PinnedFlags(const PinnedFlags&) = delete;
   PinnedFlags& operator=(const PinnedFlags&) = delete;
-  int* get(int slot) const { return p_ + slot; }
+  int* get(int slot) const { return d_ + slot; }   // device address of the slot (kernel argument)
   int take() {
     int any = 0;
     for (int i = 0; i < kSlots; ++i) any |= __atomic_exchange_n(p_ + i, 0, __ATOMIC_ACQ_REL);
@@ -71,6 +73,7 @@ class PinnedFlags {
 
  private:
   int* p_ = nullptr;
+  int* d_ = nullptr;
 };
 
 struct Folded {        // per-channel affine y = x*scale + shift

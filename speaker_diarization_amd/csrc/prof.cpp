@@ -10,11 +10,11 @@ namespace {
 struct Rec {
   std::string name;
   hipEvent_t a, b;
-  double flops, bytes;
+  double flops, bytes, steps;
 };
 struct Agg {
   long long launches = 0;
-  double flops = 0, bytes = 0, ms = 0;
+  double flops = 0, bytes = 0, ms = 0, steps = 0;
 };
 
 std::mutex g_mu;
@@ -32,6 +32,7 @@ void drain_locked() {
     a.flops += r.flops;
     a.bytes += r.bytes;
     a.ms += ms;
+    a.steps += r.steps;
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
   }
@@ -63,6 +64,15 @@ bool prof_query(int i, std::string& name, long long& launches, double& flops, do
   return true;
 }
 
+double prof_query_steps(int i) {
+  std::lock_guard<std::mutex> l(g_mu);
+  drain_locked();
+  if (i < 0 || i >= (int)g_agg.size()) return 0;
+  auto it = g_agg.begin();
+  std::advance(it, i);
+  return it->second.steps;
+}
+
 ProfScope::ProfScope(const char* name, double flops, double bytes, hipStream_t st)
     : name_(name), flops_(flops), bytes_(bytes), st_(st) {
   if (!g_on) return;
@@ -79,7 +89,7 @@ ProfScope::~ProfScope() {
   if (!on_) return;
   (void)hipEventRecord(b_, st_);
   std::lock_guard<std::mutex> l(g_mu);
-  g_pending.push_back(Rec{name_, a_, b_, flops_, bytes_});
+  g_pending.push_back(Rec{name_, a_, b_, flops_, bytes_, steps_});
 }
 
 }  // namespace sd

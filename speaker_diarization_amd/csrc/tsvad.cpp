@@ -34,7 +34,18 @@ void TsvadModel::finalize() {
                         "xvector.dense.nonlinear.batchnorm.running_var"})
     ps_.mark(se + k);
   // ---- speech_down_or_up (model.py:385-395)
-  down_ = conv_bn("speech_down_or_up.0.weight", "speech_down_or_up.1.bn", "speech_down_or_up.0.bias");
+  // BatchNorm1D (model.py:161-171) is not folded into the conv: a batch holding a NaN skips it, so the conv
+  // stores conv + bias and its consumer applies BN + ReLU, or ReLU alone for such a batch (BnRelu)
+  auto bn_only = [&](const std::string& bn) {
+    std::vector<float> sc, sh;
+    ps_.bn_fold(bn, sc, sh);
+    BnRelu r;
+    r.a = arena_.upload(sc);
+    r.b = arena_.upload(sh);
+    return r;
+  };
+  down_ = conv_bn("speech_down_or_up.0.weight", "", "speech_down_or_up.0.bias");
+  down_bn_ = bn_only("speech_down_or_up.1.bn");
   down_.pre_s = cam_.out_s();
   down_.pre_h = cam_.out_h();
 
@@ -47,7 +58,8 @@ void TsvadModel::finalize() {
       single_.push_back(loader().transformer("single_backend.layers." + std::to_string(i)));
       multi_.push_back(loader().transformer("multi_backend.layers." + std::to_string(i)));
     }
-    backend_down_ = conv_bn("backend_down.0.weight", "backend_down.1.bn", "backend_down.0.bias");
+    backend_down_ = conv_bn("backend_down.0.weight", "", "backend_down.0.bias");
+    backend_bn_ = bn_only("backend_down.1.bn");
     fc_ = loader().linear("fc");
   } else {
     gsp_w_ = arena_.upload(ps_.get("gsp_fc.weight").data);
@@ -101,6 +113,7 @@ void TsvadModel::alloc_workspace() {
   X2_ = ws(rows * E);
   partial_ = ws(Bm * NS * ((E + 63) / 64) * 2);
   lstm_work_ = ws(lstm_work_floats((int)Bm, cfg_.lstm_hidden, 2));
+  nonfinite_ = static_cast<int*>(arena_.alloc(4 * (size_t)Bm * sizeof(int)));
 }
 
 TsvadModel::~TsvadModel() {
@@ -147,10 +160,23 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     x4 = cam_.forward(ref, B, Tf, st);
   }
   const int T2 = CamTrunk::out_frames(Tf);
-  // ---------------- speech_down_or_up (out_nonlinear BN-ReLU fused as prologue), fp32 out
   const int E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim, NS = cfg_.max_num_speaker;
+  // ---------------- BatchNorm1D's NaN bypass: which windows hold a non-finite input, which reference forwards
+  // (groups of fwd_batch_ windows) therefore skip the BatchNorm
+  const int G = fwd_batch_ > 0 ? fwd_batch_ : B;
+  int* win_fb = nonfinite_;
+  int* win_ts = nonfinite_ + cfg_.max_batch;
+  int* grp_sd = nonfinite_ + 2 * cfg_.max_batch;
+  int* grp_bd = nonfinite_ + 3 * cfg_.max_batch;
+  SD_HIP(hipMemsetAsync(nonfinite_, 0, 4 * (size_t)cfg_.max_batch * sizeof(int), st));
+  nonfinite_windows(ref, B, (int64_t)Tf * 80, G, win_fb, grp_sd, grp_bd, st);
+  nonfinite_windows(ts, B, (int64_t)NS * SE, G, win_ts, nullptr, cfg_.variant == 0 ? grp_bd : nullptr, st);
+  BnRelu sd_bn = down_bn_, bd_bn = backend_bn_;
+  sd_bn.grp = grp_sd; sd_bn.group = G;
+  bd_bn.grp = grp_bd; bd_bn.group = G;
+  // ---------------- speech_down_or_up conv (out_nonlinear BN-ReLU fused as prologue) + bias, fp32 out; its
+  // BatchNorm1D + ReLU are applied by the consumer (gsp_fc / build_speaker_input)
   ConvGemmArgs pd = cam_conv1d(x4, B, T2, CamTrunk::kChannels, down_, 2, 2, 1, Tens{mix_, false}, SE);
-  pd.act = kActRelu;
   const int T3 = pd.Wo;
   conv_gemm(pd, bf, st);
   const int S = B * NS;
@@ -159,7 +185,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
              "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
     SD_CHECK(Tl <= pe_len_, kErrShape, "label length exceeds positional-encoding max_len");
     // Per-speaker encoder over S = B*NS sequences (model.py:869-879).
-    build_speaker_input(ts, mix_, SE, T3, B, NS, Tl, SE, pe_, X_, st);
+    build_speaker_input(ts, mix_, SE, T3, B, NS, Tl, SE, pe_, X_, st, sd_bn);
     // bf16(X) for the first layer's in-projection too (every later layer gets it from the LayerNorms): an
     // fp32 A operand would send that GEMM to the register-staged kernel (C4: 1.5 ms per 640 windows vs 0.3)
     if (bf) f32_to_bf16(X_, (int64_t)S * Tl * E, enc_work().AO, st);
@@ -167,9 +193,8 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
       run_transformer(single_[i], X_, S, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, bf || i > 0);
     speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
     ConvGemmArgs p = cam_conv1d(Tens{X2_, bf}, B, Tl, NS * E, backend_down_, 1, 2, 1, Tens{X_, false}, E);
-    p.act = kActRelu;
     conv_gemm(p, bf, st);
-    add_pe(X_, B * Tl, Tl, E, E, pe_, st);
+    add_pe(X_, B * Tl, Tl, E, E, pe_, st, bd_bn);   // backend_down's BatchNorm1D + ReLU, then the PE
     if (bf) f32_to_bf16(X_, (int64_t)B * Tl * E, enc_work().AO, st);
     for (size_t i = 0; i < multi_.size(); ++i)
       run_transformer(multi_[i], X_, B, Tl, E, cfg_.num_attention_head, nullptr, enc_work(), st, 0, 0, bf || i > 0);
@@ -179,7 +204,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   } else {
     SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape,
              "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
-    gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st);
+    gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st, sd_bn, T3);
     if (SE == 192 && E == 2 * SE && conformer_stack_fused(conf_, E, bf)) {
       // the row programs build [ts | mix] on load and write the bf16 speakers-to-channels rows directly
       // windows [b0, b0 + Bh): every buffer of the fused stack is addressed from the slice's first row
@@ -224,6 +249,8 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
   }
+  // a window whose fbank or target-speaker embeddings hold a NaN / Inf has NaN logits in the reference
+  poison_windows(logits, B, (int64_t)NS * Tl, win_fb, win_ts, st);
 }
 
 }  // namespace sd

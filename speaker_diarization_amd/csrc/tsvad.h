@@ -32,6 +32,9 @@ class TsvadModel {
   // ref_speech (B, T_fb, 80) fbank, target_speech (B, NS, 192), logits out (B, NS, T_lab).
   void forward(const float* ref_speech, const float* target_speech, int B, int T_fb, int T_lab,
                float* logits, hipStream_t st);
+  // Windows per reference forward call: the scope of BatchNorm1D's NaN bypass (model.py:161-171), i.e. the
+  // batch a NaN window disables speech_down_or_up's / backend_down's BatchNorm for.  0: the whole call.
+  void set_forward_batch(int windows) { fwd_batch_ = windows; }
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
   // waits for `st` and raises kErrHip if a persistent LSTM of the forwards enqueued on it timed out
@@ -52,7 +55,10 @@ class TsvadModel {
   bool finalized_ = false;
 
   CamTrunk cam_;     // speech_encoder.* (CAM++ get_time_out=True)
-  ConvL down_;
+  ConvL down_;        // speech_down_or_up conv: epilogue = + bias only (its BatchNorm1D is down_bn_)
+  BnRelu down_bn_, backend_bn_;   // folded BatchNorms, applied (or bypassed) by the consumers
+  int fwd_batch_ = 0;
+  int* nonfinite_ = nullptr;      // [win_fbank B | win_ts B | grp_speech B | grp_backend B]
   const float *gsp_w_ = nullptr, *gsp_b_ = nullptr;
   const float* pe_ = nullptr;
   int pe_len_ = 0;

@@ -91,11 +91,16 @@ class TSVADModel:
         return int(_lib.load().sd_tsvad_device_bytes(self._h))
 
     # ------------------------------------------------------------------ forward
-    def forward(self, ref_speech, target_speech, labels, num_updates: int = 0, out=None, check: bool = True):
+    def forward(self, ref_speech, target_speech, labels, num_updates: int = 0, out=None, check: bool = True,
+                forward_batch: int = 0):
         """ref_speech (B, T_fb, 80), target_speech (B, NS, 192), labels (B, NS, T) (only
         labels.size(-1) is read, model.py:681/770) -> logits (B, NS, T).  check: wait for the
         stream and raise RuntimeError in this call if the BiLSTM's persistent recurrence lost
-        co-residency (its logits are NaN); check=False defers that to status()."""
+        co-residency (its logits are NaN); check=False defers that to status().
+        forward_batch: windows per reference forward call when this call covers several of them (the
+        pipeline's fused device batches): the scope of BatchNorm1D's NaN bypass (model.py:161-171).  0: this
+        call is one batch (up to max_batch windows: a call split into several device forwards bypasses per
+        device forward)."""
         import torch
         B, T_fb, F = ref_speech.shape
         T_lab = labels if isinstance(labels, int) else labels.size(-1)
@@ -108,10 +113,11 @@ class TSVADModel:
         if B > self.max_batch:
             for s in range(0, B, self.max_batch):
                 e = min(B, s + self.max_batch)
-                self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False)
+                self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False, forward_batch=forward_batch)
             if check:
                 self.status()
             return out
+        _lib.call("sd_tsvad_set_forward_batch", self._h, int(forward_batch))
         _lib.call("sd_tsvad_forward", self._h, _lib.ptr(ref), _lib.ptr(ts), B, T_fb, T_lab, _lib.ptr(out),
                   _lib.stream_ptr(self.device))
         if check:

@@ -42,6 +42,8 @@ class TSVADPipeline:
         # a model that fixes the reference batch (the streaming decoder: batch 1) overrides it
         batch_size = getattr(model, "reference_batch_size", batch_size)
         self.batch_size = min(batch_size, model.max_batch)
+        # a device batch fuses whole reference batches: BatchNorm1D's NaN bypass keeps the reference scope
+        self._fwd_kw = {"forward_batch": self.batch_size} if isinstance(model, TSVADModel) else {}
 
     def plan(self, n_labels: int) -> WindowPlan:
         return plan_windows(n_labels, self.cfg.rs_len, self.segment_shift, self.cfg.label_rate,
@@ -68,7 +70,8 @@ class TSVADPipeline:
         ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
         for b0, b1, T_out, T_lab in self.device_batches(plan, w0, w1):
             ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
-            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab, check=False)
+            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab, check=False,
+                                    **self._fwd_kw)
             out[b0 - w0:b1 - w0, :, :T_lab] = lg
         status = getattr(self.model, "status", None)
         if status is not None:

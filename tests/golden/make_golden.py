@@ -54,13 +54,32 @@ TSVAD_CASES = {
     "tsvad_v1_rs6": (1, 6, 2, 598, 150, 99, 779),
 }
 
+# BatchNorm1D's NaN bypass (model.py:161-171): one window of the batch carries a NaN fbank value, so the
+# reference skips speech_down_or_up's (and variant 0's backend_down's) BatchNorm for EVERY window of the
+# batch.  name: (base TSVAD_CASES entry, window, fbank frame, mel bin of the NaN)
+TSVAD_NAN_CASES = {
+    "tsvad_v1_rs6_nan": ("tsvad_v1_rs6", 1, 300, 17),
+    "tsvad_v0_rs4_nan": ("tsvad_v0_rs4_short", 2, 5, 0),
+}
+
+
+def tsvad_case_inputs(name):
+    """(case tuple, ref_speech, ts) of a TSVAD_CASES or TSVAD_NAN_CASES name."""
+    base, nan_at = (TSVAD_NAN_CASES[name][0], TSVAD_NAN_CASES[name][1:]) if name in TSVAD_NAN_CASES else (name, None)
+    case = TSVAD_CASES[base]
+    _, _, B, T_fb, n_lab, iseed, _ = case
+    ref_speech, ts = tsvad_inputs(B, T_fb, n_lab, seed=iseed)
+    if nan_at is not None:
+        ref_speech[nan_at] = np.nan
+    return case, ref_speech, ts
+
 
 def make_tsvad(name):
     import torch
     from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
     from oracle.torchaudio_conformer import Conformer
 
-    variant, rs_len, B, T_fb, n_lab, iseed, wseed = TSVAD_CASES[name]
+    (variant, rs_len, B, T_fb, n_lab, iseed, wseed), ref_speech, ts = tsvad_case_inputs(name)
     install_stubs(Conformer)
     sys.path.insert(0, os.path.join(REF, "egs/alimeeting/ts_vad2"))
     import model as ref_model  # reference TSVADModel
@@ -83,7 +102,6 @@ def make_tsvad(name):
     m.eval()
     sd = to_torch(tsvad_state_dict(cfg, seed=wseed))
     m.load_state_dict(sd, strict=True)
-    ref_speech, ts = tsvad_inputs(B, T_fb, n_lab, seed=iseed)
     labels = torch.zeros(B, 4, n_lab)
     with torch.no_grad():
         logits = m(torch.from_numpy(ref_speech), torch.from_numpy(ts), labels, num_updates=0)
@@ -469,7 +487,7 @@ if __name__ == "__main__":
     names = sys.argv[1:] or (list(TSVAD_CASES) + list(EDA_CASES) + ["eda_tfm_batch"] + list(FEATURE_CASES)
                              + list(FSEEND_CASES) + list(EEND_CASES) + list(CAMPP_CASES) + list(CAMPP_EXTRACT) + list(TSVAD_STREAM_CASES))
     for n in names:
-        if n in TSVAD_CASES:
+        if n in TSVAD_CASES or n in TSVAD_NAN_CASES:
             make_tsvad(n)
         elif n in CAMPP_CASES:
             make_campp(n)

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from make_golden import TSVAD_CASES, tsvad_inputs
+from make_golden import TSVAD_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
 from speaker_diarization_amd.ts_vad.model import TSVADModel
 from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
 
@@ -45,6 +45,41 @@ def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
     err = np.abs(out - g["logits"]).max()
     print(f"{name} {precision}: max|logit diff| = {err:.3e} (|logit| max {np.abs(g['logits']).max():.3f})")
     assert err < (FP32_ATOL if precision == "fp32" else BF16_ATOL)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(TSVAD_NAN_CASES))
+def test_tsvad_nan_window_bypasses_batchnorm(gpu, name, precision):
+    """BatchNorm1D's NaN bypass (model.py:161-171) against the reference run on a batch with one NaN fbank
+    value: the NaN window's logits are NaN, every other window matches the reference (whose BatchNorm was
+    skipped for the whole batch) within the usual bound.  Then the scope: with forward_batch = 1 each window
+    is its own reference batch, so the others keep their BatchNorm (== the golden without the NaN)."""
+    (v, rs, B, T, nl, iseed, wseed), x, ts = tsvad_case_inputs(name)
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    m = _model(v, rs, wseed, precision, gpu)
+    xd, tsd = torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu)
+    out = m.forward(xd, tsd, nl).cpu().numpy()
+    bad = TSVAD_NAN_CASES[name][1]
+    keep = [i for i in range(B) if i != bad]
+    assert np.isnan(out[bad]).all() and np.isfinite(out[keep]).all()
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    assert np.abs(out[keep] - g["logits"][keep]).max() < tol
+    base = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{TSVAD_NAN_CASES[name][0]}.npz")["logits"]
+    alone = m.forward(xd, tsd, nl, forward_batch=1).cpu().numpy()
+    assert np.isnan(alone[bad]).all()
+    assert np.abs(alone[keep] - base[keep]).max() < tol
+    # a NaN in a window's target-speaker embedding poisons that window only (no BatchNorm sees it in
+    # variant 1; variant 0's backend_down does, so its batch bypasses there too -- oracle)
+    ts2 = ts.copy()
+    ts2[keep[0], 1, 3] = np.nan
+    out2 = m.forward(torch.from_numpy(np.nan_to_num(x, nan=0.0)).to(gpu), torch.from_numpy(ts2).to(gpu), nl).cpu().numpy()
+    assert np.isnan(out2[keep[0]]).all()
+    from oracle.tsvad_ref import tsvad_forward
+    ref2 = tsvad_forward(to_torch(tsvad_state_dict(_cfg(v, rs), seed=wseed)), _cfg(v, rs),
+                         torch.from_numpy(np.nan_to_num(x, nan=0.0)), torch.from_numpy(ts2), nl).numpy()
+    assert np.isnan(ref2[keep[0]]).all()
+    others = [i for i in range(B) if i != keep[0]]
+    assert np.abs(out2[others] - ref2[others]).max() < tol
 
 
 def test_tsvad_strict_load_errors(gpu):

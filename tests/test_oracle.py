@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from make_golden import TSVAD_CASES, tsvad_inputs
+from make_golden import TSVAD_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
 from oracle import fbank_ref
 from oracle.tsvad_ref import speech_encoder_out, tsvad_forward
 from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
@@ -25,6 +25,25 @@ def test_tsvad_oracle_matches_reference(name):
     np.testing.assert_allclose(out, g["logits"], atol=2e-5, rtol=1e-5)
     enc = speech_encoder_out(sd, torch.from_numpy(x)).numpy()
     np.testing.assert_allclose(enc, g["speech_enc"], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", list(TSVAD_NAN_CASES))
+def test_tsvad_oracle_nan_bypass_matches_reference(name):
+    """BatchNorm1D (model.py:161-171): one NaN fbank value in window w -> the reference skips the wrapped
+    BatchNorm for EVERY window of the batch and window w's logits are NaN.  The oracle restates it and is
+    pinned by the reference run on that input (make_golden.py TSVAD_NAN_CASES)."""
+    (v, rs, B, T, nl, iseed, wseed), x, ts = tsvad_case_inputs(name)
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    cfg = _cfg(v, rs)
+    sd = to_torch(tsvad_state_dict(cfg, seed=wseed))
+    out = tsvad_forward(sd, cfg, torch.from_numpy(x), torch.from_numpy(ts), nl).numpy()
+    bad = TSVAD_NAN_CASES[name][1]
+    assert np.isnan(g["logits"][bad]).all() and np.isnan(out[bad]).all()
+    keep = [i for i in range(B) if i != bad]
+    np.testing.assert_allclose(out[keep], g["logits"][keep], atol=2e-5, rtol=1e-5)
+    # the bypass is real: the finite windows differ from the same windows in a batch without the NaN
+    base = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{TSVAD_NAN_CASES[name][0]}.npz")["logits"]
+    assert np.abs(base[keep] - g["logits"][keep]).max() > 1e-3
 
 
 def test_tsvad_golden_shapes():

@@ -8,9 +8,11 @@ OUT=$1; shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for WL in "$@"; do
-  BENCH="bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline"
+  # --no-c4-ref: the C2 line would otherwise also run the 60-min C4 meeting (c4_60min_ms), whose kernels
+  # would land in C2's kernel-trace table; C4 is profiled as its own workload
+  BENCH="bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-c4-ref"
   if [ "${FULL:-0}" = 1 ]; then
-    timeout -k 10 400 python3 bench.py --workload $WL --steps 5 --warmup 2 > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
+    timeout -k 10 400 python3 bench.py --workload $WL --steps 5 --warmup 2 --no-c4-ref > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
   else
     timeout -k 10 240 python3 $BENCH > "$OUT/bench_$WL.json" 2> "$OUT/bench_$WL.err"
   fi
