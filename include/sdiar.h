@@ -91,6 +91,13 @@ int sd_tsvad_status(sd_tsvad* h, void* stream);
  * BatchNorm for every window of ITS batch.  0 (default): the whole sd_tsvad_forward call is one batch. */
 int sd_tsvad_set_forward_batch(sd_tsvad* h, int windows);
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
+/* Diagnostics only (not on the product path, which launches directly): capture sd_tsvad_forward once into a
+ * hipGraph, optionally write its DOT dump to `dot_path`, replay it `replays` times on `stream` (each replay
+ * rewrites logits) and wait; and the device buffers of the forward's stages (which: 0 mix, 1 mixg, 2 X2,
+ * 3 H, 4 Y) for stage-by-stage comparisons. */
+int sd_tsvad_forward_graph(sd_tsvad* h, const float* ref_speech, const float* target_speech, int B, int T_fbank,
+                           int T_label, float* logits, int replays, const char* dot_path, void* stream);
+int sd_tsvad_debug_buffer(const sd_tsvad* h, int which, void** ptr, int64_t* bytes);
 int sd_tsvad_destroy(sd_tsvad* h);
 
 /* ------------------------------------------------------------------ chunk-streaming TS-VAD

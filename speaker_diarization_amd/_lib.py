@@ -121,6 +121,9 @@ _SIGS = {
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_status": (c_int, [c_void_p, c_void_p]),
     "sd_tsvad_set_forward_batch": (c_int, [c_void_p, c_int]),
+    "sd_tsvad_forward_graph": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_char_p,
+                                       c_void_p]),
+    "sd_tsvad_debug_buffer": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_int64)]),
     "sd_tsvad_device_bytes": (c_int64, [c_void_p]),
     "sd_tsvad_destroy": (c_int, [c_void_p]),
     "sd_tsvad_stream_create": (c_int, [POINTER(TsvadStreamConfig), POINTER(c_void_p)]),
@@ -247,6 +250,11 @@ def check(status: int, what: str = ""):
     if status == SD_ERR_PARAM:
         raise RuntimeError(f"Error(s) in loading state_dict: {msg}")
     raise SdiarError(msg)
+
+
+def has(name: str) -> bool:
+    """Whether the loaded library exports `name` (only an older SDIAR_LIB build in an A/B run may not)."""
+    return hasattr(load(), name)
 
 
 def call(name: str, *args):

@@ -168,6 +168,21 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref, const float* ts, int B, int 
   });
 }
 
+int sd_tsvad_forward_graph(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
+                           int replays, const char* dot_path, void* stream) {
+  return guard([&] {
+    SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
+    h->model->forward_graph(ref, ts, B, Tf, Tl, logits, replays, dot_path, S(stream));
+  });
+}
+
+int sd_tsvad_debug_buffer(const sd_tsvad* h, int which, void** ptr, int64_t* bytes) {
+  return guard([&] {
+    SD_CHECK(h && ptr && bytes, sd::kErrInvalid, "null argument");
+    h->model->debug_buffer(which, ptr, bytes);
+  });
+}
+
 int sd_tsvad_status(sd_tsvad* h, void* stream) {
   return guard([&] {
     SD_CHECK(h, sd::kErrInvalid, "null argument");

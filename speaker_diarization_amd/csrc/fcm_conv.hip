@@ -345,29 +345,53 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       f32x2 sw2[4][9];
 #pragma unroll
       for (int k = 0; k < 72; ++k) sw2[k / 18][k % 9][(k / 9) & 1] = swp[k];
-      for (int i = tid; i < n_vec; i += kBandThreads) {
-        const int pix = i >> 2, rr = pix / Wp, px = pix - rr * Wp;
-        const bool ok = (unsigned)(hb + rr) < (unsigned)p.H && (unsigned)(w0 + px) < (unsigned)W;
-        float x9[9];
+      // Items: (staged row rr, 4 consecutive frames px0.., this thread's channel group).  The 4 pixels share
+      // their 3 x 6 fbank taps (one 16-B + one 8-B LDS read per tap row instead of 9 reads per pixel), and
+      // (rr, quad) advance incrementally: the per-pixel pix / Wp of the one-pixel loop was a division per item.
+      // The fmaf chain per (pixel, channel) is unchanged (taps in (dh, dw) order): bit-identical output.
+      const int nq = (Wp + 3) >> 2;
+      const int n_items = NR * nq;                 // per channel group
+      int qx = (tid >> 2) % nq, qr = (tid >> 2) / nq;
+      for (int it = tid >> 2; it < n_items; it += kBandThreads / 4) {
+        const int px0 = qx * 4;
+        float xw[3][6];
 #pragma unroll
-        for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-          for (int dw = 0; dw < 3; ++dw) x9[dh * 3 + dw] = fbs[(rr + dh) * (Wp + 2) + px + dw];
-        float v[8];
-#pragma unroll
-        for (int u2 = 0; u2 < 4; ++u2) {
-          f32x2 acc = {0.f, 0.f};
-#pragma unroll
-          for (int k = 0; k < 9; ++k) acc = __builtin_elementwise_fma(sw2[u2][k], f32x2{x9[k], x9[k]}, acc);
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int u = 2 * u2 + e;
-            v[u] = ok ? fmaxf(acc[e] * s_al[u] + s_be[u], 0.f) : 0.f;
-          }
+        for (int dh = 0; dh < 3; ++dh) {
+          const float* r0 = fbs + (qr + dh) * (Wp + 2) + px0;
+          const float4 a4 = *reinterpret_cast<const float4*>(r0);
+          const float2 b2 = *reinterpret_cast<const float2*>(r0 + 4);
+          xw[dh][0] = a4.x; xw[dh][1] = a4.y; xw[dh][2] = a4.z; xw[dh][3] = a4.w; xw[dh][4] = b2.x; xw[dh][5] = b2.y;
         }
-        *reinterpret_cast<uint4*>(xs + pix * kPS + (i & 3) * 8) =
-            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                       pack_bf16x2(v[6], v[7]));
+        const bool row_ok = (unsigned)(hb + qr) < (unsigned)p.H;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+          const int px = px0 + pp;
+          if (px >= Wp) break;
+          const bool ok = row_ok && (unsigned)(w0 + px) < (unsigned)W;
+          float v[8];
+#pragma unroll
+          for (int u2 = 0; u2 < 4; ++u2) {
+            f32x2 acc = {0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+              const float xv = xw[k / 3][pp + k % 3];
+              acc = __builtin_elementwise_fma(sw2[u2][k], f32x2{xv, xv}, acc);
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int u = 2 * u2 + e;
+              v[u] = ok ? fmaxf(acc[e] * s_al[u] + s_be[u], 0.f) : 0.f;
+            }
+          }
+          *reinterpret_cast<uint4*>(xs + (qr * Wp + px) * kPS + (tid & 3) * 8) =
+              make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+        }
+        qx += kBandThreads / 4;
+        while (qx >= nq) {
+          qx -= nq;
+          ++qr;
+        }
       }
       const uint16_t* wtp = reinterpret_cast<const uint16_t*>(p.Wt);
       asm volatile("" : "+s"(wtp));

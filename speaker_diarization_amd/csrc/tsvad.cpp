@@ -122,6 +122,54 @@ TsvadModel::~TsvadModel() {
   if (side_) (void)hipStreamDestroy(side_);
 }
 
+void TsvadModel::forward_graph(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits, int replays,
+                               const char* dot, hipStream_t st) {
+  SD_CHECK(replays >= 0, kErrInvalid, "forward_graph: replays < 0");
+  hipStream_t cap = nullptr;
+  SD_HIP(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ex = nullptr;
+  try {
+    SD_HIP(hipStreamSynchronize(st));
+    SD_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    try {
+      forward(ref, ts, B, Tf, Tl, logits, cap);
+    } catch (...) {
+      hipGraph_t bad = nullptr;
+      (void)hipStreamEndCapture(cap, &bad);
+      if (bad) (void)hipGraphDestroy(bad);
+      throw;
+    }
+    SD_HIP(hipStreamEndCapture(cap, &g));
+    if (dot) SD_HIP(hipGraphDebugDotPrint(g, dot, 0));
+    SD_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    for (int r = 0; r < replays; ++r) SD_HIP(hipGraphLaunch(ex, st));
+    SD_HIP(hipStreamSynchronize(st));
+  } catch (...) {
+    if (ex) (void)hipGraphExecDestroy(ex);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(cap);
+    throw;
+  }
+  (void)hipGraphExecDestroy(ex);
+  (void)hipGraphDestroy(g);
+  (void)hipStreamDestroy(cap);
+}
+
+void TsvadModel::debug_buffer(int which, void** ptr, int64_t* bytes) const {
+  const int64_t Bm = cfg_.max_batch, T3 = ((CamTrunk::out_frames(cfg_.max_fbank_frames)) - 1) / 2 + 1;
+  const int64_t Tl = std::max<int64_t>(T3 + 3, (int64_t)cfg_.rs_len * 25), E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim;
+  const int64_t NS = cfg_.max_num_speaker;
+  switch (which) {
+    case 0: *ptr = mix_; *bytes = Bm * T3 * SE * 4; break;
+    case 1: *ptr = mixg_; *bytes = Bm * T3 * SE * 4; break;
+    case 2: *ptr = X2_; *bytes = Bm * NS * Tl * E * 4; break;
+    case 3: *ptr = H_; *bytes = Bm * NS * Tl * E * 4; break;
+    case 4: *ptr = Y_; *bytes = Bm * NS * Tl * E * 4; break;
+    default: throw Error{kErrInvalid, "debug_buffer: unknown buffer"};
+  }
+}
+
 // Direct launches only.  A hipGraph replay of this forward was tried (round 2-3) and dropped: it measured no
 // faster on C2 (34.3 vs 34.4 ms per 10-min step: ~150 launches against a 34-ms GPU span) and its replays did
 // not reproduce the direct launches' posteriors (max |diff| 0.098 from the second replay on, and a replayed

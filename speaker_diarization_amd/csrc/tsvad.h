@@ -37,6 +37,14 @@ class TsvadModel {
   void set_forward_batch(int windows) { fwd_batch_ = windows; }
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
+  // Diagnostics (graph-replay investigation): captures forward() once into a hipGraph on a capture stream
+  // (the fork / join side stream included), then replays it `replays` times on st; `dot` (nullable) receives
+  // hipGraphDebugDotPrint of the captured graph.
+  void forward_graph(const float* ref_speech, const float* target_speech, int B, int T_fb, int T_lab, float* logits,
+                     int replays, const char* dot, hipStream_t st);
+  // Device buffers of the forward's stages for stage-by-stage comparisons: 0 mix (speech_down_or_up conv),
+  // 1 mixg (gsp_fc), 2 X2 (conformer stack output), 3 H (BiLSTM gates), 4 Y (BiLSTM output).
+  void debug_buffer(int which, void** ptr, int64_t* bytes) const;
   // waits for `st` and raises kErrHip if a persistent LSTM of the forwards enqueued on it timed out
   void status(hipStream_t st) { SD_HIP(hipStreamSynchronize(st)); lstm_err_.raise_if_set(); }
   ~TsvadModel();
