@@ -420,6 +420,10 @@ int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const
 /* Diagnostics: while `stamps` (device, >= 16 u64 per workgroup of a launch) is non-NULL, every cam_dense
  * launch records its workgroups' phase-boundary s_memrealtime stamps there (tools/cam_dense_probe.py). */
 int sd_debug_cam_dense_probe(void* stamps);
+/* Diagnostics: a captured graph [memsetAsync(X, 0) -> kernel: Y = X, then X = 7] (fork != 0: the kernel behind
+ * an event fork / join of a second captured stream) replayed `replays` times; bad_per_replay (host, replays
+ * ints) = Y values that were not 0 after each replay. */
+int sd_probe_graph_memset(int n, int replays, int fork, int* bad_per_replay, void* stream);
 /* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);

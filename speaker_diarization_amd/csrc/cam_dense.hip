@@ -379,6 +379,56 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
       }
     }
   }
+  barrier();
+  const int nseg = (T + kSeg - 1) / kSeg;
+  float sq[kMaxSegs];                    // thread c < 128: this part's segment sums of channel c
+#pragma unroll
+  for (int q = 0; q < kMaxSegs; ++q) {
+    sq[q] = 0.f;
+    if (tid < kC)
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) sq[q] += red[(ww * kMaxSegs + q) * kC + tid];
+  }
+  // ---- a split item's two parts meet through the record (hand-off table row 1: write-through stores, every
+  // storing wave's vmcnt(0), a workgroup barrier, one lane's agent-scope add; the reader loads sc1 only after
+  // its own add (or poll) has returned and a barrier).  The part publishes and counts its arrival as soon as its
+  // sums exist, so the other part's arrival overlaps this part's conv MFMAs.
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(a.xr + (int64_t)b * kXBytes, (short)0, kXBytes, 0x00020000);
+  unsigned* cnt = a.cnt + (int64_t)b * kCnt;
+  // the cross-cut taps' weight rows (used after the MLP): frame S - kMaxDil + fi (part 0, fi < kMaxDil) misses
+  // tap 2 at part 1's row fi + dil - kMaxDil; frame S + i (part 1, i = fi - kMaxDil < dil) misses tap 0 at part
+  // 0's row kMaxDil - dil + i
+  int fsrc = -1, ftap = 0;
+  u32x4_t fw[kC / 8];
+  if (split) {
+    if (tid < kC)
+#pragma unroll
+      for (int q = 0; q < kMaxSegs; ++q)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq[q]), xr, kXSums + ((part * kMaxSegs + q) * kC + tid) * 4, 0, kSc1);
+    if (tid < kMaxDil * (kC / 8)) {   // the kMaxDil h rows next to the cut, un-swizzled, also into `edge`
+      const int i = tid / (kC / 8), c = (tid % (kC / 8)) * 8;
+      const int row = part ? kMaxDil + i : ntt * 16 + i;           // part 0: frames S - kMaxDil + i, part 1: S + i
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(row, c));
+      *reinterpret_cast<u32x4_t*>(edge + (part * kMaxDil + i) * kC + c) = v;
+      __builtin_amdgcn_raw_buffer_store_b128(v, xr, kXRows + ((part * kMaxDil + i) * kC + c) * 2, 0, kSc1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    if (tid == 0) bcast[0] = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 2 * kMaxDil * kC2) {
+      const int fi = tid / kC2, o = tid % kC2;
+      if (fi < kMaxDil) {
+        if (fi + a.dil >= kMaxDil) { fsrc = fi + a.dil; ftap = 2; }      // edge row kMaxDil + (fi + dil - kMaxDil)
+      } else if (fi - kMaxDil < a.dil) {
+        fsrc = kMaxDil - a.dil + (fi - kMaxDil);
+        ftap = 0;
+      }
+      if (fsrc >= 0)
+#pragma unroll
+        for (int c = 0; c < kC / 8; ++c) fw[c] = *reinterpret_cast<const u32x4_t*>(a.wl + o * (3 * kC) + ftap * kC + 8 * c);
+    }
+  }
   // local conv (k 3, dilation dil, zero padding) of the wave's frame tiles: it only needs h, so its MFMAs run
   // here; the gate (and, next to a cut, the other part's taps) is applied once the MLP has produced it
   floatx4 cacc[3][2];
@@ -405,15 +455,6 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
     for (int r = 0; r < 4; ++r) bl4[nt][r] = a.bl ? a.bl[nt * 16 + 4 * g + r] : 0.f;
   barrier();
   stamp(4);
-  const int nseg = (T + kSeg - 1) / kSeg;
-  float sq[kMaxSegs];                    // thread c < 128: this part's segment sums of channel c
-#pragma unroll
-  for (int q = 0; q < kMaxSegs; ++q) {
-    sq[q] = 0.f;
-    if (tid < kC)
-#pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) sq[q] += red[(ww * kMaxSegs + q) * kC + tid];
-  }
   // ctx[q][c] = mean over all frames + mean over segment q, from the item's segment sums s (both parts')
   auto context = [&](const float* s) {
     float tot = 0.f;
@@ -487,27 +528,6 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
     return;
   }
 
-  // ---- the two parts of a split item meet through the record (hand-off table row 1: write-through stores,
-  // every storing wave's vmcnt(0), a workgroup barrier, one lane's agent-scope add; the reader loads sc1 only
-  // after its own add (or poll) has returned and a barrier)
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc(a.xr + (int64_t)b * kXBytes, (short)0, kXBytes, 0x00020000);
-  unsigned* cnt = a.cnt + (int64_t)b * kCnt;
-  if (tid < kC)
-#pragma unroll
-    for (int q = 0; q < kMaxSegs; ++q)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq[q]), xr, kXSums + ((part * kMaxSegs + q) * kC + tid) * 4, 0, kSc1);
-  if (tid < kMaxDil * (kC / 8)) {   // the kMaxDil h rows next to the cut, un-swizzled, also into `edge`
-    const int i = tid / (kC / 8), c = (tid % (kC / 8)) * 8;
-    const int row = part ? kMaxDil + i : ntt * 16 + i;           // part 0: frames S - kMaxDil + i, part 1: S + i
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(hs + h_off(row, c));
-    *reinterpret_cast<u32x4_t*>(edge + (part * kMaxDil + i) * kC + c) = v;
-    __builtin_amdgcn_raw_buffer_store_b128(v, xr, kXRows + ((part * kMaxDil + i) * kC + c) * 2, 0, kSc1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  barrier();
-  if (tid == 0) bcast[0] = (int)__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  barrier();
   stamp(5);
   const unsigned arrived = (unsigned)bcast[0];
   const unsigned epoch = (arrived >> 1) + 1u;          // 1-based index of this launch for the item
@@ -553,24 +573,7 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
   }
   stamp(5);
   // Finish this part's frames (both parts when they met; the last part also finishes a handed-over part).
-  // The cross-cut taps' weight rows are requested first (used after the MLP): frame S - kMaxDil + fi (part 0,
-  // fi < kMaxDil) misses tap 2 at part 1's row fi + dil - kMaxDil; frame S + i (part 1, i = fi - kMaxDil < dil)
-  // misses tap 0 at part 0's row kMaxDil - dil + i
   const int other = 1 - part;
-  int fsrc = -1, ftap = 0;
-  u32x4_t fw[kC / 8];
-  if (tid < 2 * kMaxDil * kC2) {
-    const int fi = tid / kC2, o = tid % kC2;
-    if (fi < kMaxDil) {
-      if (fi + a.dil >= kMaxDil) { fsrc = fi + a.dil; ftap = 2; }      // edge row kMaxDil + (fi + dil - kMaxDil)
-    } else if (fi - kMaxDil < a.dil) {
-      fsrc = kMaxDil - a.dil + (fi - kMaxDil);
-      ftap = 0;
-    }
-    if (fsrc >= 0)
-#pragma unroll
-      for (int c = 0; c < kC / 8; ++c) fw[c] = *reinterpret_cast<const u32x4_t*>(a.wl + o * (3 * kC) + ftap * kC + 8 * c);
-  }
   if (tid < kC) {
     float so[kMaxSegs], s[kMaxSegs];
 #pragma unroll

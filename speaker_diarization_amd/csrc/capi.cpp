@@ -704,6 +704,13 @@ int sd_op_gemm_bf16(const void* x, int M, int K, int lda, int a_coff, const floa
   });
 }
 
+int sd_probe_graph_memset(int n, int replays, int fork, int* bad_per_replay, void* stream) {
+  return guard([&] {
+    SD_CHECK(n > 0 && replays > 0 && bad_per_replay, sd::kErrInvalid, "probe_graph_memset: bad argument");
+    sd::graph_memset_probe(n, replays, fork != 0, bad_per_replay, S(stream));
+  });
+}
+
 int sd_debug_cam_dense_probe(void* stamps) {
   return guard([&] { sd::cam_dense_set_probe(stamps); });
 }

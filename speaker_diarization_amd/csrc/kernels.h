@@ -130,7 +130,10 @@ void cam_context(const void* x, bool x_bf16, int B, int T, int C, int ldx, int s
 bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, int taps, int dil, int seg_len,
                          bool bf16);
 size_t cam_dense_record_bytes(int B);
-void cam_dense_set_probe(void* stamps);   // test-only phase stamps ([grid][16] u64), null = off
+void cam_dense_set_probe(void* stamps);
+// Graph-replay diagnostic (diag.hip): [memset(X, 0) -> kernel Y = X; X = 7] replayed `replays` times;
+// bad_per_replay[r] = non-zero Y values after replay r (host array).
+void graph_memset_probe(int n, int replays, bool fork, int* bad_per_replay, hipStream_t st);   // test-only phase stamps ([grid][16] u64), null = off
 size_t cam_dense_counter_bytes(int B);
 void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,

@@ -117,7 +117,7 @@ class TSVADModel:
             if check:
                 self.status()
             return out
-        if forward_batch or _lib.has("sd_tsvad_set_forward_batch"):
+        if _lib.has("sd_tsvad_set_forward_batch"):   # (absent only from an older SDIAR_LIB in an A/B run)
             _lib.call("sd_tsvad_set_forward_batch", self._h, int(forward_batch))
         _lib.call("sd_tsvad_forward", self._h, _lib.ptr(ref), _lib.ptr(ts), B, T_fb, T_lab, _lib.ptr(out),
                   _lib.stream_ptr(self.device))

@@ -1,6 +1,6 @@
 """Print per-kernel (and per-GEMM-shape with SDIAR_PROF_DETAIL=1) timing of one pipeline step."""
 import os, sys, json
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))   # the repo root
 import torch
 from speaker_diarization_amd import _lib
 from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
