@@ -47,6 +47,8 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
   H_ = arena_.alloc(rd * ffn * es_);
   n_blocks_ = attn_decode_blocks(cap_);
   ws_ = wsb<float>((size_t)C_ * cfg.n_heads * n_blocks_ * c_ * (2 + 64));
+  dcnt_ = wsb<unsigned>((size_t)C_ * cfg.n_heads);
+  SD_HIP(hipMemset(dcnt_, 0, (size_t)C_ * cfg.n_heads * sizeof(unsigned)));
   for (int l = 0; l < cfg.enc_n_layers; ++l) kv_enc_.push_back(arena_.alloc((size_t)cap_ * 2 * D * es_));
   for (int a = 0; a < cfg.dec_n_layers; ++a) kv_dec_.push_back(arena_.alloc((size_t)cap_ * C_ * 2 * D * es_));
   hist_ = wsb<float>((size_t)cap_ * D);
@@ -136,7 +138,7 @@ void FsEendStream::enc_chunk(hipStream_t st) {
     a.k = kv_enc_[l]; a.v = static_cast<char*>(kv_enc_[l]) + D * es_; a.kv_tok = 2 * D;
     a.out = AO_; a.o_tok = D;
     a.nseq = 1; a.nq = c; a.nh = nh; a.hd = D / nh; a.scale = 1.f / std::sqrt((float)(D / nh));
-    a.pos = state_; a.delay = 0; a.max_keys = cap_; a.n_blocks = n_blocks_; a.ws = ws_; a.io_bf16 = bf_;
+    a.pos = state_; a.delay = 0; a.max_keys = cap_; a.n_blocks = n_blocks_; a.ws = ws_; a.io_bf16 = bf_; a.cnt = dcnt_;
     attn_decode(a, st);
     conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
     ln = PendingLn{xb[xi], T_, L.n1g, L.n1b, xb[xi ^ 1]};
@@ -192,7 +194,7 @@ void FsEendStream::dec_chunk(hipStream_t st) {
       d.kv_tok = (int64_t)C * 2 * D; d.kv_seq = 2 * D;
       d.out = AO_; d.o_tok = (int64_t)C * D; d.o_seq = D;
       d.nseq = C; d.nq = c; d.nh = nh; d.hd = D / nh; d.scale = scale;
-      d.pos = state_ + 2; d.delay = 0; d.max_keys = cap_; d.n_blocks = n_blocks_; d.ws = ws_; d.io_bf16 = bf_;
+      d.pos = state_ + 2; d.delay = 0; d.max_keys = cap_; d.n_blocks = n_blocks_; d.ws = ws_; d.io_bf16 = bf_; d.cnt = dcnt_;
       attn_decode(d, st);
     }
     conv_gemm(lin(ao, n, D, f.out1, f.out1_b, t, D), bf_, st);

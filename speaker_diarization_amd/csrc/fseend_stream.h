@@ -65,6 +65,7 @@ class FsEendStream {
   // staging (chunk-sized)
   float *F_ = nullptr, *Y_ = nullptr, *X_ = nullptr, *W_ = nullptr, *Yc_ = nullptr, *E_ = nullptr;
   float *X2_ = nullptr, *A2_ = nullptr, *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;
+  unsigned* dcnt_ = nullptr;           // attn_decode's per-(sequence, head) block counters (zeroed once)
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

@@ -471,6 +471,9 @@ struct DecodeAttnArgs {
   int n_blocks = 0;           // workspace partials per (sequence, head) >= attn_decode_blocks(max_keys)
   float* ws = nullptr;        // nseq*nh*n_blocks*nq*(2+hd) floats
   bool io_bf16 = false;
+  // optional: nseq*nh counters, zeroed once when allocated and shared only by launches that run one after
+  // another -- the last block of each (sequence, head) then merges the partials (no combine launch)
+  unsigned* cnt = nullptr;
 };
 int attn_decode_blocks(int max_keys);
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st);

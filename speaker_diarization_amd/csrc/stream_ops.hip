@@ -72,12 +72,42 @@ __device__ __forceinline__ void load_row64(const act_t<IOBF>* p, float* v) {
   }
 }
 
+// The nblk partials of one (sequence, head), merged: wave -> query, lane -> head dim (lane-parallel max /
+// weights, shuffled weights for o).  SC1: the partials were handed over inside this launch (write-through
+// stores, read back with L1-bypassing sc1 loads).
+template <bool IOBF, bool SC1>
+__device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh, int qi, int lane, int nblk) {
+  using io_t = act_t<IOBF>;
+  const int s = sh / a.nh, h = sh % a.nh;
+  const int64_t bstride = (int64_t)a.nq * (2 + kHD);
+  const int64_t base = (int64_t)sh * nblk * bstride + qi * (2 + kHD);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
+  auto ld = [&](int64_t i) {
+    if constexpr (SC1) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, (uint32_t)(i * 4), 0, 16));
+    else return a.ws[i];
+  };
+  const float mv = lane < nblk ? ld(base + lane * bstride) : -INFINITY;
+  const float lv = lane < nblk ? ld(base + lane * bstride + 1) : 0.f;
+  const float M = warp_max(mv);
+  const float w = (mv == -INFINITY) ? 0.f : __expf(mv - M);
+  const float L = warp_sum(w * lv);
+  float o = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < nblk; ++b) o = fmaf(__shfl(w, b, 64), ld(base + b * bstride + 2 + lane), o);
+  io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
+  st_act(ob, lane, o / L);
+}
+
 // grid (nblk, nseq*nh), 256 threads.  Wave w of block b walks the 64-key tiles
 // t = 4b + w, 4b + w + 4*nblk, ... below the device cursor's key count with an online
 // softmax per query (lane = key for q·k; lane = (key parity, head-dim pair) for p·v, so
 // each lane issues 32 independent 4/8-B V loads per tile), the 4 waves merge in LDS and
-// the block writes one (m, l, o[64]) partial per query.
-template <bool IOBF, int QMAX>
+// the block writes one (m, l, o[64]) partial per query.  FUSED (a.cnt set): the partials are
+// stored write-through, every block counts itself on its (sequence, head)'s counter, and the
+// block whose add completes the launch's nblk merges them (MI355X guide hand-off row 1) -- the
+// separate combine launch (a dependent kernel boundary + its own ramp per attention) is gone.
+// The counters are monotonic: each launch adds exactly nblk per (sequence, head).
+template <bool IOBF, int QMAX, bool FUSED>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
   using io_t = act_t<IOBF>;
   __shared__ float qs[QMAX][kHD];
@@ -170,7 +200,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
     }
   }
   __syncthreads();
-  float* part = a.ws + ((int64_t)sh * gridDim.x + blockIdx.x) * nq * (2 + kHD);
+  const int64_t poff = ((int64_t)sh * gridDim.x + blockIdx.x) * nq * (2 + kHD);
+  float* part = a.ws + poff;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
+  auto put = [&](int64_t i, float v) {   // i: index within this block's partial
+    if constexpr (FUSED) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rw, (uint32_t)((poff + i) * 4), 0, 16);
+    else part[i] = v;
+  };
   for (int i = tid; i < nq * kHD; i += 256) {
     const int qi = i / kHD, d = i % kHD;
     float M = -INFINITY;
@@ -183,11 +219,23 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
       L = fmaf(e, wl[w][qi], L);
       O = fmaf(e, ps[w][qi][d], O);
     }
-    part[qi * (2 + kHD) + 2 + d] = O;
+    put(qi * (2 + kHD) + 2 + d, O);
     if (d == 0) {
-      part[qi * (2 + kHD)] = M;
-      part[qi * (2 + kHD) + 1] = L;
+      put(qi * (2 + kHD), M);
+      put(qi * (2 + kHD) + 1, L);
     }
+  }
+  if constexpr (FUSED) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned n = gridDim.x;
+      last = (__hip_atomic_fetch_add(a.cnt + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % n) == n - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int qi = wid; qi < nq; qi += 4) combine_partials<IOBF, true>(a, sh, qi, lane, gridDim.x);
   }
 }
 
@@ -195,22 +243,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
 // nblk (<= 64) block partials (lane-parallel max / weights, shuffled weights for o).
 template <bool IOBF>
 __global__ __launch_bounds__(256) void attn_combine_kernel(DecodeAttnArgs a, int nblk) {
-  using io_t = act_t<IOBF>;
-  const int sh = blockIdx.x, s = sh / a.nh, h = sh % a.nh;
   const int qi = blockIdx.y * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (qi >= a.nq) return;
-  const int64_t bstride = (int64_t)a.nq * (2 + kHD);
-  const float* part = a.ws + (int64_t)sh * nblk * bstride + qi * (2 + kHD);
-  const float mv = lane < nblk ? part[lane * bstride] : -INFINITY;
-  const float lv = lane < nblk ? part[lane * bstride + 1] : 0.f;
-  const float M = warp_max(mv);
-  const float w = (mv == -INFINITY) ? 0.f : __expf(mv - M);
-  const float L = warp_sum(w * lv);
-  float o = 0.f;
-#pragma unroll 8
-  for (int b = 0; b < nblk; ++b) o = fmaf(__shfl(w, b, 64), part[b * bstride + 2 + lane], o);
-  io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
-  st_act(ob, lane, o / L);
+  combine_partials<IOBF, false>(a, blockIdx.x, qi, lane, nblk);
 }
 
 __global__ __launch_bounds__(256) void gather_window_kernel(const float* __restrict__ hist, int D,
@@ -351,14 +386,24 @@ void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes,
 
 int attn_decode_blocks(int max_keys) { return std::min(cdiv(max_keys, 256), 32); }
 
+template <bool IOBF, bool FUSED>
+static void launch_decode_q(const DecodeAttnArgs& a, dim3 g1, hipStream_t st) {
+  if (a.nq == 1) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 1, FUSED>), g1, dim3(256), 0, st, a);
+  else if (a.nq <= 8) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 8, FUSED>), g1, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_decode_kernel<IOBF, 32, FUSED>), g1, dim3(256), 0, st, a);
+  SD_LAUNCH_CHECK();
+}
+
 template <bool IOBF>
 static void launch_decode(const DecodeAttnArgs& a, int nblk, hipStream_t st) {
+  static const bool split = getenv("SDIAR_DECODE_SPLIT") != nullptr;   // A/B: the separate combine launch
   const int nsh = a.nseq * a.nh;
   const dim3 g1(nblk, nsh), g2(nsh, cdiv(a.nq, 4));
-  if (a.nq == 1) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 1>), g1, dim3(256), 0, st, a);
-  else if (a.nq <= 8) hipLaunchKernelGGL((attn_decode_kernel<IOBF, 8>), g1, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_decode_kernel<IOBF, 32>), g1, dim3(256), 0, st, a);
-  SD_LAUNCH_CHECK();
+  if (a.cnt && !split) {
+    launch_decode_q<IOBF, true>(a, g1, st);
+    return;
+  }
+  launch_decode_q<IOBF, false>(a, g1, st);
   hipLaunchKernelGGL(attn_combine_kernel<IOBF>, g2, dim3(256), 0, st, a, nblk);
   SD_LAUNCH_CHECK();
 }

@@ -291,8 +291,10 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     }
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
+    // SDIAR_LSTM_FP32 (diagnostic, tools/parity_stages.py): the exact-fp32 recurrence in bf16 mode too
+    static const bool lstm_fp32 = getenv("SDIAR_LSTM_FP32") != nullptr;
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
-                    nullptr, lstm_work_, st, lstm_hh_bf_, lstm_err_.get(0));
+                    nullptr, lstm_work_, st, lstm_fp32 ? nullptr : lstm_hh_bf_, lstm_err_.get(0));
     ConvGemmArgs f = cam_conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);

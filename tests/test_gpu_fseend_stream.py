@@ -248,3 +248,38 @@ def test_audio_stream_reset_modes_and_errors(gpu):
     s.set_audio()
     with pytest.raises(SdiarError, match="audio"):
         s._push_rows(f[:3])
+
+
+SPLIT = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+import tests.test_gpu_fseend_stream as t
+from tests.golden.make_golden import eda_inputs
+m = t._model(806, {prec!r}, max_frames=1100)
+x = torch.from_numpy(eda_inputs([1100], seed=86)[0]).cuda()
+out, _ = t._stream_all(m, x, 1)
+torch.save(out.cpu(), {path!r})
+"""
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_decode_attention_fused_combine_bit_identical(gpu, precision, tmp_path):
+    """attn_decode's last block merges the partials in the same launch (write-through partials + a
+    per-(sequence, head) counter) with the separate combine launch's arithmetic: the 1-frame-chunk stream
+    over 1100 frames (5 key blocks) is bit-identical with SDIAR_DECODE_SPLIT=1 (child processes: the switch is
+    read once) and, on the way, every counter stays a multiple of the block count across 2 x 1100 x 6 launches."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for split in (None, "1"):
+        env = dict(os.environ)
+        env.pop("SDIAR_DECODE_SPLIT", None)
+        if split:
+            env["SDIAR_DECODE_SPLIT"] = split
+        path = str(tmp_path / f"o_{split}.pt")
+        r = subprocess.run([sys.executable, "-c", SPLIT.format(repo=repo, prec=precision, path=path)], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(path, weights_only=True))
+    assert torch.equal(outs[0], outs[1])
