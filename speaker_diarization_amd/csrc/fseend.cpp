@@ -186,10 +186,9 @@ void FsEendModel::forward(const float* feats, int ld_in, int S, int T, const int
     const int len = lengths ? lengths[s] : T;
     SD_CHECK(len >= 1 && len <= T, kErrInvalid, "sequence length out of range");
     if (len < T) {
-      SD_HIP(hipMemsetAsync(X_ + ((int64_t)s * T + len) * D, 0, (size_t)(T - len) * D * sizeof(float), st));
+      zero_fill(X_ + ((int64_t)s * T + len) * D, (size_t)(T - len) * D * sizeof(float), st);
       if (bf)   // the encoder's last LayerNorm left bf16(X) in AO_: the conv reads that copy
-        SD_HIP(hipMemsetAsync(reinterpret_cast<uint16_t*>(AO_) + ((int64_t)s * T + len) * D, 0,
-                              (size_t)(T - len) * D * sizeof(uint16_t), st));
+        zero_fill(reinterpret_cast<uint16_t*>(AO_) + ((int64_t)s * T + len) * D, (size_t)(T - len) * D * sizeof(uint16_t), st);
     }
   }
   int ks = 1;

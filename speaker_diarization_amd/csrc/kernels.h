@@ -287,6 +287,10 @@ void tile_rows(const float* src, int src_rows, int D, float* dst, int dst_rows, 
 void mean_sigmoid_affine(const float* x, int rows, int T, int ldx, const float* w, const float* b, int N, float* out,
                          int ldo, hipStream_t st);
 
+// Stream-ordered zeroing of `bytes` (4-byte words) as a kernel: every forward uses it instead of
+// hipMemsetAsync so that a captured forward holds no memset node (ops.hip).
+void zero_fill(void* p, size_t bytes, hipStream_t st);
+
 // ---------------------------------------------------------------- ts-vad glue
 // BatchNorm1D + ReLU applied by the consumer of a conv output x = conv + bias (model.py:161-171, used at :255
 // and :393): v = relu(a[c] x + b[c]), or v = relu(x) for every window of a reference forward (a group of

@@ -573,7 +573,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
                "lstm: work buffer too small");
       uint16_t* hx = reinterpret_cast<uint16_t*>(work);
       unsigned* ctl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + hx_bytes);
-      SD_HIP(hipMemsetAsync(ctl, 0, ctl_bytes, st));
+      zero_fill(ctl, ctl_bytes, st);
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       prof.set_steps(T);   // sequential steps (an upper bound with packed lengths: the launch runs max(len))
@@ -596,9 +596,9 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
   float* hB = work + n;
   float* c = work + 2 * n;
   if (h0) SD_HIP(hipMemcpyAsync(hA, h0, n * 4, hipMemcpyDeviceToDevice, st));
-  else SD_HIP(hipMemsetAsync(hA, 0, n * 4, st));
+  else zero_fill(hA, n * 4, st);
   if (c0) SD_HIP(hipMemcpyAsync(c, c0, n * 4, hipMemcpyDeviceToDevice, st));
-  else SD_HIP(hipMemsetAsync(c, 0, n * 4, st));
+  else zero_fill(c, n * 4, st);
   const size_t smem = sizeof(float) * ((kBB + kRows) * (H + 4) + kBB * (kRows + 1));
   static bool attr_set = false;
   if (!attr_set) {

@@ -216,7 +216,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   int* win_ts = nonfinite_ + cfg_.max_batch;
   int* grp_sd = nonfinite_ + 2 * cfg_.max_batch;
   int* grp_bd = nonfinite_ + 3 * cfg_.max_batch;
-  SD_HIP(hipMemsetAsync(nonfinite_, 0, 4 * (size_t)cfg_.max_batch * sizeof(int), st));
+  zero_fill(nonfinite_, 4 * (size_t)cfg_.max_batch * sizeof(int), st);
   nonfinite_windows(ref, B, (int64_t)Tf * 80, G, win_fb, grp_sd, grp_bd, st);
   nonfinite_windows(ts, B, (int64_t)NS * SE, G, win_ts, nullptr, cfg_.variant == 0 ? grp_bd : nullptr, st);
   BnRelu sd_bn = down_bn_, bd_bn = backend_bn_;

@@ -52,7 +52,8 @@ for name, (v, rs, B, T, nl, iseed, wseed) in TSVAD_CASES.items():
     x, ts = tsvad_inputs(B, T, nl, seed=iseed)
     for rep in range(2):      # a repeated call reuses the handle's workspaces
         out = m.forward(torch.from_numpy(x).to(dev), torch.from_numpy(ts).to(dev), nl).cpu().numpy()
-    res["tsvad/" + name] = (float(np.abs(out - np.load(os.path.join(G, name + ".npz"))["logits"]).max()), 2e-2)
+    # the main test's bf16 bound (test_gpu_tsvad.py BF16_ATOL): every switch setting is held to it
+    res["tsvad/" + name] = (float(np.abs(out - np.load(os.path.join(G, name + ".npz"))["logits"]).max()), 1.5e-2)
 def fse(delay, wseed, T=512):
     m = OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, conv_delay=9,
                                        mask_delay=delay, precision="bf16", max_seqs=2, max_frames=T, max_nspks=6)

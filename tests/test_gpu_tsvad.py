@@ -127,9 +127,9 @@ def test_pipeline_vs_oracle(gpu, variant, precision):
     err = np.abs(post[:3] - ref[:3]).max()
     print(f"pipeline v{variant} {precision}: max|post diff| = {err:.3e}")
     # posterior level (the bf16 product path measured 1.2e-3 / 1.4e-3 on MI355X for v1 / v0): 1e-3 fp32
-    # (north_star), 5e-3 bf16; and the recipe's threshold decisions (ts_vad2/infer.py thresholds) agree on
-    # >= 99 % of the frames at every threshold
-    assert err < (1e-3 if precision == "fp32" else 5e-3)
+    # (north_star), 3e-3 bf16 (about 2x measured); and the recipe's threshold decisions (ts_vad2/infer.py
+    # thresholds) agree on >= 99 % of the frames at every threshold
+    assert err < (1e-3 if precision == "fp32" else 3e-3)
     for thr in (0.2, 0.3, 0.35, 0.4, 0.45, 0.5, 0.55, 0.6, 0.7, 0.8):
         flips = int(((post[:3] > thr) != (ref[:3] > thr)).sum())
         assert flips <= 0.01 * post[:3].size, (thr, flips)
