@@ -198,6 +198,8 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
     if (i == 0) {
       fu.fbank = ref; fu.fb_F = F;
       fu.stem_w = fcm_conv1_.pre_s; fu.stem_alpha = fcm_conv1_.alpha; fu.stem_beta = fcm_conv1_.beta;
+      static const bool stem_valu = getenv("SDIAR_FCM_STEM_VALU") != nullptr;   // A/B switch: fp32 fmaf stem
+      fu.stem_mfma = stem_valu ? 0 : 1;
     }
     const bool fused = bf && !no_fused_ && rb.has_sc && rb.sc.w.N == 32 && rb.sc.w.K == 32 && fcm_fused_supported(p, fu);
     if (i == 0 && !fused) {

@@ -200,7 +200,7 @@ __host__ __device__ inline int band_channel(int i, int nt) { return 8 * (i >> 2)
 constexpr int kToutBlk = 4;
 constexpr int kToutRow = 328;   // LDS frame-row stride in bf16 (656 B: 16-B aligned, rows 36 banks apart)
 
-template <int R, int SH, bool STEM = false, bool SC = false, bool TOUT = false>
+template <int R, int SH, bool STEM = false, bool SC = false, bool TOUT = false, bool SMF = false>
 __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, FcmFuse f, int n_bands,
                                                                        int n_blk) {
   // A band: (image b, R output rows from ho0, time tile tt of n_blk 16-frame blocks).
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       for (int nt = 0; nt < 2; ++nt)
         wf[t][nt] = *reinterpret_cast<const bf16x8*>(Wt + band_channel(l15, nt) * 288 + t * 32 + q * 8);
   };
-  if constexpr (!STEM) load_wf(reinterpret_cast<const uint16_t*>(p.Wt));
+  if constexpr (!STEM || SMF) load_wf(reinterpret_cast<const uint16_t*>(p.Wt));
   bf16x8 wsc[2];
   float sal[2][4], sbe[2][4];
   if constexpr (SC) {
@@ -292,12 +292,37 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
   const int fb_n = (NR + 2) * (Wp + 2);
   constexpr int kFbPer = 5;   // fbank tile floats per thread (<= 2560)
   float s_al[8], s_be[8];
+  // MFMA stem (f.stem_mfma): v_mfma_f32_32x32x16_bf16 with the 32 channels as rows and 32 staged pixels as
+  // columns; k = the 9 taps (dh, dw) in order, then beta's bf16 hi and lo parts against a constant 1 (BN
+  // folded: A = bf16(alpha_c * w_c), so a pixel is relu(sum + beta) with no epilogue FMAs).  A row m is
+  // channel 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3), so accumulator i of lane half h is channel 16 h + i
+  // and a lane stores its pixel's 16 contiguous channels as two 16-B LDS writes.
+  bf16x8 stem_a;
   if constexpr (STEM) {
-    const int c0 = (tid & 3) * 8;
+    if constexpr (SMF) {
+      const int m = lane & 31, h = lane >> 5;
+      const int c = 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3);
+      const float al = f.stem_alpha[c], be = f.stem_beta[c];
+      float e[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s_al[u] = f.stem_alpha[c0 + u];
-      s_be[u] = f.stem_beta[c0 + u];
+      for (int j = 0; j < 8; ++j) e[j] = al * f.stem_w[c * 9 + min(8 * h + j, 8)];
+      const float bh = __uint_as_float(f2bf_bits(be) << 16);
+      if (h) {
+        e[1] = bh;
+        e[2] = __uint_as_float(f2bf_bits(be - bh) << 16);
+#pragma unroll
+        for (int j = 3; j < 8; ++j) e[j] = 0.f;
+      }
+      const uint32_t w4[4] = {pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]), pack_bf16x2(e[4], e[5]),
+                              pack_bf16x2(e[6], e[7])};
+      stem_a = *reinterpret_cast<const bf16x8*>(w4);
+    } else {
+      const int c0 = (tid & 3) * 8;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s_al[u] = f.stem_alpha[c0 + u];
+        s_be[u] = f.stem_beta[c0 + u];
+      }
     }
   }
   // fbank value (bin hb - 1 + j, frame w0 - 1 + x) of a band, j < NR + 2, x < Wp + 2; zero outside the map
@@ -331,12 +356,45 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
         const int x = i / (NR + 2), j = i - x * (NR + 2);
         if (i < fb_n) fbs[j * (Wp + 2) + x] = fv[k];   // LDS tile [bin][frame]
       }
-      __syncthreads();
+      if constexpr (SMF) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else __syncthreads();
       const int next = band + gridDim.x;
       if (next < n_bands) load_fb(next, fv);
       // stem: staged pixel (rr, px) = conv1 row hb + rr, frame w0 + px; zero outside (next conv's padding)
       const int tt = band % n_tt, bh = band / n_tt;
       const int hb = (bh % n_rb) * R * SH - 1, w0 = tt * n_blk * 16 - 1;
+      if constexpr (SMF) {
+        const int n = lane & 31, h = lane >> 5;
+        const int ngr = (Wp + 31) >> 5;   // 32-pixel groups per staged row (reads past Wp hit the tile's pad)
+        for (int g = wv; g < NR * ngr; g += kBandThreads / 64) {
+          const int rr = g / ngr, px = (g - rr * ngr) * 32 + n;
+          const float* t0 = fbs + rr * (Wp + 2) + px;
+          float tp[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) tp[k] = t0[(k / 3) * (Wp + 2) + k % 3];
+          float e[8];
+          e[0] = h ? tp[8] : tp[0];
+          e[1] = h ? 1.f : tp[1];
+          e[2] = h ? 1.f : tp[2];
+#pragma unroll
+          for (int j = 3; j < 8; ++j) e[j] = h ? 0.f : tp[j];
+          const uint32_t b4[4] = {pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]), pack_bf16x2(e[4], e[5]),
+                                  pack_bf16x2(e[6], e[7])};
+          typedef float floatx16 __attribute__((ext_vector_type(16)));
+          floatx16 acc = {};
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(stem_a, *reinterpret_cast<const bf16x8*>(b4), acc, 0, 0, 0);
+          if (px < Wp) {
+            const bool ok = (unsigned)(hb + rr) < (unsigned)p.H && (unsigned)(w0 + px) < (unsigned)W;
+            uint32_t o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              o[u] = ok ? pack_bf16x2(fmaxf(acc[2 * u], 0.f), fmaxf(acc[2 * u + 1], 0.f)) : 0u;
+            uint16_t* dst = xs + (rr * Wp + px) * kPS + 16 * h;
+            *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<uint4*>(dst + 8) = make_uint4(o[4], o[5], o[6], o[7]);
+          }
+        }
+      } else {
       const float* swb = f.stem_w;
       asm volatile("" : "+s"(swb));
       const float* swp = swb + (tid & 3) * 72;
@@ -396,7 +454,11 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       const uint16_t* wtp = reinterpret_cast<const uint16_t*>(p.Wt);
       asm volatile("" : "+s"(wtp));
       load_wf(wtp);
-      __syncthreads();
+      }
+      // SMF: LDS-only barriers (a __syncthreads() fence would also drain the next band's fbank prefetch
+      // and this band's output stores)
+      if constexpr (SMF) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else __syncthreads();
     } else {
 #pragma unroll
       for (int k = 0; k < kVP; ++k) {
@@ -497,7 +559,8 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
             *reinterpret_cast<const uint4*>(so + fr * kToutRow + ck * 8);
       }
     }
-    __syncthreads();   // xs free for the next band
+    if constexpr (SMF) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // xs free
+    else __syncthreads();   // xs free for the next band
   }
 }
 
@@ -692,7 +755,8 @@ inline int band_blocks(int W) {
 template <int R, int SH, bool STEM = false>
 size_t band_lds(int n_blk) {
   constexpr int nr = (R - 1) * SH + 3;
-  const size_t fb = STEM ? (size_t)(nr + 2) * (n_blk * 16 + 4) * 4 : 0;
+  // STEM: fbank tile + 32 floats of pad (the MFMA stem's last 32-pixel group reads up to 31 past the tile)
+  const size_t fb = STEM ? (size_t)(nr + 2) * (n_blk * 16 + 4) * 4 + 128 : 0;
   return (size_t)nr * (n_blk * 16 + 2) * kPS * 2 + fb;
 }
 
@@ -708,20 +772,20 @@ bool band_fits(const ConvGemmArgs& p) {
          (!p.res || (p.res_ld % 8 == 0)) && (p.o_sn != 1 || p.o_sw % 8 == 0);
 }
 
-template <int R, int SH, bool STEM = false, bool SC = false>
+template <int R, int SH, bool STEM = false, bool SC = false, bool SMF = false>
 void launch_band(const ConvGemmArgs& p, hipStream_t st, const FcmFuse& f = FcmFuse{}) {
   const int nb = band_blocks(p.W);
   const int64_t bands = (int64_t)p.B * cdiv(p.Ho, R) * cdiv(p.W, nb * 16);
   SD_CHECK(bands < (1ll << 31), kErrInvalid, "fcm conv: too many bands");
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, SH, STEM, SC>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, SH, STEM, SC, false, SMF>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
   const size_t smem = band_lds<R, SH, STEM>(nb);
-  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, SH, STEM, SC>), dim3(grid), dim3(kBandThreads), smem, st, p, f,
+  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, SH, STEM, SC, false, SMF>), dim3(grid), dim3(kBandThreads), smem, st, p, f,
                      (int)bands, nb);
 }
 
@@ -826,8 +890,8 @@ void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st) 
   if (f.fbank) flops += 2.0 * (double)p.B * p.H * p.W * 32 * 9;
   const double bytes = in_px * 64 + (f.fbank ? 4.0 * p.B * p.W * f.fb_F : 0.0) + px * 64 * (f.sc_w ? 2 : 1);
   ProfScope prof(f.fbank ? "fcm_stem" : "fcm_conv3x3_band", flops, bytes, st);
-  if (f.fbank && f.sc_w) launch_band<2, 2, true, true>(p, st, f);
-  else if (f.fbank) launch_band<2, 2, true, false>(p, st, f);
+  if (f.fbank && f.sc_w) f.stem_mfma ? launch_band<2, 2, true, true, true>(p, st, f) : launch_band<2, 2, true, true>(p, st, f);
+  else if (f.fbank) f.stem_mfma ? launch_band<2, 2, true, false, true>(p, st, f) : launch_band<2, 2, true, false>(p, st, f);
   else if (f.sc_w) launch_band<2, 2, false, true>(p, st, f);
   else launch_band<2, 2>(p, st);
   SD_LAUNCH_CHECK();

@@ -84,6 +84,7 @@ struct FcmFuse {
   const float* fbank = nullptr;               // (B, W, fb_F) fp32
   int fb_F = 0;
   const float *stem_w = nullptr, *stem_alpha = nullptr, *stem_beta = nullptr;   // 32x9 raw, folded BN
+  int stem_mfma = 0;   // 1: the stem as one bf16 32x32x16 MFMA per 32 pixels (BN folded); 0: the fp32 fmaf chain
 };
 bool fcm_fused_supported(const ConvGemmArgs& p, const FcmFuse& f);
 void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st);
@@ -480,6 +481,58 @@ struct DecodeAttnArgs {
   unsigned* cnt = nullptr;
 };
 int attn_decode_blocks(int max_keys);
+// FS-EEND streaming decoder, slot-attention sub-block of the fusion layer (fs_eend.py:468-471) for one chunk:
+//   y = LN(x + t) (-> ln_out, the next residual);  qkv = y W_inᵀ + b_in;  o = softmax(q kᵀ scale) v across the
+//   C slots of each frame, per head;  out = o W_outᵀ + b_out.
+// ONE launch of nh workgroups (one per head): a head's q/k/v and attention stay in LDS, its out-projection
+// partial (the head's 64 input features) is published write-through and the last workgroup to count itself
+// sums the nh partials in head order (MI355X guide hand-off row 1; cnt monotonic, zeroed once).
+// Supported: D == 256, D / nh == 64, c * C <= 16, C <= 8; returns false otherwise (caller runs the three-launch
+// path).
+struct SlotBlockArgs {
+  const float* ln_x = nullptr;
+  const void* ln_t = nullptr;
+  bool t_bf16 = false;
+  const float *ln_g = nullptr, *ln_b = nullptr;
+  float eps = 1e-5f;
+  float* ln_out = nullptr;
+  const void* w_in = nullptr;   // packed [3D][D]
+  const float* b_in = nullptr;
+  const void* w_out = nullptr;  // packed [D][D]
+  const float* b_out = nullptr;
+  bool w_bf16 = false;
+  void* out = nullptr;          // (c*C, D), bf16 when out_bf16
+  bool out_bf16 = false;
+  float* ws = nullptr;          // nh * c*C * D floats
+  unsigned* cnt = nullptr;
+  int c = 1, C = 1, D = 256, nh = 4;
+  float scale = 0.125f;
+};
+bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st);
+// FS-EEND streaming feed-forward sub-block for a chunk's n rows: y = LN(x + t) (-> ln_out); out = relu(y W1ᵀ + b1)
+// W2ᵀ + b2.  ONE launch of H / 128 workgroups: workgroup g owns hidden units [128 g, 128 g + 128) (the hidden
+// layer never leaves LDS) and publishes its down-projection partial write-through; the last workgroup to count
+// itself sums the partials in workgroup order (MI355X guide hand-off row 1).  Supported: D == 256,
+// H % 128 == 0, H <= 4096, n <= 8; returns false otherwise.
+struct StreamFfnArgs {
+  const float* ln_x = nullptr;
+  const void* ln_t = nullptr;
+  bool t_bf16 = false;
+  const float *ln_g = nullptr, *ln_b = nullptr;
+  float eps = 1e-5f;
+  float* ln_out = nullptr;
+  const void* w1 = nullptr;     // packed [H][D]
+  const float* b1 = nullptr;
+  const void* w2 = nullptr;     // packed [D][H]
+  const float* b2 = nullptr;
+  bool w_bf16 = false;
+  void* out = nullptr;          // (n, D)
+  bool out_bf16 = false;
+  float* ws = nullptr;          // (H / 128) * n * D floats
+  unsigned* cnt = nullptr;
+  int n = 1, D = 256, H = 2048;
+};
+bool stream_ffn(const StreamFfnArgs& a, hipStream_t st);
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,

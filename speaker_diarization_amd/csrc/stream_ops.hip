@@ -359,6 +359,247 @@ __global__ __launch_bounds__(256) void dec_finish_kernel(const float* __restrict
   if (lane == 0) scores[r] = dot / sqrtf(sq);
 }
 
+// Weight rows as 16-B vectors: 8 bf16 or 4 fp32 values per vector.  Every fused stream kernel below issues a
+// thread's whole weight slice as one batch before it needs any of it (one memory latency per slice, not one
+// per vector).
+template <bool WBF>
+struct WVec {
+  static constexpr int VE = WBF ? 8 : 4;
+  __device__ __forceinline__ static uint4 load(const void* w, int64_t elem) {
+    if constexpr (WBF) return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(w) + elem);
+    else return *reinterpret_cast<const uint4*>(static_cast<const float*>(w) + elem);
+  }
+  __device__ __forceinline__ static float at(const uint4& u, int e) {
+    const uint32_t w = e < (WBF ? 2 : 1) ? u.x : e < (WBF ? 4 : 2) ? u.y : e < (WBF ? 6 : 3) ? u.z : u.w;
+    if constexpr (WBF) return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+    else return __uint_as_float(w);
+  }
+};
+
+// stream_slot_block (kernels.h).  grid nh, 512 threads; workgroup h = head h.
+constexpr int kSlotRows = 16, kSlotD = 256;
+template <bool WBF>
+__global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
+  using V = WVec<WBF>;
+  constexpr int D = kSlotD, VE = V::VE;
+  constexpr int NIN = D / 2 / VE;    // vectors of a half in-projection row
+  constexpr int NOUT = kHD / VE;     // vectors of the head's slice of an out-projection row
+  __shared__ float ys[kSlotRows][D];
+  __shared__ float qs[kSlotRows][kHD], ks[kSlotRows][kHD], vs[kSlotRows][kHD], os[kSlotRows][kHD];
+  __shared__ float sc[kSlotRows][8];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = blockIdx.x, n = a.c * a.C, C = a.C;
+  // thread t < 384: in-projection row (t / 2 / 64) * D + h * 64 + (t / 2) % 64, K half t % 2;
+  // thread t < 256: out-projection row t, the head's 64 inputs
+  // (unconditional, clamped loads: arrays filled under a branch end up in scratch)
+  const int r2 = min(tid, 6 * kHD - 1) >> 1, kh = tid & 1, sel = r2 / kHD, d2 = r2 % kHD;
+  const int64_t rin = ((int64_t)sel * D + h * kHD + d2) * D + kh * (D / 2);
+  const int64_t rout = (int64_t)(tid & (D - 1)) * D + h * kHD;
+  uint4 win[NIN], wout[NOUT];
+#pragma unroll
+  for (int v = 0; v < NIN; ++v) win[v] = V::load(a.w_in, rin + v * VE);
+#pragma unroll
+  for (int v = 0; v < NOUT; ++v) wout[v] = V::load(a.w_out, rout + v * VE);
+  // y = LN(x + t): one wave per row (every workgroup; workgroup 0 stores the residual stream)
+  for (int r = wid; r < n; r += 8) {
+    float4 y[4];
+    ln_row(a.ln_x + (int64_t)r * D, a.ln_t, a.t_bf16, (int64_t)r * D, a.ln_g, a.ln_b, a.eps, D, lane, y);
+    *reinterpret_cast<float4*>(&ys[r][lane * 4]) = y[0];
+    if (h == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
+  }
+  __syncthreads();
+  {
+    const float b = a.b_in[(int64_t)sel * D + h * kHD + d2];
+    float(*dst)[kHD] = sel == 0 ? qs : sel == 1 ? ks : vs;
+    const float mul = sel == 0 ? a.scale : 1.f;
+    for (int m = 0; m < n; ++m) {   // every lane takes part (the K-half shuffle), threads >= 384 store nothing
+      const float* yr = &ys[m][kh * (D / 2)];
+      float acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NIN; ++v) {
+        float yv[VE];
+#pragma unroll
+        for (int e = 0; e < VE; e += 4) {
+          const float4 q = *reinterpret_cast<const float4*>(yr + v * VE + e);
+          yv[e] = q.x; yv[e + 1] = q.y; yv[e + 2] = q.z; yv[e + 3] = q.w;
+        }
+#pragma unroll
+        for (int e = 0; e < VE; ++e) acc = fmaf(V::at(win[v], e), yv[e], acc);
+      }
+      const float t = acc + __shfl_xor(acc, 1, 64);   // the two K halves
+      if (tid < 6 * kHD && kh == 0) dst[m][d2] = (t + b) * mul;
+    }
+  }
+  __syncthreads();
+  // scores of row m = f * C + i against the C slots of frame f, softmax per row
+  for (int t = tid; t < n * C; t += 512) {
+    const int m = t / C, j = t % C, kr = (m / C) * C + j;
+    float s = 0.f;
+#pragma unroll 16
+    for (int d = 0; d < kHD; ++d) s = fmaf(qs[m][d], ks[kr][d], s);
+    sc[m][j] = s;
+  }
+  __syncthreads();
+  if (tid < n) {
+    float mx = -INFINITY;
+    for (int j = 0; j < C; ++j) mx = fmaxf(mx, sc[tid][j]);
+    float l = 0.f;
+    for (int j = 0; j < C; ++j) {
+      const float e = __expf(sc[tid][j] - mx);
+      sc[tid][j] = e;
+      l += e;
+    }
+    const float inv = 1.f / l;
+    for (int j = 0; j < C; ++j) sc[tid][j] *= inv;
+  }
+  __syncthreads();
+  for (int t = tid; t < n * kHD; t += 512) {
+    const int m = t / kHD, d = t % kHD, f0 = (m / C) * C;
+    float o = 0.f;
+    for (int j = 0; j < C; ++j) o = fmaf(sc[m][j], vs[f0 + j][d], o);
+    os[m][d] = o;
+  }
+  __syncthreads();
+  // out-projection partial of head h for output feature tid, published write-through
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
+  if (tid < D) {
+    for (int m = 0; m < n; ++m) {
+      float p = 0.f;
+#pragma unroll
+      for (int v = 0; v < NOUT; ++v)
+#pragma unroll
+        for (int e = 0; e < VE; ++e) p = fmaf(os[m][v * VE + e], V::at(wout[v], e), p);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p), rw, (uint32_t)((((int64_t)h * n + m) * D + tid) * 4),
+                                            0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned nh = gridDim.x;
+    last = (__hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % nh) == nh - 1;
+  }
+  __syncthreads();
+  if (!last || tid >= D) return;
+  const float bo = a.b_out[tid];
+  const int nh = gridDim.x;
+  for (int m = 0; m < n; ++m) {
+    float pv[8];
+#pragma unroll
+    for (int hh = 0; hh < 8; ++hh)   // nh <= 8 (D / 64 with D = 256: 4); all loads issued before the sum
+      pv[hh] = hh < nh ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                             rw, (uint32_t)((((int64_t)hh * n + m) * D + tid) * 4), 0, 16))
+                       : 0.f;
+    float v = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 8; ++hh)
+      if (hh < nh) v += pv[hh];
+    v += bo;
+    if (a.out_bf16) static_cast<uint16_t*>(a.out)[(int64_t)m * D + tid] = f2bf_bits(v);
+    else static_cast<float*>(a.out)[(int64_t)m * D + tid] = v;
+  }
+}
+
+// stream_ffn (kernels.h).  grid H / 128, 256 threads.
+constexpr int kFfnRows = 8, kFfnHid = 128, kFfnMaxG = 32;
+template <bool WBF>
+__global__ __launch_bounds__(256) void stream_ffn_kernel(StreamFfnArgs a) {
+  using V = WVec<WBF>;
+  constexpr int D = kSlotD, VE = V::VE;
+  constexpr int N1 = D / 2 / VE;       // vectors of this thread's half up-projection row
+  constexpr int N2 = kFfnHid / VE;     // vectors of its down-projection row slice
+  __shared__ float ys[kFfnRows][D];
+  __shared__ float hs[kFfnRows][kFfnHid];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = blockIdx.x, n = a.n, H = a.H;
+  const int j = tid >> 1, kh = tid & 1;
+  const int64_t r1 = (int64_t)(g * kFfnHid + j) * D + kh * (D / 2);
+  const int64_t r2 = (int64_t)tid * H + g * kFfnHid;
+  uint4 w1[N1], w2[N2];
+#pragma unroll
+  for (int v = 0; v < N1; ++v) w1[v] = V::load(a.w1, r1 + v * VE);
+  if constexpr (WBF) {   // bf16: both slices in flight at once (fp32: the down slice after the up product)
+#pragma unroll
+    for (int v = 0; v < N2; ++v) w2[v] = V::load(a.w2, r2 + v * VE);
+  }
+  for (int r = wid; r < n; r += 4) {
+    float4 y[4];
+    ln_row(a.ln_x + (int64_t)r * D, a.ln_t, a.t_bf16, (int64_t)r * D, a.ln_g, a.ln_b, a.eps, D, lane, y);
+    *reinterpret_cast<float4*>(&ys[r][lane * 4]) = y[0];
+    if (g == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
+  }
+  __syncthreads();
+  {
+    const float bj = a.b1[g * kFfnHid + j];
+    for (int m = 0; m < n; ++m) {
+      const float* yr = &ys[m][kh * (D / 2)];
+      float acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < N1; ++v) {
+        float yv[VE];
+#pragma unroll
+        for (int e = 0; e < VE; e += 4) {
+          const float4 q = *reinterpret_cast<const float4*>(yr + v * VE + e);
+          yv[e] = q.x; yv[e + 1] = q.y; yv[e + 2] = q.z; yv[e + 3] = q.w;
+        }
+#pragma unroll
+        for (int e = 0; e < VE; ++e) acc = fmaf(V::at(w1[v], e), yv[e], acc);
+      }
+      const float t = acc + __shfl_xor(acc, 1, 64);
+      if (kh == 0) hs[m][j] = fmaxf(t + bj, 0.f);
+    }
+  }
+  if constexpr (!WBF) {
+#pragma unroll
+    for (int v = 0; v < N2; ++v) w2[v] = V::load(a.w2, r2 + v * VE);
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
+  for (int m = 0; m < n; ++m) {
+    float p = 0.f;
+#pragma unroll
+    for (int v = 0; v < N2; ++v) {
+      float hv[VE];
+#pragma unroll
+      for (int e = 0; e < VE; e += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(&hs[m][v * VE + e]);
+        hv[e] = q.x; hv[e + 1] = q.y; hv[e + 2] = q.z; hv[e + 3] = q.w;
+      }
+#pragma unroll
+      for (int e = 0; e < VE; ++e) p = fmaf(V::at(w2[v], e), hv[e], p);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p), rw, (uint32_t)((((int64_t)g * n + m) * D + tid) * 4), 0,
+                                          16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned G = gridDim.x;
+    last = (__hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % G) == G - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  const float bo = a.b2[tid];
+  const int G = gridDim.x;
+  for (int m = 0; m < n; ++m) {
+    float pv[kFfnMaxG];
+#pragma unroll
+    for (int gg = 0; gg < kFfnMaxG; ++gg)   // all partial loads issued before the ordered sum
+      pv[gg] = gg < G ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                            rw, (uint32_t)((((int64_t)gg * n + m) * D + tid) * 4), 0, 16))
+                      : 0.f;
+    float v = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < kFfnMaxG; ++gg)
+      if (gg < G) v += pv[gg];
+    v += bo;
+    if (a.out_bf16) static_cast<uint16_t*>(a.out)[(int64_t)m * D + tid] = f2bf_bits(v);
+    else static_cast<float*>(a.out)[(int64_t)m * D + tid] = v;
+  }
+}
+
 __global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
   if (threadIdx.x == 0) {
     const int v = *cursor + by;
@@ -419,6 +660,33 @@ void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
                  2.0 * a.max_keys * kHD * nsh * (a.io_bf16 ? 2 : 4), st);
   if (a.io_bf16) launch_decode<true>(a, nblk, st);
   else launch_decode<false>(a, nblk, st);
+}
+
+bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st) {
+  // opt-in until it measures faster than the three launches (SDIAR_STREAM_FUSE=1)
+  static const bool off = getenv("SDIAR_STREAM_FUSE") == nullptr || getenv("SDIAR_NO_SLOT_BLOCK") != nullptr;
+  const int n = a.c * a.C;
+  if (off || a.D != kSlotD || a.nh * kHD != a.D || a.nh > 8 || n < 1 || n > kSlotRows || a.C > 8 || !a.ws || !a.cnt)
+    return false;
+  ProfScope prof("slot_block", 2.0 * n * a.D * 4.0 * a.D + 4.0 * n * a.C * a.D, (a.w_bf16 ? 2.0 : 4.0) * 4 * a.D * a.D, st);
+  if (a.w_bf16) hipLaunchKernelGGL(slot_block_kernel<true>, dim3(a.nh), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(slot_block_kernel<false>, dim3(a.nh), dim3(512), 0, st, a);
+  SD_LAUNCH_CHECK();
+  return true;
+}
+
+bool stream_ffn(const StreamFfnArgs& a, hipStream_t st) {
+  // opt-in until it measures faster than the two launches (SDIAR_STREAM_FUSE=1)
+  static const bool off = getenv("SDIAR_STREAM_FUSE") == nullptr || getenv("SDIAR_NO_STREAM_FFN") != nullptr;
+  if (off || a.D != kSlotD || a.H % kFfnHid != 0 || a.H > kFfnMaxG * kFfnHid || a.n < 1 || a.n > kFfnRows || !a.ws ||
+      !a.cnt)
+    return false;
+  ProfScope prof("stream_ffn", 4.0 * a.n * a.D * (double)a.H, (a.w_bf16 ? 2.0 : 4.0) * 2 * a.D * (double)a.H, st);
+  const dim3 grid(a.H / kFfnHid);
+  if (a.w_bf16) hipLaunchKernelGGL(stream_ffn_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(stream_ffn_kernel<false>, grid, dim3(256), 0, st, a);
+  SD_LAUNCH_CHECK();
+  return true;
 }
 
 void gather_window(const float* hist, int D, const int* cursor, const int* n_valid, int pad, int rows, float* dst,

@@ -22,8 +22,9 @@ GROUPS = {
     "rowprog_off+tiny_off+hpw2+splitk_off+camdense_off": {"SDIAR_NO_ROWPROG": "1", "SDIAR_NO_ATTN_TINY": "1",
                                                           "SDIAR_ATTN_HPW": "2", "SDIAR_NO_SPLITK": "1",
                                                           "SDIAR_NO_CAM_DENSE": "1"},
-    "mha_off+long_off+camfused_off+dwpk_off": {"SDIAR_NO_MHA_BLOCK": "1", "SDIAR_NO_ATTN_LONG": "1",
-                                               "SDIAR_NO_CAM_FUSED": "1", "SDIAR_NO_DWCONV_PK": "1"},
+    "mha_off+long_off+camfused_off+dwpk_off+stemvalu": {"SDIAR_NO_MHA_BLOCK": "1", "SDIAR_NO_ATTN_LONG": "1",
+                                                        "SDIAR_NO_CAM_FUSED": "1", "SDIAR_NO_DWCONV_PK": "1",
+                                                        "SDIAR_FCM_STEM_VALU": "1"},
     "fcmband_off+areg_off+ringpersist_off+xremap_off": {
         "SDIAR_NO_FCM_BAND": "1", "SDIAR_NO_AREG_GEMM": "1", "SDIAR_NO_RING_PERSIST": "1",
         "SDIAR_ATTN_NO_XREMAP": "1", "SDIAR_RP_STAGGER": "0"},

@@ -12,7 +12,7 @@ for i in $(seq 1 "$R"); do
     python3 - "$V=$val" "$out" <<'PY'
 import json, sys
 d = json.loads([x for x in open(sys.argv[2]) if x.startswith("{")][-1])
-top = sorted(d.get("kernels", {}).items(), key=lambda kv: -kv[1]["ms"])[:6]
+top = sorted(d.get("kernels", {}).items(), key=lambda kv: -kv[1]["ms"])[:12]
 print(sys.argv[1], d["ms_per_step"], " ".join(f"{k}={v['ms']:.3f}" for k, v in top), flush=True)
 PY
   done
