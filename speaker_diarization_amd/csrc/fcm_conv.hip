@@ -197,6 +197,8 @@ __host__ __device__ inline int band_channel(int i, int nt) { return 8 * (i >> 2)
 // 640-B frame rows.  The epilogue scatters into an LDS image of those rows and the band leaves as 16-B
 // stores (per-element stores of R-row bands left every frame row to be assembled from 2-B pieces by
 // five different bands).
+// SMF: the band barriers are LDS-only (`lgkmcnt(0)` + `s_barrier`): a __syncthreads() fence also waits for the
+// next band's prefetch and this band's output stores; with STEM also the MFMA stem (see the stem block below).
 constexpr int kToutBlk = 4;
 constexpr int kToutRow = 328;   // LDS frame-row stride in bf16 (656 B: 16-B aligned, rows 36 banks apart)
 
@@ -465,7 +467,8 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
         const int i = tid + k * kBandThreads;
         if (i < n_vec) *reinterpret_cast<uint4*>(xs + (i >> 2) * kPS + (i & 3) * 8) = hv[k];
       }
-      __syncthreads();
+      if constexpr (SMF) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else __syncthreads();
       const int next = band + gridDim.x;
       if (next < n_bands) load_band(next, hv);   // in flight while this band computes
     }
@@ -549,7 +552,8 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       }
     }
     if constexpr (TOUT) {   // the band's frame rows are contiguous in the output: 16-B copies
-      __syncthreads();
+      if constexpr (SMF) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else __syncthreads();
       const int nfr = min(n_blk * 16, p.Wo - wo0), cpr = R * 4;
       uint16_t* ob = reinterpret_cast<uint16_t*>(p.out) + ((int64_t)b * p.Wo + wo0) * 32 * R;
       const uint16_t* so = xs + NR * Wp * kPS;
@@ -808,12 +812,12 @@ void launch_tout(const ConvGemmArgs& p, hipStream_t st) {
                 "LDS budget");
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, 2, false, false, true>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fcm_conv3x3_band_kernel<R, 2, false, false, true, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     attr = true;
   }
   const int grid = (int)std::min<int64_t>(bands, (int64_t)g_fcm_cu);
-  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, 2, false, false, true>), dim3(grid), dim3(kBandThreads), smem, st,
+  hipLaunchKernelGGL((fcm_conv3x3_band_kernel<R, 2, false, false, true, true>), dim3(grid), dim3(kBandThreads), smem, st,
                      p, FcmFuse{}, (int)bands, kToutBlk);
 }
 
@@ -892,7 +896,7 @@ void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st) 
   ProfScope prof(f.fbank ? "fcm_stem" : "fcm_conv3x3_band", flops, bytes, st);
   if (f.fbank && f.sc_w) f.stem_mfma ? launch_band<2, 2, true, true, true>(p, st, f) : launch_band<2, 2, true, true>(p, st, f);
   else if (f.fbank) f.stem_mfma ? launch_band<2, 2, true, false, true>(p, st, f) : launch_band<2, 2, true, false>(p, st, f);
-  else if (f.sc_w) launch_band<2, 2, false, true>(p, st, f);
+  else if (f.sc_w) launch_band<2, 2, false, true, true>(p, st, f);
   else launch_band<2, 2>(p, st);
   SD_LAUNCH_CHECK();
 }

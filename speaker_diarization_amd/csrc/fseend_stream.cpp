@@ -52,9 +52,6 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
   sws_ = wsb<float>((size_t)cfg.n_heads * rd * D);
   scnt_ = wsb<unsigned>(1);
   SD_HIP(hipMemset(scnt_, 0, sizeof(unsigned)));
-  fws_ = wsb<float>((size_t)cdiv(ffn, 128) * std::min<int64_t>(rd, 8) * D);
-  fcnt_ = wsb<unsigned>(2);
-  SD_HIP(hipMemset(fcnt_, 0, 2 * sizeof(unsigned)));
   for (int l = 0; l < cfg.enc_n_layers; ++l) kv_enc_.push_back(arena_.alloc((size_t)cap_ * 2 * D * es_));
   for (int a = 0; a < cfg.dec_n_layers; ++a) kv_dec_.push_back(arena_.alloc((size_t)cap_ * C_ * 2 * D * es_));
   hist_ = wsb<float>((size_t)cap_ * D);
@@ -120,18 +117,6 @@ void gemm_fused(ConvGemmArgs p, const PendingLn* ln, const KvEpi* kv, int D, boo
   }
 }
 
-// The feed-forward sub-block as one launch (stream_ffn) when it applies: y = LN(pending) becomes ln.out, the
-// FFN output lands in `t_out` for the next LayerNorm.
-bool ffn_fused(const PendingLn& ln, const PackedW& w1, const float* b1, const PackedW& w2, const float* b2, int rows,
-               int D, bool bf, void* t_out, float* ws, unsigned* cnt, hipStream_t st) {
-  StreamFfnArgs f;
-  f.ln_x = ln.x; f.ln_t = ln.t; f.t_bf16 = bf; f.ln_g = ln.g; f.ln_b = ln.b; f.ln_out = ln.out;
-  f.w1 = w1.w; f.b1 = b1; f.w2 = w2.w; f.b2 = b2; f.w_bf16 = bf;
-  f.out = t_out; f.out_bf16 = bf; f.ws = ws; f.cnt = cnt;
-  f.n = rows; f.D = D; f.H = w1.N;
-  return ln.t && w1.K == D && w2.N == D && w2.K == w1.N && stream_ffn(f, st);
-}
-
 }  // namespace
 
 void FsEendStream::enc_chunk(hipStream_t st) {
@@ -161,12 +146,10 @@ void FsEendStream::enc_chunk(hipStream_t st) {
     conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
     ln = PendingLn{xb[xi], T_, L.n1g, L.n1b, xb[xi ^ 1]};
     xi ^= 1;
-    if (!ffn_fused(ln, L.l1, L.b1, L.l2, L.b2, c, D, bf_, T_, fws_, fcnt_, st)) {
-      ConvGemmArgs p = lin(Tens{xb[xi], false}, c, D, L.l1, L.b1, h, L.l1.N);
-      p.act = kActRelu;
-      gemm_fused(p, &ln, nullptr, D, bf_, st);
-      conv_gemm(lin(h, c, L.l1.N, L.l2, L.b2, t, D), bf_, st);
-    }
+    ConvGemmArgs p = lin(Tens{xb[xi], false}, c, D, L.l1, L.b1, h, L.l1.N);
+    p.act = kActRelu;
+    gemm_fused(p, &ln, nullptr, D, bf_, st);
+    conv_gemm(lin(h, c, L.l1.N, L.l2, L.b2, t, D), bf_, st);
     ln = PendingLn{xb[xi], T_, L.n2g, L.n2b, xb[xi ^ 1]};
     xi ^= 1;
   }
@@ -237,12 +220,10 @@ void FsEendStream::dec_chunk(hipStream_t st) {
     ln = PendingLn{ab[ai], T_, f.n21g, f.n21b, ab[ai ^ 1]};
     ai ^= 1;
     // (3) feed-forward
-    if (!ffn_fused(ln, f.l1, f.b1, f.l2, f.b2, n, D, bf_, T_, fws_, fcnt_ + 1, st)) {
-      ConvGemmArgs p = lin(Tens{ab[ai], false}, n, D, f.l1, f.b1, h, f.l1.N);
-      p.act = kActRelu;
-      gemm_fused(p, &ln, nullptr, D, bf_, st);
-      conv_gemm(lin(h, n, f.l1.N, f.l2, f.b2, t, D), bf_, st);
-    }
+    ConvGemmArgs p = lin(Tens{ab[ai], false}, n, D, f.l1, f.b1, h, f.l1.N);
+    p.act = kActRelu;
+    gemm_fused(p, &ln, nullptr, D, bf_, st);
+    conv_gemm(lin(h, n, f.l1.N, f.l2, f.b2, t, D), bf_, st);
     ln = PendingLn{ab[ai], T_, f.n22g, f.n22b, ab[ai ^ 1]};
     ai ^= 1;
     pending = true;

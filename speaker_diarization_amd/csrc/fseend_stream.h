@@ -68,8 +68,6 @@ class FsEendStream {
   unsigned* dcnt_ = nullptr;           // attn_decode's per-(sequence, head) block counters (zeroed once)
   float* sws_ = nullptr;               // stream_slot_block's per-head out-projection partials
   unsigned* scnt_ = nullptr;           // its arrival counter (zeroed once)
-  float* fws_ = nullptr;               // stream_ffn's per-workgroup down-projection partials
-  unsigned* fcnt_ = nullptr;           // its arrival counters: [0] encoder, [1] decoder (zeroed once)
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

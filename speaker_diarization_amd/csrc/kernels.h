@@ -509,30 +509,6 @@ struct SlotBlockArgs {
   float scale = 0.125f;
 };
 bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st);
-// FS-EEND streaming feed-forward sub-block for a chunk's n rows: y = LN(x + t) (-> ln_out); out = relu(y W1ᵀ + b1)
-// W2ᵀ + b2.  ONE launch of H / 128 workgroups: workgroup g owns hidden units [128 g, 128 g + 128) (the hidden
-// layer never leaves LDS) and publishes its down-projection partial write-through; the last workgroup to count
-// itself sums the partials in workgroup order (MI355X guide hand-off row 1).  Supported: D == 256,
-// H % 128 == 0, H <= 4096, n <= 8; returns false otherwise.
-struct StreamFfnArgs {
-  const float* ln_x = nullptr;
-  const void* ln_t = nullptr;
-  bool t_bf16 = false;
-  const float *ln_g = nullptr, *ln_b = nullptr;
-  float eps = 1e-5f;
-  float* ln_out = nullptr;
-  const void* w1 = nullptr;     // packed [H][D]
-  const float* b1 = nullptr;
-  const void* w2 = nullptr;     // packed [D][H]
-  const float* b2 = nullptr;
-  bool w_bf16 = false;
-  void* out = nullptr;          // (n, D)
-  bool out_bf16 = false;
-  float* ws = nullptr;          // (H / 128) * n * D floats
-  unsigned* cnt = nullptr;
-  int n = 1, D = 256, H = 2048;
-};
-bool stream_ffn(const StreamFfnArgs& a, hipStream_t st);
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,

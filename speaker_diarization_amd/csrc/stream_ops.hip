@@ -359,9 +359,8 @@ __global__ __launch_bounds__(256) void dec_finish_kernel(const float* __restrict
   if (lane == 0) scores[r] = dot / sqrtf(sq);
 }
 
-// Weight rows as 16-B vectors: 8 bf16 or 4 fp32 values per vector.  Every fused stream kernel below issues a
-// thread's whole weight slice as one batch before it needs any of it (one memory latency per slice, not one
-// per vector).
+// Weight rows as 16-B vectors: 8 bf16 or 4 fp32 values per vector.  The fused slot block below issues a thread's
+// whole weight slice as one batch before it needs any of it (one memory latency per slice, not one per vector).
 template <bool WBF>
 struct WVec {
   static constexpr int VE = WBF ? 8 : 4;
@@ -501,105 +500,6 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   }
 }
 
-// stream_ffn (kernels.h).  grid H / 128, 256 threads.
-constexpr int kFfnRows = 8, kFfnHid = 128, kFfnMaxG = 32;
-template <bool WBF>
-__global__ __launch_bounds__(256) void stream_ffn_kernel(StreamFfnArgs a) {
-  using V = WVec<WBF>;
-  constexpr int D = kSlotD, VE = V::VE;
-  constexpr int N1 = D / 2 / VE;       // vectors of this thread's half up-projection row
-  constexpr int N2 = kFfnHid / VE;     // vectors of its down-projection row slice
-  __shared__ float ys[kFfnRows][D];
-  __shared__ float hs[kFfnRows][kFfnHid];
-  __shared__ int last;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int g = blockIdx.x, n = a.n, H = a.H;
-  const int j = tid >> 1, kh = tid & 1;
-  const int64_t r1 = (int64_t)(g * kFfnHid + j) * D + kh * (D / 2);
-  const int64_t r2 = (int64_t)tid * H + g * kFfnHid;
-  uint4 w1[N1], w2[N2];
-#pragma unroll
-  for (int v = 0; v < N1; ++v) w1[v] = V::load(a.w1, r1 + v * VE);
-  if constexpr (WBF) {   // bf16: both slices in flight at once (fp32: the down slice after the up product)
-#pragma unroll
-    for (int v = 0; v < N2; ++v) w2[v] = V::load(a.w2, r2 + v * VE);
-  }
-  for (int r = wid; r < n; r += 4) {
-    float4 y[4];
-    ln_row(a.ln_x + (int64_t)r * D, a.ln_t, a.t_bf16, (int64_t)r * D, a.ln_g, a.ln_b, a.eps, D, lane, y);
-    *reinterpret_cast<float4*>(&ys[r][lane * 4]) = y[0];
-    if (g == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
-  }
-  __syncthreads();
-  {
-    const float bj = a.b1[g * kFfnHid + j];
-    for (int m = 0; m < n; ++m) {
-      const float* yr = &ys[m][kh * (D / 2)];
-      float acc = 0.f;
-#pragma unroll
-      for (int v = 0; v < N1; ++v) {
-        float yv[VE];
-#pragma unroll
-        for (int e = 0; e < VE; e += 4) {
-          const float4 q = *reinterpret_cast<const float4*>(yr + v * VE + e);
-          yv[e] = q.x; yv[e + 1] = q.y; yv[e + 2] = q.z; yv[e + 3] = q.w;
-        }
-#pragma unroll
-        for (int e = 0; e < VE; ++e) acc = fmaf(V::at(w1[v], e), yv[e], acc);
-      }
-      const float t = acc + __shfl_xor(acc, 1, 64);
-      if (kh == 0) hs[m][j] = fmaxf(t + bj, 0.f);
-    }
-  }
-  if constexpr (!WBF) {
-#pragma unroll
-    for (int v = 0; v < N2; ++v) w2[v] = V::load(a.w2, r2 + v * VE);
-  }
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
-  for (int m = 0; m < n; ++m) {
-    float p = 0.f;
-#pragma unroll
-    for (int v = 0; v < N2; ++v) {
-      float hv[VE];
-#pragma unroll
-      for (int e = 0; e < VE; e += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(&hs[m][v * VE + e]);
-        hv[e] = q.x; hv[e + 1] = q.y; hv[e + 2] = q.z; hv[e + 3] = q.w;
-      }
-#pragma unroll
-      for (int e = 0; e < VE; ++e) p = fmaf(V::at(w2[v], e), hv[e], p);
-    }
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p), rw, (uint32_t)((((int64_t)g * n + m) * D + tid) * 4), 0,
-                                          16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned G = gridDim.x;
-    last = (__hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % G) == G - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  const float bo = a.b2[tid];
-  const int G = gridDim.x;
-  for (int m = 0; m < n; ++m) {
-    float pv[kFfnMaxG];
-#pragma unroll
-    for (int gg = 0; gg < kFfnMaxG; ++gg)   // all partial loads issued before the ordered sum
-      pv[gg] = gg < G ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                            rw, (uint32_t)((((int64_t)gg * n + m) * D + tid) * 4), 0, 16))
-                      : 0.f;
-    float v = 0.f;
-#pragma unroll
-    for (int gg = 0; gg < kFfnMaxG; ++gg)
-      if (gg < G) v += pv[gg];
-    v += bo;
-    if (a.out_bf16) static_cast<uint16_t*>(a.out)[(int64_t)m * D + tid] = f2bf_bits(v);
-    else static_cast<float*>(a.out)[(int64_t)m * D + tid] = v;
-  }
-}
-
 __global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
   if (threadIdx.x == 0) {
     const int v = *cursor + by;
@@ -663,28 +563,13 @@ void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
 }
 
 bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st) {
-  // opt-in until it measures faster than the three launches (SDIAR_STREAM_FUSE=1)
-  static const bool off = getenv("SDIAR_STREAM_FUSE") == nullptr || getenv("SDIAR_NO_SLOT_BLOCK") != nullptr;
+  static const bool off = getenv("SDIAR_NO_SLOT_BLOCK") != nullptr;   // A/B switch: the three-launch path
   const int n = a.c * a.C;
   if (off || a.D != kSlotD || a.nh * kHD != a.D || a.nh > 8 || n < 1 || n > kSlotRows || a.C > 8 || !a.ws || !a.cnt)
     return false;
   ProfScope prof("slot_block", 2.0 * n * a.D * 4.0 * a.D + 4.0 * n * a.C * a.D, (a.w_bf16 ? 2.0 : 4.0) * 4 * a.D * a.D, st);
   if (a.w_bf16) hipLaunchKernelGGL(slot_block_kernel<true>, dim3(a.nh), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(slot_block_kernel<false>, dim3(a.nh), dim3(512), 0, st, a);
-  SD_LAUNCH_CHECK();
-  return true;
-}
-
-bool stream_ffn(const StreamFfnArgs& a, hipStream_t st) {
-  // opt-in until it measures faster than the two launches (SDIAR_STREAM_FUSE=1)
-  static const bool off = getenv("SDIAR_STREAM_FUSE") == nullptr || getenv("SDIAR_NO_STREAM_FFN") != nullptr;
-  if (off || a.D != kSlotD || a.H % kFfnHid != 0 || a.H > kFfnMaxG * kFfnHid || a.n < 1 || a.n > kFfnRows || !a.ws ||
-      !a.cnt)
-    return false;
-  ProfScope prof("stream_ffn", 4.0 * a.n * a.D * (double)a.H, (a.w_bf16 ? 2.0 : 4.0) * 2 * a.D * (double)a.H, st);
-  const dim3 grid(a.H / kFfnHid);
-  if (a.w_bf16) hipLaunchKernelGGL(stream_ffn_kernel<true>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(stream_ffn_kernel<false>, grid, dim3(256), 0, st, a);
   SD_LAUNCH_CHECK();
   return true;
 }

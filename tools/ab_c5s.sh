@@ -1,11 +1,11 @@
 #!/bin/bash
-# c5s p50 with the fused stream sub-blocks on / off (one box): bash tools/ab_c5s.sh rounds
+# c5s p50 with the fused slot block on / off (one box): bash tools/ab_c5s.sh rounds
 set -euo pipefail
 R=${1:-1}
 mkdir -p gpurun_out/ab
 for i in $(seq 1 "$R"); do
   for tag in fused unfused; do
-    if [ "$tag" = unfused ]; then unset SDIAR_STREAM_FUSE; else export SDIAR_STREAM_FUSE=1; fi
+    if [ "$tag" = unfused ]; then export SDIAR_NO_SLOT_BLOCK=1; else unset SDIAR_NO_SLOT_BLOCK; fi
     out="gpurun_out/ab/c5s_${tag}_$i.json"
     timeout -k 10 300 python3 bench.py --workload c5s --steps 2 --warmup 1 --no-cpu-baseline > "$out" 2> "${out%.json}.err"
     python3 - "$tag" "$out" <<'PY'
