@@ -270,7 +270,8 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
     conv_gemm_skinny(p, bf16, st);
     return;
   }
-  SD_CHECK(!p.ln_g && !p.kv_out, kErrInvalid, "conv_gemm: LN prologue / K-V epilogue exist on the skinny path only");
+  SD_CHECK(!p.ln_g && !p.kv_out && !p.pro_mode, kErrInvalid,
+           "conv_gemm: LN / other prologues and the K-V epilogue exist on the skinny path only");
   if (bf16) {
     conv_gemm_bf16(p, st);
     return;

@@ -167,7 +167,10 @@ void FsEendStream::dec_chunk(hipStream_t st) {
   const int n = c * C;
   const Tens qkv{QKV_, bf_}, ao{AO_, bf_}, t{T_, bf_}, h{H_, bf_};
   const float scale = 1.f / std::sqrt((float)(D / nh));
-  gather_window(hist_, D, state_ + 2, state_ + 1, 9, c + 18, W_, st);
+  // The window gather, the embedding's L2 norm and the slot init run as the A prologues of the GEMMs that
+  // consume them (gemm_skinny pro_mode 3 / 1 / 2: same values, three launches fewer) when the skinny path
+  // takes the chunk; SDIAR_NO_STREAM_PRO=1 keeps them as their own kernels.
+  static const bool no_pro = getenv("SDIAR_NO_STREAM_PRO") != nullptr;
   {
     ConvGemmArgs p;
     p.A = W_; p.a_bf16 = false; p.B = 1; p.H = 1; p.W = c + 18; p.Cin = D; p.lda = D; p.a_coff = 0;
@@ -177,19 +180,46 @@ void FsEendStream::dec_chunk(hipStream_t st) {
     p.beta = m.cnn_.beta;
     p.out = Yc_; p.out_bf16 = false;
     p.o_sb = (int64_t)c * D; p.o_sh = 0; p.o_sw = D; p.o_sn = 1;
-    conv_gemm(p, bf_, st);
+    ConvGemmArgs q = p;
+    q.pro_mode = 3; q.ln_x = hist_; q.pro_cursor = state_ + 2; q.pro_nvalid = state_ + 1; q.pro_pad = 9;
+    if (!no_pro && gemm_skinny_supported(q)) {
+      conv_gemm_skinny(q, bf_, st);
+    } else {
+      gather_window(hist_, D, state_ + 2, state_ + 1, 9, c + 18, W_, st);
+      conv_gemm(p, bf_, st);
+    }
   }
-  row_l2norm(Yc_, c, D, E_, st);
-  conv_gemm(lin(Tens{E_, false}, c, D, m.conv_emb_, nullptr, Tens{G_, false}, D), bf_, st);
+  {
+    ConvGemmArgs p = lin(Tens{E_, false}, c, D, m.conv_emb_, nullptr, Tens{G_, false}, D);
+    ConvGemmArgs q = p;
+    q.pro_mode = 1; q.ln_x = Yc_; q.ln_out = E_;
+    if (!no_pro && gemm_skinny_supported(q)) {
+      conv_gemm_skinny(q, bf_, st);
+    } else {
+      row_l2norm(Yc_, c, D, E_, st);
+      conv_gemm(p, bf_, st);
+    }
+  }
   float* ab[2] = {A_, A2_};
   int ai = 0;
-  slot_init(G_, c, C, D, m.slot_bias_, ab[0], st);
   PendingLn ln;
   bool pending = false;
   for (int app = 0; app < m.cfg_.dec_n_layers; ++app) {
     // (1) time attention per slot against this application's history (causal)
     const KvEpi kv{kv_dec_[app], state_ + 2, C, 2 * D};
-    gemm_fused(lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D), pending ? &ln : nullptr, &kv, D, bf_, st);
+    if (app == 0) {   // slot_init as the in-projection's A prologue (ab[0] = G rows + slot bias)
+      ConvGemmArgs q = lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D);
+      q.pro_mode = 2; q.ln_x = G_; q.pro_p = m.slot_bias_; q.pro_C = C; q.ln_out = ab[0];
+      q.kv_out = kv.dst; q.kv_cursor = kv.cursor; q.kv_mult = kv.mult; q.kv_col0 = D; q.kv_ld = kv.ld;
+      if (!no_pro && gemm_skinny_supported(q)) {
+        conv_gemm_skinny(q, bf_, st);
+      } else {
+        slot_init(G_, c, C, D, m.slot_bias_, ab[0], st);
+        gemm_fused(lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D), nullptr, &kv, D, bf_, st);
+      }
+    } else {
+      gemm_fused(lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D), pending ? &ln : nullptr, &kv, D, bf_, st);
+    }
     {
       DecodeAttnArgs d;
       d.q = QKV_; d.q_tok = (int64_t)C * 3 * D; d.q_seq = 3 * D;

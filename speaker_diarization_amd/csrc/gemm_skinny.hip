@@ -114,6 +114,45 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M,
         }
       }
     }
+  } else if (p.pro_mode == 1) {
+    // row_l2norm (fseend_ops.hip) per row: lane + 64 j elements, fmaf sum of squares in j order, warp sum
+    for (int m = wid; m < M; m += 4) {
+      const float* xr = p.ln_x + (int64_t)m * K;
+      float v[8];
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = lane + 64 * j;
+        v[j] = i < K ? xr[i] : 0.f;
+        sq = fmaf(v[j], v[j], sq);
+      }
+      const float nrm = sqrtf(warp_sum(sq));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = lane + 64 * j;
+        if (i < K) {
+          const float y = v[j] / nrm;
+          As[m * K + i] = y;
+          if (blockIdx.x == 0) p.ln_out[(int64_t)m * K + i] = y;
+        }
+      }
+    }
+  } else if (p.pro_mode == 2) {
+    // slot_init: row r = t * C + c is ln_x[t] + pro_p[c]
+    for (int i = tid; i < M * K; i += 256) {
+      const int r = i / K, d = i - r * K;
+      const float y = p.ln_x[(int64_t)(r / p.pro_C) * K + d] + p.pro_p[(int64_t)(r % p.pro_C) * K + d];
+      As[i] = y;
+      if (blockIdx.x == 0) p.ln_out[i] = y;
+    }
+  } else if (p.pro_mode == 3) {
+    // gather_window: staged row r is history row *cursor - pad + r, zero outside [0, *n_valid)
+    const int base = *p.pro_cursor - p.pro_pad, nv = *p.pro_nvalid;
+    for (int i = tid; i < span; i += 256) {
+      const int r = i / p.lda, d = i - r * p.lda;
+      const int src = base + r;
+      As[i] = (src >= 0 && src < nv) ? p.ln_x[(int64_t)src * p.lda + d] : 0.f;
+    }
   } else if (p.a_bf16) {
     const uint16_t* a = static_cast<const uint16_t*>(p.A) + p.a_coff;
     for (int i = tid; i < span; i += 256) As[i] = bf_bits2f(a[i]);
@@ -205,7 +244,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M,
 // A(m, k) = A[a_coff + m*a_rs + k]: a plain linear (row stride lda), or a stride-1
 // unpadded 1-D conv whose taps are consecutive rows (Cin == lda).
 int skinny_row_stride(const ConvGemmArgs& p) {
-  if (p.ln_g) return p.K;   // LN prologue: dense rows of K built in LDS
+  if (p.ln_g || p.pro_mode == 1 || p.pro_mode == 2) return p.K;   // prologue rows of K built in LDS
   if (a_rows_linear(p)) return p.lda;
   if (p.B == 1 && p.H == 1 && p.Ho == 1 && p.kh == 1 && p.sw == 1 && p.dw == 1 && p.pw == 0 && p.ph == 0 &&
       p.Cin == p.lda && p.W >= p.Wo + p.kw - 1)
@@ -245,6 +284,16 @@ bool gemm_skinny_supported(const ConvGemmArgs& p) {
   if (((int64_t)(M - 1) * rs + p.K) > kSkinnyLdsFloats) return false;
   if (p.ln_g && (p.K % 256 != 0 || p.K > 1024 || !p.ln_x || !p.ln_b || !p.ln_out || p.ln_out == p.ln_x))
     return false;
+  if (p.pro_mode != 0) {
+    if (p.ln_g || !p.ln_x || p.a_bf16) return false;
+    if (p.pro_mode == 1 && (p.K > 512 || !p.ln_out || p.ln_out == p.ln_x || !a_rows_linear(p) || p.lda != p.K))
+      return false;
+    if (p.pro_mode == 2 && (!p.pro_p || p.pro_C < 1 || !p.ln_out || p.ln_out == p.ln_x || !a_rows_linear(p) ||
+                            p.lda != p.K))
+      return false;
+    if (p.pro_mode == 3 && (!p.pro_cursor || !p.pro_nvalid)) return false;
+    if (p.pro_mode > 3) return false;
+  }
   return p.a_coff % 4 == 0 && rs % 4 == 0;
 }
 

@@ -44,6 +44,17 @@ struct ConvGemmArgs {
   const float* ln_b = nullptr;
   float ln_eps = 1e-5f;
   float* ln_out = nullptr;
+  // Other skinny-only A prologues (pro_mode; ln_g unset):
+  //   1  rows of ln_x (fp32, K wide, K <= 512) scaled to unit L2 norm with row_l2norm's arithmetic;
+  //      workgroup 0 stores them to ln_out
+  //   2  row r of A = ln_x[r / pro_C] + pro_p[r % pro_C] (slot_init's sum); workgroup 0 stores them to ln_out
+  //   3  the staged span (the rows a stride-1 1-D conv reads) = rows [*pro_cursor - pro_pad, ...) of ln_x
+  //      (row stride lda), zero outside [0, *pro_nvalid) (gather_window's window; p.A unused)
+  int pro_mode = 0;
+  const float* pro_p = nullptr;
+  int pro_C = 1, pro_pad = 0;
+  const int* pro_cursor = nullptr;
+  const int* pro_nvalid = nullptr;
   // K/V history epilogue: columns n >= kv_col0 are also stored (out dtype) at
   // kv_out[(*kv_cursor * kv_mult + m) * kv_ld + n - kv_col0].
   void* kv_out = nullptr;

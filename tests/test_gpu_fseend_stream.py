@@ -325,3 +325,38 @@ def test_slot_block_matches_three_launches(gpu, precision, tmp_path):
         np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=tol)
     d = float((res[0][0] - res[1][0]).abs().max())
     assert d <= (1e-5 if precision == "fp32" else 1e-2), d
+
+
+PRO = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+import tests.test_gpu_fseend_stream as t
+from tests.golden.make_golden import eda_inputs
+m = t._model(808, {prec!r}, max_frames=300)
+x = torch.from_numpy(eda_inputs([300], seed=88)[0]).cuda()
+outs = [t._stream_all(m, x, c)[0].cpu() for c in (1, 2)]
+torch.save(outs, {path!r})
+"""
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_gemm_prologues_bit_identical(gpu, precision, tmp_path):
+    """The decoder's window gather, embedding L2 norm and slot init run as A prologues of the skinny GEMMs
+    that consume them (gemm_skinny pro_mode 3 / 1 / 2) with the same arithmetic as gather_window, row_l2norm
+    and slot_init: the streams (chunks of 1 and 2 frames) are bit-identical with SDIAR_NO_STREAM_PRO=1."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for off in (None, "1"):
+        env = dict(os.environ)
+        env.pop("SDIAR_NO_STREAM_PRO", None)
+        if off:
+            env["SDIAR_NO_STREAM_PRO"] = off
+        path = str(tmp_path / f"p_{off}.pt")
+        r = subprocess.run([sys.executable, "-c", PRO.format(repo=repo, prec=precision, path=path)], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(torch.load(path, weights_only=True))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
