@@ -313,6 +313,7 @@ struct BnRelu {
   const float* b = nullptr;
   const int* grp = nullptr;
   int group = 1;
+  int win0 = 0;   // the kernel's window 0 is window win0 of the batch (a window slice): group (w + win0) / group
 };
 // Non-finite scan of per-window inputs x (B windows of per_win floats, 16-B aligned rows): win[w] |= 1 and
 // grp_a[w / group] |= 1, grp_b[w / group] |= 1 (each nullable) for every window holding a NaN / Inf.  The

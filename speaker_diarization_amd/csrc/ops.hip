@@ -530,7 +530,7 @@ void zero_fill(void* p, size_t bytes, hipStream_t st) {
 // ------------------------------------------------------------------ TS-VAD glue
 __device__ __forceinline__ float bn_relu(const BnRelu& p, int window, int c, float x) {
   if (!p.a) return x;
-  const bool bypass = p.grp && p.grp[window / p.group];
+  const bool bypass = p.grp && p.grp[(window + p.win0) / p.group];
   return fmaxf(bypass ? x : fmaf(p.a[c], x, p.b[c]), 0.f);
 }
 

@@ -190,27 +190,17 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   // each kernel's HIP-event time is its own and not shared with the other slice's kernels.
   static const bool one_stream_env = getenv("SDIAR_CAM_ONE_STREAM") != nullptr;
   const bool one_stream = one_stream_env || prof_enabled();
-  Tens x4;
-  if (!one_stream && B >= 384) {
-    if (!side_) {
-      SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-      SD_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-      SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-    }
-    const int B1 = B / 2;
-    SD_HIP(hipEventRecord(ev_fork_, st));
-    SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-    x4 = cam_.forward(ref, B1, Tf, st, 0);
-    (void)cam_.forward(ref, B - B1, Tf, side_, B1);
-    SD_HIP(hipEventRecord(ev_join_, side_));
-    SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
-  } else {
-    x4 = cam_.forward(ref, B, Tf, st);
-  }
-  const int T2 = CamTrunk::out_frames(Tf);
   const int E = cfg_.embed_dim, SE = cfg_.speaker_embed_dim, NS = cfg_.max_num_speaker;
+  const int T2 = CamTrunk::out_frames(Tf);
+  const bool two = !one_stream && B >= 384;
+  if (two && !side_) {
+    SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    SD_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  }
   // ---------------- BatchNorm1D's NaN bypass: which windows hold a non-finite input, which reference forwards
-  // (groups of fwd_batch_ windows) therefore skip the BatchNorm
+  // (groups of fwd_batch_ windows) therefore skip the BatchNorm (from the inputs alone, so first: the window
+  // slices below then need nothing from each other until the LSTM)
   const int G = fwd_batch_ > 0 ? fwd_batch_ : B;
   int* win_fb = nonfinite_;
   int* win_ts = nonfinite_ + cfg_.max_batch;
@@ -222,10 +212,65 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   BnRelu sd_bn = down_bn_, bd_bn = backend_bn_;
   sd_bn.grp = grp_sd; sd_bn.group = G;
   bd_bn.grp = grp_bd; bd_bn.group = G;
+  // speech_down_or_up conv geometry (its output frame count T3)
+  const int T3 = cam_conv1d(Tens{nullptr, bf}, 1, T2, CamTrunk::kChannels, down_, 2, 2, 1, Tens{mix_, false}, SE).Wo;
+  const bool fused_v1 = cfg_.variant == 1 && SE == 192 && E == 2 * SE && conformer_stack_fused(conf_, E, bf);
+  // v1 conformer stack over windows [b0, b0 + Bh): every buffer of the fused stack is addressed from the slice's
+  // first row (bf16 y / qkv / ao / h, fp32 X, per-sequence GroupNorm partials, the speaker streams)
+  auto conformer_slice = [&](int b0, int Bh, hipStream_t s) {
+    const int64_t s0 = (int64_t)b0 * NS, r0 = s0 * Tl;
+    auto at = [](float* p, int64_t bytes) { return reinterpret_cast<float*>(reinterpret_cast<char*>(p) + bytes); };
+    EncoderWork w = enc_work();
+    w.Y = at(Y_, r0 * E * 2);
+    w.QKV = at(QKV_, r0 * 3 * E * 2);
+    w.AO = at(AO_, r0 * E * 2);
+    w.H = at(H_, r0 * 2 * E * 2);
+    w.partial = partial_ + s0 * ((E + 63) / 64) * 2;
+    SpeakerStreams io;
+    io.ts = ts + s0 * SE; io.mix = mixg_ + (int64_t)b0 * T3 * SE; io.ldmix = SE; io.Tmix = T3; io.NS = NS;
+    io.out = at(X2_, (int64_t)b0 * Tl * NS * E * 2);
+    run_conformer_stack(conf_, X_ + r0 * E, Bh * NS, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, w,
+                        s, &io);
+  };
+  if (fused_v1) SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape, "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
+  if (fused_v1 && two) {
+    // Two window slices, each through the whole per-window part of the model on its own stream: CAM++ trunk,
+    // speech_down conv, gsp_fc, conformer stack.  Nothing joins between the trunk and the conformer, so one
+    // slice's HBM-bound CAM++ kernels overlap the other's MFMA-bound conformer programs (bit-identical per
+    // window: every kernel up to the LSTM computes a window independently of the rest of the batch).
+    const int B1 = B / 2;
+    SD_HIP(hipEventRecord(ev_fork_, st));
+    SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+    auto slice = [&](int b0, int Bh, hipStream_t s) {
+      const Tens x4s = cam_.forward(ref, Bh, Tf, s, b0);
+      float* mx = mix_ + (int64_t)b0 * T3 * SE;
+      conv_gemm(cam_conv1d(x4s, Bh, T2, CamTrunk::kChannels, down_, 2, 2, 1, Tens{mx, false}, SE), bf, s);
+      BnRelu sb = sd_bn;
+      sb.win0 = b0;
+      gsp_fc(mx, Bh * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_ + (int64_t)b0 * T3 * SE, SE, s, sb, T3);
+      conformer_slice(b0, Bh, s);
+    };
+    slice(0, B1, st);
+    slice(B1, B - B1, side_);
+    SD_HIP(hipEventRecord(ev_join_, side_));
+    SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
+  } else {
+  // CAM++ up to transit3, (B, T2, 512): two window slices on two streams for large batches (v0)
+  Tens x4;
+  if (two) {
+    const int B1 = B / 2;
+    SD_HIP(hipEventRecord(ev_fork_, st));
+    SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+    x4 = cam_.forward(ref, B1, Tf, st, 0);
+    (void)cam_.forward(ref, B - B1, Tf, side_, B1);
+    SD_HIP(hipEventRecord(ev_join_, side_));
+    SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
+  } else {
+    x4 = cam_.forward(ref, B, Tf, st);
+  }
   // ---------------- speech_down_or_up conv (out_nonlinear BN-ReLU fused as prologue) + bias, fp32 out; its
   // BatchNorm1D + ReLU are applied by the consumer (gsp_fc / build_speaker_input)
   ConvGemmArgs pd = cam_conv1d(x4, B, T2, CamTrunk::kChannels, down_, 2, 2, 1, Tens{mix_, false}, SE);
-  const int T3 = pd.Wo;
   conv_gemm(pd, bf, st);
   const int S = B * NS;
   if (cfg_.variant == 0) {
@@ -249,46 +294,20 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     ConvGemmArgs f = cam_conv1d(Tens{X_, false}, B, Tl, E, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);
+    poison_windows(logits, B, (int64_t)NS * Tl, win_fb, win_ts, st);
+    return;
+  }
+  SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape, "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
+  gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st, sd_bn, T3);
+  if (fused_v1) {
+    conformer_slice(0, B, st);
   } else {
-    SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape,
-             "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
-    gsp_fc(mix_, B * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_, SE, st, sd_bn, T3);
-    if (SE == 192 && E == 2 * SE && conformer_stack_fused(conf_, E, bf)) {
-      // the row programs build [ts | mix] on load and write the bf16 speakers-to-channels rows directly
-      // windows [b0, b0 + Bh): every buffer of the fused stack is addressed from the slice's first row
-      // (bf16 y / qkv / ao / h, fp32 X, per-sequence GroupNorm partials, the speaker streams)
-      auto run_slice = [&](int b0, int Bh, hipStream_t s) {
-        const int64_t s0 = (int64_t)b0 * NS, r0 = s0 * Tl;
-        auto at = [](float* p, int64_t bytes) { return reinterpret_cast<float*>(reinterpret_cast<char*>(p) + bytes); };
-        EncoderWork w = enc_work();
-        w.Y = at(Y_, r0 * E * 2);
-        w.QKV = at(QKV_, r0 * 3 * E * 2);
-        w.AO = at(AO_, r0 * E * 2);
-        w.H = at(H_, r0 * 2 * E * 2);
-        w.partial = partial_ + s0 * ((E + 63) / 64) * 2;
-        SpeakerStreams io;
-        io.ts = ts + s0 * SE; io.mix = mixg_ + (int64_t)b0 * T3 * SE; io.ldmix = SE; io.Tmix = T3; io.NS = NS;
-        io.out = at(X2_, (int64_t)b0 * Tl * NS * E * 2);
-        run_conformer_stack(conf_, X_ + r0 * E, Bh * NS, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr,
-                            w, s, &io);
-      };
-      // like the CAM++ trunk above: two window slices on two streams fill each other's idle CUs
-      if (!one_stream && B >= 384) {
-        const int B1 = B / 2;
-        SD_HIP(hipEventRecord(ev_fork_, st));
-        SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-        run_slice(0, B1, st);
-        run_slice(B1, B - B1, side_);
-        SD_HIP(hipEventRecord(ev_join_, side_));
-        SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
-      } else {
-        run_slice(0, B, st);
-      }
-    } else {
-      build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
-      run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
-      speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
-    }
+    build_speaker_input(ts, mixg_, SE, T3, B, NS, Tl, SE, nullptr, X_, st);
+    run_conformer_stack(conf_, X_, S, Tl, E, cfg_.conformer_heads, cfg_.conformer_kernel, nullptr, enc_work(), st);
+    speakers_to_channels(X_, B, NS, Tl, E, X2_, bf, st);
+  }
+  }
+  {
     const int Hh = cfg_.lstm_hidden;
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     // SDIAR_LSTM_FP32 (diagnostic, tools/parity_stages.py): the exact-fp32 recurrence in bf16 mode too
