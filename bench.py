@@ -973,8 +973,10 @@ def main_stream(a, wl):
     elapsed, _ = timed(lambda: step(True), 0, a.steps, world, dev)
     st1 = stats()
     lat[:] = lat[-(len(lat) // a.steps) * a.steps:]   # timed steps only
+    # every step streams the whole recording from reset: a push attends over (T + 1) / 2 history rows on average
     latency_model = stream_latency_model(sd_np, st0, st1, len(lat), float(np.percentile(np.array(lat) * 1e6, 50)),
-                                         audio, a.precision) if a.steps else None
+                                         audio, a.precision, kv=dict(rows=(T + 1) / 2, enc_layers=4, dec_layers=2,
+                                                                     slots=6, d=256)) if a.steps else None
     # parity of this very run: against the whole-recording GPU test() on the same features, and against
     # the fp32 CPU oracle (oracle/fseend_ref.py test() on oracle/eend_ref.py features) over the first frames
     Tc = min(T, 2000)
@@ -1045,11 +1047,13 @@ def kernel_boundary_us(n=200, reps=20):
     return e0.elapsed_time(e1) * 1000.0 / (n * reps)
 
 
-def stream_latency_model(sd_np, st0, st1, pushes, p50_us, audio, precision):
+def stream_latency_model(sd_np, st0, st1, pushes, p50_us, audio, precision, kv=None):
     """C5 latency roofline (SURVEY §8(d) latency model): a push cannot finish faster than its chain of
     dependent device operations: (graph nodes run per push + the per-push copies) x the measured kernel
-    boundary, plus the weight bytes those chunk runs stream / HBM peak.  achieved = p50 per push (host
-    wall, incl. the graph launch and the synchronisation); frac = floor / achieved."""
+    boundary, plus the bytes those chunk runs must read / HBM peak: the weights, and the K|V history rows
+    each attention scores (encoder: one sequence per layer; decoder: `slots` sequences per application;
+    2 * d values per row, `rows` = the mean history length over the timed pushes).  achieved = p50 per push
+    (host wall, incl. the graph launch and the synchronisation); frac = floor / achieved."""
     enc_runs, dec_runs = st1[0] - st0[0], st1[1] - st0[1]
     ne, nd = st1[2], st1[3]
     esz = 2 if precision == "bf16" else 4
@@ -1064,6 +1068,11 @@ def stream_latency_model(sd_np, st0, st1, pushes, p50_us, audio, precision):
     per_push_copies = 1.0 + dec_runs / max(pushes, 1)     # the samples' copy, each emitted frame's copy
     b_us = kernel_boundary_us()
     bytes_per_push = (enc_runs * enc_bytes + dec_runs * dec_bytes) / max(pushes, 1)
+    kv_bytes = 0.0
+    if kv:
+        row = 2 * kv["d"] * esz * kv["rows"]
+        kv_bytes = (enc_runs * kv["enc_layers"] * row + dec_runs * kv["dec_layers"] * kv["slots"] * row) / max(pushes, 1)
+    bytes_per_push += kv_bytes
     floor = (per_push_nodes + per_push_copies) * b_us + bytes_per_push / (HBM_PEAK * 1e9) * 1e6
     return dict(bound="latency", achieved=round(p50_us, 2), peak=round(floor, 2), unit="us/push",
                 frac=round(floor / p50_us, 4), traffic=None,
@@ -1072,10 +1081,12 @@ def stream_latency_model(sd_np, st0, st1, pushes, p50_us, audio, precision):
                        "encoder_graph_nodes": ne, "decoder_graph_nodes": nd,
                        "device_ops_per_push": round(per_push_nodes + per_push_copies, 2),
                        "kernel_boundary_us": round(b_us, 3),
-                       "weight_bytes_per_push": int(bytes_per_push),
+                       "weight_bytes_per_push": int(bytes_per_push - kv_bytes),
+                       "kv_history_bytes_per_push": int(kv_bytes),
                        "input": "audio" if audio else "feature rows",
                        "floor": "(graph nodes + copies per push) x measured dependent-kernel boundary "
-                                "(replayed hipGraph of trivial kernels) + weight bytes per push / 8 TB/s"})
+                                "(replayed hipGraph of trivial kernels) + (weight + K|V history bytes) per push "
+                                "/ 8 TB/s"})
 
 
 def fseend_oracle_parity(meeting, sd_np, gpu_scores, frames=1000):

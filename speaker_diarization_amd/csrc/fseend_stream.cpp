@@ -61,7 +61,7 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
 }
 
 FsEendStream::~FsEendStream() {
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 3; ++i) {
     if (exec_[i]) (void)hipGraphExecDestroy(exec_[i]);
     if (graph_[i]) (void)hipGraphDestroy(graph_[i]);
   }
@@ -270,10 +270,11 @@ int FsEendStream::graph_nodes(int which) const {
 }
 
 void FsEendStream::run(int which, hipStream_t st) {
-  ++runs_[which];
+  if (which != 1) ++runs_[0];
+  if (which != 0) ++runs_[1];
   auto body = [&](hipStream_t s) {
-    if (which == 0) enc_chunk(s);
-    else dec_chunk(s);
+    if (which != 1) enc_chunk(s);
+    if (which != 0) dec_chunk(s);
   };
   if (!use_graph_ || !ran_direct_[which]) {
     // First call (or graphs off): direct launches, which also perform the launchers'
@@ -337,10 +338,12 @@ void FsEendStream::set_audio(const float* mel_fb, int n_mels, int frame_size, in
   }
   const int open_bound[2] = {INT_MAX, INT_MAX};
   SD_HIP(hipMemcpy(bound_, open_bound, sizeof(open_bound), hipMemcpyHostToDevice));
-  // the encoder graph now starts with the frontend: capture it anew
-  if (exec_[0]) (void)hipGraphExecDestroy(exec_[0]);
-  if (graph_[0]) (void)hipGraphDestroy(graph_[0]);
-  exec_[0] = nullptr; graph_[0] = nullptr; ran_direct_[0] = false;
+  // the encoder graphs now start with the frontend: capture them anew
+  for (int i = 0; i < 3; i += 2) {
+    if (exec_[i]) (void)hipGraphExecDestroy(exec_[i]);
+    if (graph_[i]) (void)hipGraphDestroy(graph_[i]);
+    exec_[i] = nullptr; graph_[i] = nullptr; ran_direct_[i] = false;
+  }
   audio_ = true;
 }
 
@@ -361,8 +364,20 @@ int FsEendStream::push_audio(const float* samples, int64_t n, float* preds, int 
   int out = 0;
   while (n_model - n_enc_ >= c_) {
     SD_CHECK(n_enc_ + c_ <= cap_, kErrInvalid, "stream exceeds max_frames");
-    run(0, st);
-    out += after_enc(c_, preds ? preds + (size_t)out * C_ : nullptr, cap - out, st);
+    // steady state: this encoder chunk makes exactly one decoder chunk ready -> both in one graph launch
+    // (SDIAR_NO_COMBINED_GRAPH=1: two launches, for A/B)
+    static const bool no_comb = getenv("SDIAR_NO_COMBINED_GRAPH") != nullptr;
+    const int nv = n_enc_ + c_;
+    if (!no_comb && n_dec_ + c_ + 9 <= nv && n_dec_ + 2 * c_ + 9 > nv) {
+      run(2, st);
+      n_enc_ = nv;
+      n_valid_ = nv;
+      n_dec_ += c_;
+      out += emit(preds ? preds + (size_t)out * C_ : nullptr, cap - out, c_, st);
+    } else {
+      run(0, st);
+      out += after_enc(c_, preds ? preds + (size_t)out * C_ : nullptr, cap - out, st);
+    }
   }
   return out;
 }
@@ -422,9 +437,11 @@ void FsEendStream::reset(hipStream_t st) {
   if (audio_) {   // back to feature rows until set_audio() again (the next capture rebuilds the encoder graph)
     audio_ = false;
     n_samp_ = 0;
-    if (exec_[0]) (void)hipGraphExecDestroy(exec_[0]);
-    if (graph_[0]) (void)hipGraphDestroy(graph_[0]);
-    exec_[0] = nullptr; graph_[0] = nullptr; ran_direct_[0] = false;
+    for (int i = 0; i < 3; i += 2) {
+      if (exec_[i]) (void)hipGraphExecDestroy(exec_[i]);
+      if (graph_[i]) (void)hipGraphDestroy(graph_[i]);
+      exec_[i] = nullptr; graph_[i] = nullptr; ran_direct_[i] = false;
+    }
   }
 }
 

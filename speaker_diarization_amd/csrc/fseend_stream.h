@@ -82,9 +82,11 @@ class FsEendStream {
   int* bound_ = nullptr;               // [0] samples, [1] STFT frames of the input (INT_MAX while open)
   // graphs
   hipStream_t cap_st_ = nullptr;
-  hipGraph_t graph_[2] = {nullptr, nullptr};
-  hipGraphExec_t exec_[2] = {nullptr, nullptr};
-  bool ran_direct_[2] = {false, false};
+  // graphs: 0 encoder chunk, 1 decoder chunk, 2 both back to back (the steady state of an audio stream: one
+  // graph launch per push instead of two)
+  hipGraph_t graph_[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t exec_[3] = {nullptr, nullptr, nullptr};
+  bool ran_direct_[3] = {false, false, false};
   int64_t runs_[2] = {0, 0};
 };
 

@@ -36,6 +36,8 @@ namespace {
 
 constexpr int kMaxQ = 32;
 constexpr int kHD = 64;
+constexpr int kMaxBlk = 32;   // partials per (sequence, head): attn_decode_blocks' cap
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // 16-B row copy; rows of `width16` uint4 units.
 __global__ __launch_bounds__(256) void kv_append_kernel(const uint4* __restrict__ src, int64_t ld_src16, int rows,
@@ -86,14 +88,21 @@ __device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh
     if constexpr (SC1) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, (uint32_t)(i * 4), 0, 16));
     else return a.ws[i];
   };
-  const float mv = lane < nblk ? ld(base + lane * bstride) : -INFINITY;
-  const float lv = lane < nblk ? ld(base + lane * bstride + 1) : 0.f;
+  // every load issued before the first use: one memory round trip for the whole merge (nblk <= 32 by
+  // attn_decode_blocks; rows past nblk re-read the last partial and get weight 0)
+  const float mv0 = ld(base + min(lane, nblk - 1) * bstride);
+  const float lv0 = ld(base + min(lane, nblk - 1) * bstride + 1);
+  float ov[kMaxBlk];
+#pragma unroll
+  for (int b = 0; b < kMaxBlk; ++b) ov[b] = ld(base + min(b, nblk - 1) * bstride + 2 + lane);
+  const float mv = lane < nblk ? mv0 : -INFINITY;
+  const float lv = lane < nblk ? lv0 : 0.f;
   const float M = warp_max(mv);
   const float w = (mv == -INFINITY) ? 0.f : __expf(mv - M);
   const float L = warp_sum(w * lv);
   float o = 0.f;
-#pragma unroll 8
-  for (int b = 0; b < nblk; ++b) o = fmaf(__shfl(w, b, 64), ld(base + b * bstride + 2 + lane), o);
+#pragma unroll
+  for (int b = 0; b < kMaxBlk; ++b) o = fmaf(__shfl(w, b, 64), ov[b], o);
   io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
   st_act(ob, lane, o / L);
 }
@@ -119,24 +128,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
   const int pos = *a.pos;
   const int total = pos + nq;                           // keys present after this chunk's append
   const io_t* qb = reinterpret_cast<const io_t*>(a.q) + (int64_t)s * a.q_seq + h * kHD;
-  for (int i = tid; i < nq * kHD; i += 256) {
-    const int qi = i / kHD, d = i % kHD;
-    qs[qi][d] = ld_act(qb, (int64_t)qi * a.q_tok + d) * a.scale;
-  }
-  __syncthreads();
   const io_t* kb = reinterpret_cast<const io_t*>(a.k) + (int64_t)s * a.kv_seq + h * kHD;
   const io_t* vb = reinterpret_cast<const io_t*>(a.v) + (int64_t)s * a.kv_seq + h * kHD;
   const int half = lane >> 5, d2 = (lane & 31) * 2;
-  float m_run[QMAX], l_run[QMAX], o0[QMAX], o1[QMAX];
-#pragma unroll
-  for (int qi = 0; qi < QMAX; ++qi) { m_run[qi] = -INFINITY; l_run[qi] = 0.f; o0[qi] = 0.f; o1[qi] = 0.f; }
-  for (int t = blockIdx.x * 4 + wid; t * 64 < total; t += gridDim.x * 4) {
-    const int k0 = t * 64, j = k0 + lane;
-    const bool kv = j < total;
-    float kr[kHD];
-    load_row64<IOBF>(kb + (int64_t)min(j, total - 1) * a.kv_tok, kr);
-    // V operands for this tile: keys k0 + 2i + half, dims d2, d2 + 1
-    float v0[32], v1[32];
+  // K row (lane = key) and V operands (keys k0 + 2i + half, dims d2, d2 + 1) of tile t
+  float kr[kHD], v0[32], v1[32];
+  auto load_tile = [&](int t) {
+    const int k0 = t * 64;
+    load_row64<IOBF>(kb + (int64_t)min(k0 + lane, total - 1) * a.kv_tok, kr);
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const int key = min(k0 + 2 * i + half, total - 1);
@@ -151,6 +150,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
         v1[i] = u.y;
       }
     }
+  };
+  // the wave's first tile is in flight while the queries are staged (at short histories a wave has one tile)
+  int t = blockIdx.x * 4 + wid;
+  if (t * 64 < total) load_tile(t);
+  for (int i = tid; i < nq * kHD; i += 256) {
+    const int qi = i / kHD, d = i % kHD;
+    qs[qi][d] = ld_act(qb, (int64_t)qi * a.q_tok + d) * a.scale;
+  }
+  __syncthreads();
+  float m_run[QMAX], l_run[QMAX], o0[QMAX], o1[QMAX];
+#pragma unroll
+  for (int qi = 0; qi < QMAX; ++qi) { m_run[qi] = -INFINITY; l_run[qi] = 0.f; o0[qi] = 0.f; o1[qi] = 0.f; }
+  while (t * 64 < total) {
+    const int j = t * 64 + lane;
+    const bool kv = j < total;
 #pragma unroll
     for (int qi = 0; qi < QMAX; ++qi) {
       if (qi < nq) {
@@ -182,6 +196,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    t += gridDim.x * 4;
+    if (t * 64 < total) load_tile(t);
   }
   // merge the two key-parity halves, park the wave's partial in LDS
 #pragma unroll
@@ -373,11 +389,27 @@ struct WVec {
     if constexpr (WBF) return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
     else return __uint_as_float(w);
   }
+  // weights 2p, 2p + 1 of the vector as an f32 pair (one v_pk_fma_f32 operand)
+  __device__ __forceinline__ static f32x2 pair(const uint4& u, int p) { return f32x2{at(u, 2 * p), at(u, 2 * p + 1)}; }
 };
 
-// stream_slot_block (kernels.h).  grid nh, 512 threads; workgroup h = head h.
+// acc += w . y over VE consecutive inputs as VE / 2 packed-pair FMAs (even / odd inputs in the pair's halves)
+template <int VE>
+__device__ __forceinline__ f32x2 fma_pairs(const f32x2 (&w2)[VE / 2], const float* y, f32x2 acc) {
+#pragma unroll
+  for (int e = 0; e < VE; e += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(y + e);
+    acc = __builtin_elementwise_fma(w2[e / 2], f32x2{q.x, q.y}, acc);
+    acc = __builtin_elementwise_fma(w2[e / 2 + 1], f32x2{q.z, q.w}, acc);
+  }
+  return acc;
+}
+
+// stream_slot_block (kernels.h).  grid nh, 512 threads; workgroup h = head h.  The two projections run
+// weight-vector outer, row inner: a vector is unpacked once for all NR (>= n, padded) rows, and each row's dot
+// is a chain of packed-pair FMAs (rows n..NR-1 read unused LDS rows and are never stored).
 constexpr int kSlotRows = 16, kSlotD = 256;
-template <bool WBF>
+template <bool WBF, int NR>
 __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   using V = WVec<WBF>;
   constexpr int D = kSlotD, VE = V::VE;
@@ -408,26 +440,29 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
     if (h == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
   }
   __syncthreads();
-  {
+  if (wid < 6) {   // 384 threads: (q|k|v column, K half); waves 6, 7 have no column
     const float b = a.b_in[(int64_t)sel * D + h * kHD + d2];
     float(*dst)[kHD] = sel == 0 ? qs : sel == 1 ? ks : vs;
     const float mul = sel == 0 ? a.scale : 1.f;
-    for (int m = 0; m < n; ++m) {   // every lane takes part (the K-half shuffle), threads >= 384 store nothing
-      const float* yr = &ys[m][kh * (D / 2)];
-      float acc = 0.f;
+    f32x2 acc[NR];
 #pragma unroll
-      for (int v = 0; v < NIN; ++v) {
-        float yv[VE];
+    for (int m = 0; m < NR; ++m) acc[m] = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < VE; e += 4) {
-          const float4 q = *reinterpret_cast<const float4*>(yr + v * VE + e);
-          yv[e] = q.x; yv[e + 1] = q.y; yv[e + 2] = q.z; yv[e + 3] = q.w;
-        }
+    for (int v = 0; v < NIN; ++v) {
+      f32x2 w2[VE / 2];
 #pragma unroll
-        for (int e = 0; e < VE; ++e) acc = fmaf(V::at(win[v], e), yv[e], acc);
-      }
-      const float t = acc + __shfl_xor(acc, 1, 64);   // the two K halves
-      if (tid < 6 * kHD && kh == 0) dst[m][d2] = (t + b) * mul;
+      for (int e = 0; e < VE / 2; ++e) w2[e] = V::pair(win[v], e);
+#pragma unroll
+      for (int m = 0; m < NR; ++m) acc[m] = fma_pairs<VE>(w2, &ys[m][kh * (D / 2) + v * VE], acc[m]);
+      asm volatile("" ::: "memory");   // keeps each vector's LDS reads in its own iteration (else they are all hoisted and spill)
+    }
+    // every row stored by every lane (rows n..NR-1 of qs/ks/vs are never read): a store under `m < n` or
+    // `kh == 0` lets the compiler sink the row's whole FMA chain behind the branch and spill the LDS operands
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+      float t = acc[m].x + acc[m].y;
+      t += __shfl_xor(t, 1, 64);   // the two K halves (both lanes of a pair hold the same sum and store it)
+      dst[m][d2] = (t + b) * mul;
     }
   }
   __syncthreads();
@@ -463,15 +498,23 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   // out-projection partial of head h for output feature tid, published write-through
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
   if (tid < D) {
-    for (int m = 0; m < n; ++m) {
-      float p = 0.f;
+    f32x2 acc[NR];
 #pragma unroll
-      for (int v = 0; v < NOUT; ++v)
+    for (int m = 0; m < NR; ++m) acc[m] = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < VE; ++e) p = fmaf(os[m][v * VE + e], V::at(wout[v], e), p);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p), rw, (uint32_t)((((int64_t)h * n + m) * D + tid) * 4),
-                                            0, 16);
+    for (int v = 0; v < NOUT; ++v) {
+      f32x2 w2[VE / 2];
+#pragma unroll
+      for (int e = 0; e < VE / 2; ++e) w2[e] = V::pair(wout[v], e);
+#pragma unroll
+      for (int m = 0; m < NR; ++m) acc[m] = fma_pairs<VE>(w2, &os[m][v * VE], acc[m]);
+      asm volatile("" ::: "memory");
     }
+#pragma unroll
+    for (int m = 0; m < NR; ++m)   // rows >= n: an offset past the buffer's range, the store is dropped (no branch)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[m].x + acc[m].y), rw,
+                                            m < n ? (uint32_t)((((int64_t)h * n + m) * D + tid) * 4) : 0xfffffff0u,
+                                            0, 16);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -525,7 +568,7 @@ void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes,
   SD_LAUNCH_CHECK();
 }
 
-int attn_decode_blocks(int max_keys) { return std::min(cdiv(max_keys, 256), 32); }
+int attn_decode_blocks(int max_keys) { return std::min(cdiv(max_keys, 256), kMaxBlk); }
 
 template <bool IOBF, bool FUSED>
 static void launch_decode_q(const DecodeAttnArgs& a, dim3 g1, hipStream_t st) {
@@ -562,15 +605,24 @@ void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
   else launch_decode<false>(a, nblk, st);
 }
 
+template <int NR>
+static void launch_slot_block(const SlotBlockArgs& a, hipStream_t st) {
+  if (a.w_bf16) hipLaunchKernelGGL((slot_block_kernel<true, NR>), dim3(a.nh), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((slot_block_kernel<false, NR>), dim3(a.nh), dim3(512), 0, st, a);
+  SD_LAUNCH_CHECK();
+}
+
 bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st) {
   static const bool off = getenv("SDIAR_NO_SLOT_BLOCK") != nullptr;   // A/B switch: the three-launch path
   const int n = a.c * a.C;
   if (off || a.D != kSlotD || a.nh * kHD != a.D || a.nh > 8 || n < 1 || n > kSlotRows || a.C > 8 || !a.ws || !a.cnt)
     return false;
   ProfScope prof("slot_block", 2.0 * n * a.D * 4.0 * a.D + 4.0 * n * a.C * a.D, (a.w_bf16 ? 2.0 : 4.0) * 4 * a.D * a.D, st);
-  if (a.w_bf16) hipLaunchKernelGGL(slot_block_kernel<true>, dim3(a.nh), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL(slot_block_kernel<false>, dim3(a.nh), dim3(512), 0, st, a);
-  SD_LAUNCH_CHECK();
+  if (n <= 2) launch_slot_block<2>(a, st);
+  else if (n <= 4) launch_slot_block<4>(a, st);
+  else if (n <= 6) launch_slot_block<6>(a, st);
+  else if (n <= 8) launch_slot_block<8>(a, st);
+  else launch_slot_block<kSlotRows>(a, st);
   return true;
 }
 
