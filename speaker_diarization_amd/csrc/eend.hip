@@ -36,16 +36,24 @@ constexpr int kMaxMels = 64;
 // f + frame0 with frame0 = cursor[0] * sub - context (the first frame a chunk's splice reads) and the
 // sample bound min(n_samples, bound[0]) read from device memory, so one captured graph serves every
 // chunk; the arithmetic per global frame is the whole-recording kernel's, bit for bit.
-template <int LOG2N, bool STREAM>
-__global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
-                                                          int n_frames, int hop, int win_len,
-                                                          const float* __restrict__ mel_fb, int n_mels,
-                                                          double* __restrict__ out, const int* __restrict__ cursor,
-                                                          const int* __restrict__ bound, int sub, int context) {
+// STREAM also stages the mel filters in LDS (the projection's per-bin reads were dependent L2 round trips) and
+// loads the frame's samples before the table prologue.  SPLICE (STREAM, FPB 16: a whole c = 1 chunk's 15
+// logmel frames in one workgroup): the logmel frames stay in LDS and the same workgroup writes the chunk's
+// spliced rows (splice_stream_kernel's arithmetic) -- no second launch.
+template <int LOG2N, bool STREAM, int FPB = 8, bool SPLICE = false>
+__global__ __launch_bounds__(FPB * 64) void stft_logmel_kernel(const float* __restrict__ wav, int64_t n_samples,
+                                                               int n_frames, int hop, int win_len,
+                                                               const float* __restrict__ mel_fb, int n_mels,
+                                                               double* __restrict__ out, const int* __restrict__ cursor,
+                                                               const int* __restrict__ bound, int sub, int context,
+                                                               int rows = 0, float* __restrict__ sout = nullptr,
+                                                               int ld_out = 0) {
   constexpr int N = 1 << LOG2N;
   constexpr int BINS = N / 2 + 1;
-  constexpr int FPB = 8;
+  static_assert(!SPLICE || STREAM, "the fused splice is the streaming frontend's");
   __shared__ double2 buf[FPB][N + N / 16];   // +1 element per 16: padded index pz(i) = i + i / 16
+  __shared__ float melS[STREAM ? kMaxMels * BINS : 1];
+  __shared__ double lmS[SPLICE ? FPB : 1][SPLICE ? kMaxMels : 1];
   // the bit-reversed scatter and the small-stride stages hit a few banks without the pad (PMC: 46 percent of
   // the LDS cycles were bank conflicts); the padded index spreads them, the arithmetic is unchanged
   auto pz = [](int i) { return i + (i >> 4); };
@@ -56,6 +64,23 @@ __global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restric
   const int w = threadIdx.x >> 6;
   const int f = blockIdx.x * FPB + w;
   const bool active = f < n_frames;
+  // Frame f covers padded samples [f*hop, f*hop + N) of the wav zero-padded by N/2;
+  // the periodic Hann window of win_len sits at offset (N - win_len)/2.
+  const int lpad = (N - win_len) / 2;
+  int64_t fg = f;
+  const int64_t cap = n_samples;
+  if constexpr (STREAM) {
+    fg += (int64_t)cursor[0] * sub - context;
+    n_samples = min(n_samples, (int64_t)bound[0]);
+  }
+  const int64_t base = fg * hop - N / 2 + lpad;
+  // the frame's samples, in flight during the table prologue (clamped loads, masked after)
+  float raw[N / 64];
+#pragma unroll
+  for (int u = 0; u < N / 64; ++u) {
+    const int64_t gi = base + (lane + 64 * u) - lpad;
+    raw[u] = cap > 0 ? wav[min(max(gi, (int64_t)0), cap - 1)] : 0.f;
+  }
   for (int k = threadIdx.x; k < N / 2; k += blockDim.x) {
     double s, c;
     sincospi(-2.0 * (double)k / (double)N, &s, &c);
@@ -71,29 +96,34 @@ __global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restric
     mhi[m] = 0;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n_mels * BINS; i += blockDim.x) {
-    const int m = i / BINS, k = i - m * BINS;
-    if (mel_fb[i] != 0.f) {
-      atomicMin(&mlo[m], k);
-      atomicMax(&mhi[m], k + 1);
+  // each filter's nonzero bin range; the filter values' loads issued in batches of 8 (one round trip each)
+  const int nfb = n_mels * BINS;
+  for (int i0 = threadIdx.x; i0 < nfb; i0 += 8 * (int)blockDim.x) {
+    float fv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fv[u] = mel_fb[min(i0 + u * (int)blockDim.x, nfb - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      if (i < nfb) {
+        if constexpr (STREAM) melS[i] = fv[u];
+        if (fv[u] != 0.f) {
+          const int m = i / BINS, k = i - m * BINS;
+          atomicMin(&mlo[m], k);
+          atomicMax(&mhi[m], k + 1);
+        }
+      }
     }
   }
-  // Frame f covers padded samples [f*hop, f*hop + N) of the wav zero-padded by N/2;
-  // the periodic Hann window of win_len sits at offset (N - win_len)/2.
-  const int lpad = (N - win_len) / 2;
-  int64_t fg = f;
-  if constexpr (STREAM) {
-    fg += (int64_t)cursor[0] * sub - context;
-    n_samples = min(n_samples, (int64_t)bound[0]);
-  }
-  const int64_t base = fg * hop - N / 2 + lpad;
-  __syncthreads();   // window table
-  for (int n = lane; n < N; n += 64) {
+  __syncthreads();   // window table, filter ranges
+#pragma unroll
+  for (int u = 0; u < N / 64; ++u) {
+    const int n = lane + 64 * u;
     double v = 0.0;
     const int j = n - lpad;
     if (active && j >= 0 && j < win_len) {
       const int64_t gi = base + j;
-      if (gi >= 0 && gi < n_samples) v = (double)wav[gi] * win[j];
+      if (gi >= 0 && gi < n_samples) v = (double)raw[u] * win[j];
     }
     const int r = (int)(__brev((unsigned)n) >> (32 - LOG2N));
     buf[w][pz(r)] = make_double2(v, 0.0);
@@ -116,15 +146,37 @@ __global__ __launch_bounds__(512) void stft_logmel_kernel(const float* __restric
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (!active) return;
-  for (int m = lane; m < n_mels; m += 64) {
-    const float* fr = mel_fb + (int64_t)m * BINS;
-    double acc = 0.0;
-    for (int k = mlo[m]; k < mhi[m]; ++k) {
-      const double2 c = buf[w][pz(k)];
-      acc = fma((double)fr[k], c.x * c.x + c.y * c.y, acc);
+  if (active) {
+    for (int m = lane; m < n_mels; m += 64) {
+      const float* fr = STREAM ? melS + m * BINS : mel_fb + (int64_t)m * BINS;
+      double acc = 0.0;
+      for (int k = mlo[m]; k < mhi[m]; ++k) {
+        const double2 c = buf[w][pz(k)];
+        acc = fma((double)fr[k], c.x * c.x + c.y * c.y, acc);
+      }
+      const double y = log10(fmax(acc, 1e-10));
+      if constexpr (SPLICE) lmS[w][m] = y;
+      else out[(int64_t)f * n_mels + m] = y;
     }
-    out[(int64_t)f * n_mels + m] = log10(fmax(acc, 1e-10));
+  }
+  if constexpr (SPLICE) {
+    // splice_stream_kernel over this workgroup's frames (local frame r * sub + c of row r)
+    __syncthreads();
+    const int nf = bound[1], i0 = cursor[0];
+    const int width = (2 * context + 1) * n_mels;
+    for (int r = 0; r < rows; ++r) {
+      const int i = i0 + r;
+      const bool row_live = (int64_t)i * sub < (int64_t)nf;
+      for (int e = threadIdx.x; e < ld_out; e += blockDim.x) {
+        float v = 0.f;
+        if (row_live && e < width) {
+          const int c = e / n_mels, m = e % n_mels;
+          const int64_t fgl = (int64_t)i * sub + c - context;
+          if (fgl >= 0 && fgl < nf) v = (float)lmS[r * sub + c][m];
+        }
+        sout[(int64_t)r * ld_out + e] = v;
+      }
+    }
   }
 }
 
@@ -271,6 +323,13 @@ void stream_frontend(const float* wav, int64_t cap_samples, int rows, int n_fft,
   const int n_frames = (rows - 1) * sub + 2 * context + 1;   // logmel frames the chunk's splice reads
   ProfScope prof("stream_frontend", 5.0 * n_fft * std::log2((double)n_fft) * n_frames,
                  4.0 * (double)n_frames * hop + 4.0 * rows * ld_out, st);
+  static const bool two = getenv("SDIAR_FRONTEND_TWO_LAUNCH") != nullptr;   // A/B switch
+  if (n_fft == 256 && n_frames <= 16 && !two) {   // the chunk in one workgroup, splice included
+    hipLaunchKernelGGL((stft_logmel_kernel<8, true, 16, true>), dim3(1), dim3(1024), 0, st, wav, cap_samples, n_frames,
+                       hop, win_len, mel_fb, n_mels, lm, cursor, bound, sub, context, rows, out, ld_out);
+    SD_LAUNCH_CHECK();
+    return;
+  }
   const dim3 grid(cdiv(n_frames, 8));
   if (n_fft == 512)
     hipLaunchKernelGGL((stft_logmel_kernel<9, true>), grid, dim3(512), 0, st, wav, cap_samples, n_frames, hop,

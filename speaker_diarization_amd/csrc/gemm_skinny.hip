@@ -40,6 +40,22 @@ __device__ __forceinline__ void skinny_load(const ConvGemmArgs& p, int n0, int k
   }
 }
 
+// Staging of n float4 units over the 256 threads, loads issued in batches of 8 per thread before any is stored
+// (one memory round trip per batch; a plain strided loop waits on each load or is unrolled with a remainder
+// loop that does).  ld(i) -> float4 for unit i, st(i, v); both called with i clamped to n - 1.
+template <class Ld, class St>
+__device__ __forceinline__ void stage4(int n, int tid, Ld ld, St st) {
+  for (int i0 = tid; i0 < n; i0 += 8 * 256) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld(min(i0 + u * 256, n - 1));
+    // units past n store unit n - 1's value again (unconditional stores: a store under a branch lets the
+    // compiler sink its load behind the branch, one round trip per unit again)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) st(min(i0 + u * 256, n - 1), v[u]);
+  }
+}
+
 template <int MMAX, int NC, bool WBF>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M, int a_rs) {
   extern __shared__ float As[];
@@ -138,27 +154,39 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(ConvGemmArgs p, int M,
       }
     }
   } else if (p.pro_mode == 2) {
-    // slot_init: row r = t * C + c is ln_x[t] + pro_p[c]
-    for (int i = tid; i < M * K; i += 256) {
-      const int r = i / K, d = i - r * K;
-      const float y = p.ln_x[(int64_t)(r / p.pro_C) * K + d] + p.pro_p[(int64_t)(r % p.pro_C) * K + d];
-      As[i] = y;
-      if (blockIdx.x == 0) p.ln_out[i] = y;
-    }
+    // slot_init: row r = t * C + c is ln_x[t] + pro_p[c] (float4 units, K % 8 == 0)
+    const int kv4 = K / 4;
+    stage4(M * kv4, tid, [&](int i) {
+      const int r = i / kv4, d = (i - r * kv4) * 4;
+      const float4 x = *reinterpret_cast<const float4*>(p.ln_x + (int64_t)(r / p.pro_C) * K + d);
+      const float4 b = *reinterpret_cast<const float4*>(p.pro_p + (int64_t)(r % p.pro_C) * K + d);
+      return make_float4(x.x + b.x, x.y + b.y, x.z + b.z, x.w + b.w);
+    }, [&](int i, float4 y) {
+      *reinterpret_cast<float4*>(As + 4 * i) = y;
+      if (blockIdx.x == 0) *reinterpret_cast<float4*>(p.ln_out + 4 * (int64_t)i) = y;
+    });
   } else if (p.pro_mode == 3) {
     // gather_window: staged row r is history row *cursor - pad + r, zero outside [0, *n_valid)
-    const int base = *p.pro_cursor - p.pro_pad, nv = *p.pro_nvalid;
-    for (int i = tid; i < span; i += 256) {
-      const int r = i / p.lda, d = i - r * p.lda;
+    // (float4 units: lda % 4 == 0; rows outside read a clamped row and are replaced by zeros)
+    const int base = *p.pro_cursor - p.pro_pad, nv = *p.pro_nvalid, ld4 = p.lda / 4;
+    stage4(span / 4, tid, [&](int i) {
+      const int r = i / ld4, d = (i - r * ld4) * 4;
       const int src = base + r;
-      As[i] = (src >= 0 && src < nv) ? p.ln_x[(int64_t)src * p.lda + d] : 0.f;
-    }
+      const float4 v = *reinterpret_cast<const float4*>(p.ln_x + (int64_t)min(max(src, 0), max(nv - 1, 0)) * p.lda + d);
+      return (src >= 0 && src < nv) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }, [&](int i, float4 y) { *reinterpret_cast<float4*>(As + 4 * i) = y; });
   } else if (p.a_bf16) {
-    const uint16_t* a = static_cast<const uint16_t*>(p.A) + p.a_coff;
-    for (int i = tid; i < span; i += 256) As[i] = bf_bits2f(a[i]);
+    // 4 bf16 (8 B) per unit: a_coff % 4 == 0, span % 4 == 0
+    const uint2* a = reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.A) + p.a_coff);
+    stage4(span / 4, tid, [&](int i) {
+      const uint2 u = a[i];
+      return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                         __uint_as_float(u.y & 0xffff0000u));
+    }, [&](int i, float4 y) { *reinterpret_cast<float4*>(As + 4 * i) = y; });
   } else {
-    const float* a = static_cast<const float*>(p.A) + p.a_coff;
-    for (int i = tid; i < span; i += 256) As[i] = a[i];
+    const float4* a = reinterpret_cast<const float4*>(static_cast<const float*>(p.A) + p.a_coff);
+    stage4(span / 4, tid, [&](int i) { return a[i]; },
+           [&](int i, float4 y) { *reinterpret_cast<float4*>(As + 4 * i) = y; });
   }
   __syncthreads();
   if (!active) return;
@@ -294,6 +322,11 @@ bool gemm_skinny_supported(const ConvGemmArgs& p) {
     if (p.pro_mode == 3 && (!p.pro_cursor || !p.pro_nvalid)) return false;
     if (p.pro_mode > 3) return false;
   }
+  // the vectorised staging: 16-B (fp32) / 8-B (bf16) A units, 16-B prologue rows
+  auto al = [](const void* q, int b) { return reinterpret_cast<uintptr_t>(q) % b == 0; };
+  if (p.pro_mode == 0 && !p.ln_g && !al(p.A, p.a_bf16 ? 8 : 16)) return false;
+  if ((p.pro_mode == 2 || p.pro_mode == 3) && !al(p.ln_x, 16)) return false;
+  if (p.pro_mode == 2 && !al(p.pro_p, 16)) return false;
   return p.a_coff % 4 == 0 && rs % 4 == 0;
 }
 

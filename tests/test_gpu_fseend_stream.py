@@ -360,3 +360,39 @@ def test_gemm_prologues_bit_identical(gpu, precision, tmp_path):
         res.append(torch.load(path, weights_only=True))
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
+
+
+AUD = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+import tests.test_gpu_fseend_stream as t
+m = t._model(809, {prec!r}, max_frames=400)
+wav = t._wav8k(20.0, 96, 11)
+outs = [t._audio_stream(m, wav, c, [640])[0].cpu() for c in (1, 2)]
+torch.save(outs, {path!r})
+"""
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_audio_fusions_bit_identical(gpu, precision, tmp_path):
+    """The c = 1 audio chunk's STFT / logmel / splice in one workgroup (stft_logmel_kernel SPLICE) and the
+    encoder + decoder chunks in one captured graph per steady-state push: 80-ms audio streams (chunks 1 and
+    2) are bit-identical with SDIAR_FRONTEND_TWO_LAUNCH=1 SDIAR_NO_COMBINED_GRAPH=1 (the two-launch frontend,
+    one graph per chunk)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for off in (None, "1"):
+        env = dict(os.environ)
+        for k in ("SDIAR_FRONTEND_TWO_LAUNCH", "SDIAR_NO_COMBINED_GRAPH"):
+            env.pop(k, None)
+            if off:
+                env[k] = off
+        path = str(tmp_path / f"a_{off}.pt")
+        r = subprocess.run([sys.executable, "-c", AUD.format(repo=repo, prec=precision, path=path)], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(torch.load(path, weights_only=True))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
