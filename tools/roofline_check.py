@@ -58,8 +58,10 @@ def main(d):
         if r.get("unit") == "us/push":
             tot = sum(float(x["TotalDurationNs"]) for x in rows)
             mdl = r.get("model", {})
+            pushes = L["config"].get("pushes_per_step", 0) * (L["steps"] + L["warmup"])
             out.append(f"{wl}: latency model {r['peak']} us floor / p50 {r['achieved']} us = frac {r['frac']} "
-                       f"(line); rocprof device time {tot / 1e3:.0f} us over the profiled run, "
+                       f"(line); rocprof device time {tot / 1e3:.0f} us over the profiled run = "
+                       f"{tot / 1e3 / max(pushes, 1):.1f} us of kernels per push ({pushes} pushes), "
                        f"device ops per push {mdl.get('device_ops_per_push')}, boundary {mdl.get('kernel_boundary_us')} us")
             continue
         calls, total = group(rows, r["kernel"])
