@@ -421,6 +421,14 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int h = blockIdx.x, n = a.c * a.C, C = a.C;
+#ifdef SDIAR_SLOT_STAMPS   // probe build only: phase stamps (100 MHz), printed by thread 0 every 997th launch
+  unsigned long long stv[8];
+  int nst = 0;
+  auto stamp = [&] { stv[nst++] = __builtin_amdgcn_s_memrealtime(); };
+#else
+  auto stamp = [] {};
+#endif
+  stamp();
   // thread t < 384: in-projection row (t / 2 / 64) * D + h * 64 + (t / 2) % 64, K half t % 2;
   // thread t < 256: out-projection row t, the head's 64 inputs
   // (unconditional, clamped loads: arrays filled under a branch end up in scratch)
@@ -440,6 +448,7 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
     if (h == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
   }
   __syncthreads();
+  stamp();
   if (wid < 6) {   // 384 threads: (q|k|v column, K half); waves 6, 7 have no column
     const float b = a.b_in[(int64_t)sel * D + h * kHD + d2];
     float(*dst)[kHD] = sel == 0 ? qs : sel == 1 ? ks : vs;
@@ -466,6 +475,7 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
     }
   }
   __syncthreads();
+  stamp();
   // scores of row m = f * C + i against the C slots of frame f, softmax per row
   for (int t = tid; t < n * C; t += 512) {
     const int m = t / C, j = t % C, kr = (m / C) * C + j;
@@ -495,6 +505,7 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
     os[m][d] = o;
   }
   __syncthreads();
+  stamp();
   // out-projection partial of head h for output feature tid, published write-through
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
   if (tid < D) {
@@ -518,12 +529,32 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  stamp();
+  unsigned arrival = 0;
   if (tid == 0) {
     const unsigned nh = gridDim.x;
-    last = (__hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % nh) == nh - 1;
+    arrival = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (arrival % nh) == nh - 1;
   }
   __syncthreads();
-  if (!last || tid >= D) return;
+  stamp();
+#ifdef SDIAR_SLOT_STAMPS
+  auto report = [&] {
+    if (tid == 0 && (arrival / gridDim.x) % 997 == 5)
+      printf("SLOTSTAMP h %d last %d ln %llu inproj %llu attn %llu outproj %llu arrive %llu merge %llu\n", h, (int)last,
+             stv[1] - stv[0], stv[2] - stv[1], stv[3] - stv[2], stv[4] - stv[3], stv[5] - stv[4],
+             nst > 6 ? stv[6] - stv[5] : 0ull);
+  };
+  if (!last) { report(); return; }
+#else
+  (void)arrival;
+#endif
+  if (!last || tid >= D) {
+#ifdef SDIAR_SLOT_STAMPS
+    if (tid == 0) { stamp(); report(); }
+#endif
+    return;
+  }
   const float bo = a.b_out[tid];
   const int nh = gridDim.x;
   for (int m = 0; m < n; ++m) {
@@ -541,6 +572,9 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
     if (a.out_bf16) static_cast<uint16_t*>(a.out)[(int64_t)m * D + tid] = f2bf_bits(v);
     else static_cast<float*>(a.out)[(int64_t)m * D + tid] = v;
   }
+#ifdef SDIAR_SLOT_STAMPS
+  if (tid == 0) { stamp(); report(); }
+#endif
 }
 
 __global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
