@@ -432,6 +432,22 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   // thread t < 384: in-projection row (t / 2 / 64) * D + h * 64 + (t / 2) % 64, K half t % 2;
   // thread t < 256: out-projection row t, the head's 64 inputs
   // (unconditional, clamped loads: arrays filled under a branch end up in scratch)
+  // this wave's first LN row (x + t) and the LN affine issued ahead of the weights: the LN waits on these
+  // alone while the weight slices stream on behind it (loads return in issue order)
+  // (no load behind a branch and no use of them before the weights are issued: both t dtypes are read through
+  // bounded buffer descriptors, out-of-range and absent t read as 0, and the dtype is picked afterwards)
+  const int r0 = min(wid, n - 1);
+  const uint32_t eoff = (uint32_t)(r0 * D + lane * 4);
+  const float4 xr0 = *reinterpret_cast<const float4*>(a.ln_x + eoff);
+  const uint32_t tbytes = a.ln_t ? (uint32_t)(n * D * (a.t_bf16 ? 2 : 4)) : 0u;
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ln_t ? a.ln_t : static_cast<const void*>(a.ln_x)), (short)0,
+                                        tbytes, 0x00020000);
+  const u32x2_t tb = __builtin_amdgcn_raw_buffer_load_b64(rt, eoff * 2, 0, 0);
+  const u32x4_t tf = __builtin_amdgcn_raw_buffer_load_b128(rt, eoff * 4, 0, 0);
+  const float4 lg = *reinterpret_cast<const float4*>(a.ln_g + lane * 4);
+  const float4 lb = *reinterpret_cast<const float4*>(a.ln_b + lane * 4);
+  __builtin_amdgcn_sched_barrier(0);   // these loads stay ahead of the weight slices
   const int r2 = min(tid, 6 * kHD - 1) >> 1, kh = tid & 1, sel = r2 / kHD, d2 = r2 % kHD;
   const int64_t rin = ((int64_t)sel * D + h * kHD + d2) * D + kh * (D / 2);
   const int64_t rout = (int64_t)(tid & (D - 1)) * D + h * kHD;
@@ -440,14 +456,42 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   for (int v = 0; v < NIN; ++v) win[v] = V::load(a.w_in, rin + v * VE);
 #pragma unroll
   for (int v = 0; v < NOUT; ++v) wout[v] = V::load(a.w_out, rout + v * VE);
-  // y = LN(x + t): one wave per row (every workgroup; workgroup 0 stores the residual stream)
-  for (int r = wid; r < n; r += 8) {
+  __builtin_amdgcn_sched_barrier(0);   // ... and all are issued before the LN's first wait
+  // the LN operands enter here (an empty asm that may change them): no LN arithmetic is hoisted above the
+  // weight loads, so the wait for its inputs leaves the weights in flight
+  float4 xa0 = xr0;
+  u32x2_t tbv = tb;
+  u32x4_t tfv = tf;
+  asm volatile("" : "+v"(xa0.x), "+v"(xa0.y), "+v"(xa0.z), "+v"(xa0.w), "+v"(tbv), "+v"(tfv));
+  // y = LN(x + t): one wave per row (every workgroup; workgroup 0 stores the residual stream); ln_row's
+  // arithmetic on the prefetched first row, ln_row itself for rows past the 8 waves
+  {   // every wave (waves past n redo row n - 1 and store the same values again)
+    // x + t with t's dtype selected (not branched on); an absent t reads as zeros
+    const bool tb16 = a.t_bf16;
+    float4 xa = xa0;
+    xa.x += tb16 ? __uint_as_float(tbv[0] << 16) : __uint_as_float(tfv[0]);
+    xa.y += tb16 ? __uint_as_float(tbv[0] & 0xffff0000u) : __uint_as_float(tfv[1]);
+    xa.z += tb16 ? __uint_as_float(tbv[1] << 16) : __uint_as_float(tfv[2]);
+    xa.w += tb16 ? __uint_as_float(tbv[1] & 0xffff0000u) : __uint_as_float(tfv[3]);
+    const float mean = warp_sum((xa.x + xa.y) + (xa.z + xa.w)) / (float)D;
+    const float dx = xa.x - mean, dy = xa.y - mean, dz = xa.z - mean, dw = xa.w - mean;
+    const float rstd = rsqrtf(warp_sum((dx * dx + dy * dy) + (dz * dz + dw * dw)) / (float)D + a.eps);
+    float4 y;
+    y.x = (xa.x - mean) * rstd * lg.x + lb.x;
+    y.y = (xa.y - mean) * rstd * lg.y + lb.y;
+    y.z = (xa.z - mean) * rstd * lg.z + lb.z;
+    y.w = (xa.w - mean) * rstd * lg.w + lb.w;
+    *reinterpret_cast<float4*>(&ys[r0][lane * 4]) = y;
+    if (h == 0) *reinterpret_cast<float4*>(a.ln_out + eoff) = y;
+  }
+  for (int r = wid + 8; r < n; r += 8) {
     float4 y[4];
     ln_row(a.ln_x + (int64_t)r * D, a.ln_t, a.t_bf16, (int64_t)r * D, a.ln_g, a.ln_b, a.eps, D, lane, y);
     *reinterpret_cast<float4*>(&ys[r][lane * 4]) = y[0];
     if (h == 0) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
   }
-  __syncthreads();
+  // LDS-only barrier: __syncthreads()' workgroup fence would also wait for the weight slices still in flight
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   stamp();
   if (wid < 6) {   // 384 threads: (q|k|v column, K half); waves 6, 7 have no column
     const float b = a.b_in[(int64_t)sel * D + h * kHD + d2];
@@ -557,20 +601,26 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   }
   const float bo = a.b_out[tid];
   const int nh = gridDim.x;
-  for (int m = 0; m < n; ++m) {
-    float pv[8];
+  // every row's head partials loaded before the first sum (one round trip);
+  // rows past n re-read row n - 1 and store its value again (no load behind a branch)
+  constexpr int NHM = kSlotD / kHD;   // = nh (the launch requires nh * 64 == D == kSlotD)
+  float pv[NR][NHM];
 #pragma unroll
-    for (int hh = 0; hh < 8; ++hh)   // nh <= 8 (D / 64 with D = 256: 4); all loads issued before the sum
-      pv[hh] = hh < nh ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                             rw, (uint32_t)((((int64_t)hh * n + m) * D + tid) * 4), 0, 16))
-                       : 0.f;
+  for (int m = 0; m < NR; ++m)
+#pragma unroll
+    for (int hh = 0; hh < NHM; ++hh)
+      pv[m][hh] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rw, (uint32_t)((((int64_t)min(hh, nh - 1) * n + min(m, n - 1)) * D + tid) * 4), 0, 16));
+#pragma unroll
+  for (int m = 0; m < NR; ++m) {
     float v = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 8; ++hh)
-      if (hh < nh) v += pv[hh];
+    for (int hh = 0; hh < NHM; ++hh)
+      if (hh < nh) v += pv[m][hh];
     v += bo;
-    if (a.out_bf16) static_cast<uint16_t*>(a.out)[(int64_t)m * D + tid] = f2bf_bits(v);
-    else static_cast<float*>(a.out)[(int64_t)m * D + tid] = v;
+    const int64_t o = (int64_t)min(m, n - 1) * D + tid;
+    if (a.out_bf16) static_cast<uint16_t*>(a.out)[o] = f2bf_bits(v);
+    else static_cast<float*>(a.out)[o] = v;
   }
 #ifdef SDIAR_SLOT_STAMPS
   if (tid == 0) { stamp(); report(); }
