@@ -652,7 +652,13 @@ void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes,
   SD_LAUNCH_CHECK();
 }
 
-int attn_decode_blocks(int max_keys) { return std::min(cdiv(max_keys, 256), kMaxBlk); }
+int attn_decode_blocks(int max_keys) {
+  static const int cap = [] {   // A/B: SDIAR_DECODE_MAXBLK=<1..32> caps the blocks per (sequence, head)
+    const char* e = getenv("SDIAR_DECODE_MAXBLK");
+    return e ? std::max(1, std::min(atoi(e), kMaxBlk)) : kMaxBlk;
+  }();
+  return std::min(cdiv(max_keys, 256), cap);
+}
 
 template <bool IOBF, bool FUSED>
 static void launch_decode_q(const DecodeAttnArgs& a, dim3 g1, hipStream_t st) {
