@@ -85,11 +85,15 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref_speech, const float* target_s
  * calls it after forward(), so the failing forward itself raises (RuntimeError); an
  * uncollected report is raised by the handle's next forward at the latest. */
 int sd_tsvad_status(sd_tsvad* h, void* stream);
-/* Windows per reference forward call (the collater's batch, e.g. infer.py's batch of 64) when one device
- * forward covers several of them: the scope of BatchNorm1D's NaN bypass (ts_vad2/model.py:161-171) — a window
- * with a non-finite input makes the reference skip speech_down_or_up's (and, variant 0, backend_down's)
- * BatchNorm for every window of ITS batch.  0 (default): the whole sd_tsvad_forward call is one batch. */
-int sd_tsvad_set_forward_batch(sd_tsvad* h, int windows);
+/* sd_tsvad_forward with the scope of BatchNorm1D's NaN bypass (ts_vad2/model.py:161-171) given per call (no
+ * handle state): a window with a non-finite input makes the reference skip speech_down_or_up's (and, variant 0,
+ * backend_down's) BatchNorm for every window of ITS batch.  forward_batch: windows per reference forward call
+ * (the collater's batch, e.g. infer.py's 64) when this call covers several; 0: the call is one batch.
+ * force: this call is a slice of a larger reference batch whose non-finite input lies in another slice —
+ * bit 0: a non-finite fbank (both BatchNorms skipped for every window), bit 1: a non-finite variant-0
+ * target-speaker embedding (backend_down's skipped).  sd_tsvad_forward = forward_batch 0, force 0. */
+int sd_tsvad_forward_batched(sd_tsvad* h, const float* ref_speech, const float* target_speech, int B, int T_fbank,
+                             int T_label, int forward_batch, int force, float* logits, void* stream);
 int64_t sd_tsvad_device_bytes(const sd_tsvad* h);
 /* Diagnostics only (not on the product path, which launches directly): capture sd_tsvad_forward once into a
  * hipGraph, optionally write its DOT dump to `dot_path`, replay it `replays` times on `stream` (each replay
@@ -328,6 +332,10 @@ int64_t sd_fseend_stream_device_bytes(const sd_fseend_stream* s);
  * node count of each captured chunk graph (0 before the capture). */
 int sd_fseend_stream_stats(const sd_fseend_stream* s, int64_t* enc_runs, int64_t* dec_runs, int* enc_nodes,
                            int* dec_nodes);
+/* Diagnostics: the decode attention's per-(slot, head) block-merge counters, then the slot block's arrival
+ * counter, copied to host_out (at most cap) after `stream` drains; *n = how many there are.  Each runs
+ * 0..blocks-1 by a wrapping increment and is 0 between launches (test_gpu_fseend_stream.py). */
+int sd_fseend_stream_debug_counters(const sd_fseend_stream* s, unsigned* host_out, int cap, int* n, void* stream);
 int sd_fseend_stream_destroy(sd_fseend_stream* s);
 
 /* feature.stft + feature.transform('logmel23_mn' | 'logmel23') + feature.splice + [::subsampling]

@@ -120,7 +120,8 @@ _SIGS = {
     "sd_tsvad_finalize": (c_int, [c_void_p]),
     "sd_tsvad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sd_tsvad_status": (c_int, [c_void_p, c_void_p]),
-    "sd_tsvad_set_forward_batch": (c_int, [c_void_p, c_int]),
+    "sd_tsvad_forward_batched": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                         c_void_p]),
     "sd_tsvad_forward_graph": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_char_p,
                                        c_void_p]),
     "sd_tsvad_debug_buffer": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_int64)]),
@@ -171,6 +172,7 @@ _SIGS = {
     "sd_fseend_stream_reset": (c_int, [c_void_p, c_void_p]),
     "sd_fseend_stream_device_bytes": (c_int64, [c_void_p]),
     "sd_fseend_stream_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int), POINTER(c_int)]),
+    "sd_fseend_stream_debug_counters": (c_int, [c_void_p, POINTER(ctypes.c_uint), c_int, POINTER(c_int), c_void_p]),
     "sd_fseend_stream_destroy": (c_int, [c_void_p]),
     "sd_eend_features": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p, c_int, c_void_p]),

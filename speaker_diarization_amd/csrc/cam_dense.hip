@@ -100,9 +100,10 @@ struct CamDenseArgs {
   const float *w1, *c1, *w2, *c2;   // CAMLayer linear1 (64 x 128) / linear2 (32 x 64) + biases, fp32
   uint16_t* out;            // channel slice [cin, cin + 32) of the same map (stride ld)
   uint8_t* xr;              // [B][kXBytes] exchange records
-  unsigned* cnt;            // [B][kCnt] counters (zeroed once at allocation, monotonic)
+  unsigned* cnt;            // [B][kCnt] counters (zeroed once at allocation; compared by wrap-safe differences)
   unsigned long long* stamps;   // PROBE: [grid][16] s_memrealtime stamps of the phase boundaries
   int meet_ticks;           // the first part's wait for the other (100 MHz ticks; 0 forces the hand-over)
+  int* err;                 // device address of a pinned host flag: set when an item's parts lost each other
 };
 
 template <bool PROBE>
@@ -529,8 +530,10 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
   }
 
   stamp(5);
+  // arrivals count up by two per launch (u32, wrapping): the first part of a launch gets an even value a, the
+  // last a + 1; the decision word then holds a + 2 (met) or a + 3 (handed over), which no earlier launch
+  // wrote, so every comparison below is a wrap-safe difference or equality
   const unsigned arrived = (unsigned)bcast[0];
-  const unsigned epoch = (arrived >> 1) + 1u;          // 1-based index of this launch for the item
   const bool first = !(arrived & 1u);
   if (first) {
     // First to arrive: wait a bounded time (10 us) for the other part, which was dispatched next to this one
@@ -541,14 +544,14 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
       const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + (unsigned long long)a.meet_ticks;
       int met = 0;
       for (;;) {
-        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= arrived + 2u) {
+        if ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - arrived) >= 2) {
           met = 1;
           break;
         }
         if (__builtin_amdgcn_s_memrealtime() > deadline) break;
         __builtin_amdgcn_s_sleep(2);
       }
-      if (met) __hip_atomic_store(cnt + 1, 2u * epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // self
+      if (met) __hip_atomic_store(cnt + 1, arrived + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // self
       bcast[1] = met;
     }
     barrier();
@@ -565,7 +568,7 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       barrier();
       stamp(6);
-      if (tid == 0) __hip_atomic_store(cnt + 1, 2u * epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // handed over
+      if (tid == 0) __hip_atomic_store(cnt + 1, arrived + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // handed over
       stamp(9);
       stamp_out();
       return;
@@ -621,7 +624,8 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
   if (tid == 0) {
     unsigned spins = 0, d = 0;
     int lost = 0;
-    while (((d = __hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) < epoch) {
+    const unsigned want = arrived + 1u;   // the first part's arrival + 2
+    while (((d = __hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~1u) != want) {
       if (++spins > (1u << 24)) {   // cannot happen by construction; never hang the GPU on a broken invariant
         lost = 1;
         break;
@@ -629,6 +633,8 @@ __global__ __launch_bounds__(kThreads, 2) void cam_dense_kernel(CamDenseArgs a) 
       __builtin_amdgcn_s_sleep(1);
     }
     bcast[1] = lost ? 2 : (int)(d & 1u);
+    // sticky report to the handle (system scope: a pinned host word), raised by its next status / forward
+    if (lost && a.err) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   barrier();
   stamp(8);
@@ -698,7 +704,7 @@ size_t cam_dense_counter_bytes(int B) { return (size_t)B * kCnt * sizeof(unsigne
 void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
                const float* c1, const float* w2, const float* c2, void* out, void* records, unsigned* counters,
-               hipStream_t st) {
+               hipStream_t st, int* err) {
   SD_CHECK(B >= 1 && T >= 1 && T <= kMaxT, kErrInvalid, "cam_dense: bad item shape");
   SD_CHECK((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0, kErrInvalid,
            "cam_dense: misaligned map");
@@ -719,7 +725,7 @@ void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const floa
                  2.0 * B * T * ((double)cin + kC2) + 2.0 * kC * cin, st);
   CamDenseArgs a{static_cast<const uint16_t*>(x), ld, cin, T, dil, B, s1, h1, static_cast<const uint16_t*>(wb), a2, b2,
                  static_cast<const uint16_t*>(wl), bl, w1, c1, w2, c2, static_cast<uint16_t*>(out),
-                 static_cast<uint8_t*>(records), counters, g_cam_probe, meet_ticks()};
+                 static_cast<uint8_t*>(records), counters, g_cam_probe, meet_ticks(), err};
   if (g_cam_probe)
     hipLaunchKernelGGL(cam_dense_kernel<true>, dim3(split ? 2 * B : B), dim3(kThreads), kSmemBytes, st, a);
   else

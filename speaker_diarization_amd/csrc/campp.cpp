@@ -255,7 +255,7 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
         // the whole layer per item in one launch, the 128-channel bottleneck kept in LDS (cam_dense.hip)
         cam_dense(D.p, B, T2, ld, cin, L.dil, L.bottleneck.pre_s, L.bottleneck.pre_h, L.bottleneck.w.w,
                   L.bottleneck.alpha, L.bottleneck.beta, L.local.w.w, L.local.beta, L.c1w, L.c1b, L.c2w, L.c2b,
-                  act_at(D, cin).p, dense_rec, dense_cnt, st);
+                  act_at(D, cin).p, dense_rec, dense_cnt, st, err_.get(0));
         cin += L.local.w.N;
         continue;
       }
@@ -317,6 +317,7 @@ void CamppModel::finalize() {
 
 void CamppModel::forward(const float* fbank, int B, int Tf, float* emb, float* time_out, hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
+  trunk_.raise_if_set();   // an earlier call's cam_dense report
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_frames, kErrInvalid, "fbank frames exceed max_frames");
   const Tens x4 = trunk_.forward(fbank, B, Tf, st);

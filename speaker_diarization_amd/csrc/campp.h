@@ -43,6 +43,11 @@ class CamTrunk {
   const float* out_s() const { return out_s_; }
   const float* out_h() const { return out_h_; }
   bool bf16() const { return bf16_; }
+  // kErrHip if a cam_dense launch of an earlier forward lost a split item's exchange (its outputs are NaN;
+  // cannot happen by construction, reported instead of hanging the GPU)
+  void raise_if_set() const {
+    err_.raise_if_set("cam_dense: the two parts of a split item lost their exchange (outputs poisoned with NaN)");
+  }
 
  private:
   float* ws(DeviceArena& a, size_t n) { return static_cast<float*>(a.alloc(n * sizeof(float))); }
@@ -61,6 +66,7 @@ class CamTrunk {
   float *d_[3] = {nullptr, nullptr, nullptr}, *x4_ = nullptr, *tmp_ = nullptr, *gate_ = nullptr;
   void* dense_rec_ = nullptr;          // cam_dense exchange records, one per window
   unsigned* dense_cnt_ = nullptr;      // cam_dense counters, one set per window (zeroed once)
+  mutable PinnedFlags err_;            // cam_dense's sticky lost-exchange report (slot 0)
 };
 
 struct CamppConfig {

@@ -190,10 +190,11 @@ int sd_tsvad_status(sd_tsvad* h, void* stream) {
   });
 }
 
-int sd_tsvad_set_forward_batch(sd_tsvad* h, int windows) {
+int sd_tsvad_forward_batched(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl,
+                             int forward_batch, int force, float* logits, void* stream) {
   return guard([&] {
-    SD_CHECK(h && windows >= 0, sd::kErrInvalid, "set_forward_batch: bad argument");
-    h->model->set_forward_batch(windows);
+    SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
+    h->model->forward(ref, ts, B, Tf, Tl, logits, S(stream), forward_batch, force);
   });
 }
 
@@ -391,6 +392,13 @@ int sd_fseend_stream_stats(const sd_fseend_stream* s, int64_t* enc_runs, int64_t
     *dec_runs = s->s->runs(1);
     *enc_nodes = s->s->graph_nodes(0);
     *dec_nodes = s->s->graph_nodes(1);
+  });
+}
+
+int sd_fseend_stream_debug_counters(const sd_fseend_stream* s, unsigned* host_out, int cap, int* n, void* stream) {
+  return guard([&] {
+    SD_CHECK(s && n && (host_out || cap == 0), sd::kErrInvalid, "null argument");
+    *n = s->s->debug_counters(host_out, cap, S(stream));
   });
 }
 

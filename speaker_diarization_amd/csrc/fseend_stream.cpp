@@ -427,8 +427,20 @@ int FsEendStream::flush(float* preds, int cap, hipStream_t st) {
   return out;
 }
 
+int FsEendStream::debug_counters(unsigned* host, int cap, hipStream_t st) const {
+  const int nd = C_ * m_.cfg_.n_heads;
+  SD_HIP(hipStreamSynchronize(st));
+  if (cap > 0) SD_HIP(hipMemcpy(host, dcnt_, (size_t)std::min(cap, nd) * sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (cap > nd) SD_HIP(hipMemcpy(host + nd, scnt_, sizeof(unsigned), hipMemcpyDeviceToHost));
+  return nd + 1;
+}
+
 void FsEendStream::reset(hipStream_t st) {
   SD_HIP(hipMemsetAsync(state_, 0, 4 * sizeof(int), st));
+  // the block-merge counters return to 0 after every complete launch (wrapping increment); zeroing them here
+  // also clears what an interrupted launch may have left
+  SD_HIP(hipMemsetAsync(dcnt_, 0, (size_t)C_ * m_.cfg_.n_heads * sizeof(unsigned), st));
+  SD_HIP(hipMemsetAsync(scnt_, 0, sizeof(unsigned), st));
   // wait for the chunks flush() / push*() enqueued: they read bound_ and replay the graphs destroyed below,
   // and set_audio() rewrites bound_ with a synchronous copy that is not ordered after a non-blocking st
   SD_HIP(hipStreamSynchronize(st));

@@ -42,6 +42,9 @@ class FsEendStream {
   int64_t runs(int which) const { return runs_[which]; }
   int graph_nodes(int which) const;
   size_t device_bytes() const { return arena_.total(); }
+  // diagnostics: the block-merge counters (attn_decode's C * n_heads, then the slot block's one) copied to the
+  // host after `st` drains; returns how many there are (writes at most cap)
+  int debug_counters(unsigned* host, int cap, hipStream_t st) const;
 
  private:
   void enc_chunk(hipStream_t st);
@@ -65,9 +68,9 @@ class FsEendStream {
   // staging (chunk-sized)
   float *F_ = nullptr, *Y_ = nullptr, *X_ = nullptr, *W_ = nullptr, *Yc_ = nullptr, *E_ = nullptr;
   float *X2_ = nullptr, *A2_ = nullptr, *G_ = nullptr, *A_ = nullptr, *P_ = nullptr, *ws_ = nullptr;
-  unsigned* dcnt_ = nullptr;           // attn_decode's per-(sequence, head) block counters (zeroed once)
+  unsigned* dcnt_ = nullptr;           // attn_decode's per-(sequence, head) block counters (0..nblk-1, wrap)
   float* sws_ = nullptr;               // stream_slot_block's per-head out-projection partials
-  unsigned* scnt_ = nullptr;           // its arrival counter (zeroed once)
+  unsigned* scnt_ = nullptr;           // its arrival counter (0..n_heads-1, wraps per launch)
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

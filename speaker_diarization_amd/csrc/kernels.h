@@ -150,7 +150,7 @@ size_t cam_dense_counter_bytes(int B);
 void cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                const void* wb, const float* a2, const float* b2, const void* wl, const float* bl, const float* w1,
                const float* c1, const float* w2, const float* c2, void* out, void* records, unsigned* counters,
-               hipStream_t st);
+               hipStream_t st, int* err = nullptr);   // err: device address of a PinnedFlags slot (lost exchange)
 bool cam_local_fused_supported(int C, int C1, int C2, int N, int taps, int dil, int seg_len, int ldo, bool bf16);
 void cam_local_fused(const void* x, int B, int T, int dil, const void* wt, const float* bias, const float* w1,
                      const float* b1, const float* w2, const float* b2, void* out, int ldo, hipStream_t st);
@@ -302,6 +302,7 @@ void mean_sigmoid_affine(const float* x, int rows, int T, int ldx, const float* 
 // Stream-ordered zeroing of `bytes` (4-byte words) as a kernel: every forward uses it instead of
 // hipMemsetAsync so that a captured forward holds no memset node (ops.hip).
 void zero_fill(void* p, size_t bytes, hipStream_t st);
+void fill_u32(void* p, size_t bytes, uint32_t value, hipStream_t st);   // the same with any 32-bit word
 
 // ---------------------------------------------------------------- ts-vad glue
 // BatchNorm1D + ReLU applied by the consumer of a conv output x = conv + bias (model.py:161-171, used at :255

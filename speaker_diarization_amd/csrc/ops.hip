@@ -514,18 +514,20 @@ void add_layernorm(float* x, const void* t, bool t_bf16, int rows, int D, const 
 // captured into a hipGraph (a caller may capture our forwards) is a memset node, and on ROCm 7.2 such
 // nodes were observed not to take effect before the next kernel node from the second launch of the
 // instantiated graph on (graph-replay root cause) -- a kernel node is ordered like any other.
-__global__ __launch_bounds__(256) void zero_fill_kernel(uint32_t* __restrict__ p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0u;
+__global__ __launch_bounds__(256) void fill_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
-void zero_fill(void* p, size_t bytes, hipStream_t st) {
-  SD_CHECK(bytes % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 3) == 0, kErrInvalid, "zero_fill: 4-byte words only");
+void fill_u32(void* p, size_t bytes, uint32_t value, hipStream_t st) {
+  SD_CHECK(bytes % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 3) == 0, kErrInvalid, "fill: 4-byte words only");
   const int64_t n = (int64_t)(bytes / 4);
   if (n == 0) return;
   const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, st, static_cast<uint32_t*>(p), n);
+  hipLaunchKernelGGL(fill_u32_kernel, dim3(blocks), dim3(256), 0, st, static_cast<uint32_t*>(p), n, value);
   SD_LAUNCH_CHECK();
 }
+
+void zero_fill(void* p, size_t bytes, hipStream_t st) { fill_u32(p, bytes, 0u, st); }
 
 // ------------------------------------------------------------------ TS-VAD glue
 __device__ __forceinline__ float bn_relu(const BnRelu& p, int window, int c, float x) {

@@ -66,9 +66,9 @@ class PinnedFlags {
     return any;
   }
   // kErrHip if a recurrence of an earlier launch on the handle timed out (its outputs are NaN)
-  void raise_if_set() {
-    SD_CHECK(take() == 0, kErrHip, "lstm: a persistent LSTM launch lost workgroup co-residency "
-                                   "(its outputs were poisoned with NaN)");
+  void raise_if_set(const char* what = "lstm: a persistent LSTM launch lost workgroup co-residency "
+                                       "(its outputs were poisoned with NaN)") {
+    SD_CHECK(take() == 0, kErrHip, what);
   }
 
  private:

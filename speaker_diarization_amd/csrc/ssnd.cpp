@@ -223,6 +223,7 @@ void SsndModel::decode(const float* enc, const float* x, const float* spk, int B
 
 void SsndModel::infer(const float* feats, const float* spk, int B, int Tf, float* vad, float* emb, hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
+  cam_.raise_if_set();   // an earlier call's cam_dense report
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "blocks exceed max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
   const bool bf = cfg_.bf16;

@@ -246,8 +246,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+      // wrapping increment (old >= n-1 -> 0): the counter runs 0..n-1 and is back at 0 after every launch,
+      // whatever n is and however many launches ran (a free-running u32 % n loses the merge at the 2^32 wrap
+      // unless n divides 2^32)
       const unsigned n = gridDim.x;
-      last = (__hip_atomic_fetch_add(a.cnt + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % n) == n - 1;
+      last = __builtin_amdgcn_atomic_inc32(a.cnt + sh, n - 1, __ATOMIC_RELAXED, "agent") == n - 1;
     }
     __syncthreads();
     if (!last) return;
@@ -577,8 +580,8 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
   unsigned arrival = 0;
   if (tid == 0) {
     const unsigned nh = gridDim.x;
-    arrival = __hip_atomic_fetch_add(a.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (arrival % nh) == nh - 1;
+    arrival = __builtin_amdgcn_atomic_inc32(a.cnt, nh - 1, __ATOMIC_RELAXED, "agent");   // wraps to 0 per launch
+    last = arrival == nh - 1;
   }
   __syncthreads();
   stamp();

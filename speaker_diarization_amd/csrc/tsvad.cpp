@@ -170,17 +170,21 @@ void TsvadModel::debug_buffer(int which, void** ptr, int64_t* bytes) const {
   }
 }
 
-// Direct launches only.  A hipGraph replay of this forward was tried (round 2-3) and dropped: it measured no
-// faster on C2 (34.3 vs 34.4 ms per 10-min step: ~150 launches against a 34-ms GPU span) and its replays did
-// not reproduce the direct launches' posteriors (max |diff| 0.098 from the second replay on, and a replayed
-// persistent LSTM reported lost co-residency) - tools/lstm_repro.py.
+// Direct launches.  A hipGraph replay of this forward (forward_graph above) measured no faster on C2 (34.3 vs
+// 34.4 ms per 10-min step in round 3: ~150 launches against a 34-ms GPU span).  Its round-3 replay divergence
+// was root-caused in round 4: the captured hipMemsetAsync nodes that reset the BiLSTM's h/c state and exchange
+// counters stopped taking effect from the second replay on, so the recurrence started from the previous
+// replay's state.  Every forward now zeroes device state with zero_fill kernels, and replays are
+// bit-identical to direct launches (tests/test_gpu_tsvad_graph.py).
 void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
-                         hipStream_t st) {
+                         hipStream_t st, int forward_batch, int force) {
+  SD_CHECK(forward_batch >= 0 && force >= 0 && force <= 3, kErrInvalid, "forward: bad forward_batch / force");
   SD_CHECK(finalized_, kErrState, "model not finalized");
   SD_CHECK(B >= 1 && B <= cfg_.max_batch, kErrInvalid, "batch exceeds max_batch");
   SD_CHECK(Tf >= 8 && Tf <= cfg_.max_fbank_frames, kErrInvalid, "fbank frames exceed max_fbank_frames");
   // an earlier forward's LSTM report nobody collected with sd_tsvad_status
   lstm_err_.raise_if_set();
+  cam_.raise_if_set();
   const bool bf = cfg_.bf16;
   // CAM++ up to transit3, (B, T2, 512).  Batches of more than one round of CUs run as two window slices on
   // two streams (bit-identical per window: every CAM++ kernel computes a window independently of the rest
@@ -199,9 +203,9 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   }
   // ---------------- BatchNorm1D's NaN bypass: which windows hold a non-finite input, which reference forwards
-  // (groups of fwd_batch_ windows) therefore skip the BatchNorm (from the inputs alone, so first: the window
+  // (groups of forward_batch windows) therefore skip the BatchNorm (from the inputs alone, so first: the window
   // slices below then need nothing from each other until the LSTM)
-  const int G = fwd_batch_ > 0 ? fwd_batch_ : B;
+  const int G = forward_batch > 0 ? forward_batch : B;
   int* win_fb = nonfinite_;
   int* win_ts = nonfinite_ + cfg_.max_batch;
   int* grp_sd = nonfinite_ + 2 * cfg_.max_batch;
@@ -209,6 +213,8 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   zero_fill(nonfinite_, 4 * (size_t)cfg_.max_batch * sizeof(int), st);
   nonfinite_windows(ref, B, (int64_t)Tf * 80, G, win_fb, grp_sd, grp_bd, st);
   nonfinite_windows(ts, B, (int64_t)NS * SE, G, win_ts, nullptr, cfg_.variant == 0 ? grp_bd : nullptr, st);
+  if (force & 1) fill_u32(grp_sd, (size_t)cfg_.max_batch * sizeof(int), 1u, st);
+  if (force & 3) fill_u32(grp_bd, (size_t)cfg_.max_batch * sizeof(int), 1u, st);
   BnRelu sd_bn = down_bn_, bd_bn = backend_bn_;
   sd_bn.grp = grp_sd; sd_bn.group = G;
   bd_bn.grp = grp_bd; bd_bn.group = G;

@@ -30,11 +30,12 @@ class TsvadModel {
   ParamStore& params() { return ps_; }
   void finalize();
   // ref_speech (B, T_fb, 80) fbank, target_speech (B, NS, 192), logits out (B, NS, T_lab).
+  // forward_batch: windows per reference forward call, the scope of BatchNorm1D's NaN bypass (model.py:161-171),
+  // i.e. the batch a NaN window disables speech_down_or_up's / backend_down's BatchNorm for; 0: the whole call.
+  // force: the call is part of a larger reference batch that holds a non-finite input elsewhere: bit 0 skips
+  // both BatchNorms for every window (a non-finite fbank), bit 1 backend_down's (a non-finite v0 embedding).
   void forward(const float* ref_speech, const float* target_speech, int B, int T_fb, int T_lab,
-               float* logits, hipStream_t st);
-  // Windows per reference forward call: the scope of BatchNorm1D's NaN bypass (model.py:161-171), i.e. the
-  // batch a NaN window disables speech_down_or_up's / backend_down's BatchNorm for.  0: the whole call.
-  void set_forward_batch(int windows) { fwd_batch_ = windows; }
+               float* logits, hipStream_t st, int forward_batch = 0, int force = 0);
   bool finalized() const { return finalized_; }
   size_t device_bytes() const { return arena_.total(); }
   // Diagnostics (graph-replay investigation): captures forward() once into a hipGraph on a capture stream
@@ -46,7 +47,11 @@ class TsvadModel {
   // 1 mixg (gsp_fc), 2 X2 (conformer stack output), 3 H (BiLSTM gates), 4 Y (BiLSTM output).
   void debug_buffer(int which, void** ptr, int64_t* bytes) const;
   // waits for `st` and raises kErrHip if a persistent LSTM of the forwards enqueued on it timed out
-  void status(hipStream_t st) { SD_HIP(hipStreamSynchronize(st)); lstm_err_.raise_if_set(); }
+  void status(hipStream_t st) {
+    SD_HIP(hipStreamSynchronize(st));
+    lstm_err_.raise_if_set();
+    cam_.raise_if_set();
+  }
   ~TsvadModel();
 
  private:
@@ -65,7 +70,6 @@ class TsvadModel {
   CamTrunk cam_;     // speech_encoder.* (CAM++ get_time_out=True)
   ConvL down_;        // speech_down_or_up conv: epilogue = + bias only (its BatchNorm1D is down_bn_)
   BnRelu down_bn_, backend_bn_;   // folded BatchNorms, applied (or bypassed) by the consumers
-  int fwd_batch_ = 0;
   int* nonfinite_ = nullptr;      // [win_fbank B | win_ts B | grp_speech B | grp_backend B]
   const float *gsp_w_ = nullptr, *gsp_b_ = nullptr;
   const float* pe_ = nullptr;

@@ -122,6 +122,7 @@ void TsvadStreamModel::run_layers(const std::vector<WenetLayerL>& Ls, float* X, 
 void TsvadStreamModel::forward(const float* feats, const float* ts, int B, int T_lab, int chunk, int left,
                                float* logits, hipStream_t st) {
   SD_CHECK(finalized_, kErrState, "model not finalized");
+  cam_.raise_if_set();   // an earlier call's cam_dense report
   SD_CHECK(B >= 1 && B <= cfg_.max_windows, kErrInvalid, "windows per call exceed max_windows");
   SD_CHECK(T_lab >= 1 && T_lab <= cfg_.max_labels, kErrInvalid, "label frames exceed max_labels");
   SD_CHECK(chunk >= 1, kErrInvalid, "decoding_chunk_size must be >= 1");

@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes
 from typing import List
 
+import numpy as np
 import torch
 
 from .. import _lib
@@ -145,6 +146,14 @@ class FsEendStream:
 
     def device_bytes(self) -> int:
         return int(_lib.load().sd_fseend_stream_device_bytes(self._s))
+
+    def debug_counters(self) -> np.ndarray:
+        """The device block-merge counters (decode attention per (slot, head), then the slot block's),
+        read after the stream drains; each is 0 between launches."""
+        n = ctypes.c_int()
+        buf = (ctypes.c_uint * 256)()
+        _lib.call("sd_fseend_stream_debug_counters", self._s, buf, 256, ctypes.byref(n), _lib.stream_ptr(self.device))
+        return np.array(buf[: min(n.value, 256)], dtype=np.uint32)
 
     def _push_rows(self, rows) -> torch.Tensor:
         n = int(rows.shape[0])

@@ -92,15 +92,17 @@ class TSVADModel:
 
     # ------------------------------------------------------------------ forward
     def forward(self, ref_speech, target_speech, labels, num_updates: int = 0, out=None, check: bool = True,
-                forward_batch: int = 0):
+                forward_batch: int = 0, _force: int = 0):
         """ref_speech (B, T_fb, 80), target_speech (B, NS, 192), labels (B, NS, T) (only
         labels.size(-1) is read, model.py:681/770) -> logits (B, NS, T).  check: wait for the
         stream and raise RuntimeError in this call if the BiLSTM's persistent recurrence lost
         co-residency (its logits are NaN); check=False defers that to status().
         forward_batch: windows per reference forward call when this call covers several of them (the
         pipeline's fused device batches): the scope of BatchNorm1D's NaN bypass (model.py:161-171).  0: this
-        call is one batch (up to max_batch windows: a call split into several device forwards bypasses per
-        device forward)."""
+        call is one batch.  A call of more than max_batch windows runs as several device forwards cut at
+        reference-batch boundaries; a reference batch wider than max_batch is cut into device forwards that
+        each learn (`_force`) whether a non-finite input sits anywhere in that batch, so the bypass keeps the
+        reference's scope."""
         import torch
         B, T_fb, F = ref_speech.shape
         T_lab = labels if isinstance(labels, int) else labels.size(-1)
@@ -110,17 +112,27 @@ class TSVADModel:
         assert ts.shape == (B, self.max_num_speaker, self.cfg.speaker_embed_dim)
         if out is None:
             out = torch.empty(B, self.max_num_speaker, T_lab, device=self.device, dtype=torch.float32)
+        G = forward_batch if forward_batch > 0 else B
         if B > self.max_batch:
-            for s in range(0, B, self.max_batch):
-                e = min(B, s + self.max_batch)
-                self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False, forward_batch=forward_batch)
+            if G <= self.max_batch:      # whole reference batches per device forward
+                step = self.max_batch // G * G
+                for s in range(0, B, step):
+                    e = min(B, s + step)
+                    self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False, forward_batch=G)
+            else:                        # a reference batch spans device forwards: its non-finite flags up front
+                for g0 in range(0, B, G):
+                    g1 = min(B, g0 + G)
+                    force = 3 if not bool(torch.isfinite(ref[g0:g1]).all()) else 0
+                    if self.cfg.variant == 0 and not bool(torch.isfinite(ts[g0:g1]).all()):
+                        force |= 2
+                    for s in range(g0, g1, self.max_batch):
+                        e = min(g1, s + self.max_batch)
+                        self.forward(ref[s:e], ts[s:e], T_lab, out=out[s:e], check=False, _force=force)
             if check:
                 self.status()
             return out
-        if _lib.has("sd_tsvad_set_forward_batch"):   # (absent only from an older SDIAR_LIB in an A/B run)
-            _lib.call("sd_tsvad_set_forward_batch", self._h, int(forward_batch))
-        _lib.call("sd_tsvad_forward", self._h, _lib.ptr(ref), _lib.ptr(ts), B, T_fb, T_lab, _lib.ptr(out),
-                  _lib.stream_ptr(self.device))
+        _lib.call("sd_tsvad_forward_batched", self._h, _lib.ptr(ref), _lib.ptr(ts), B, T_fb, T_lab,
+                  int(forward_batch), int(_force), _lib.ptr(out), _lib.stream_ptr(self.device))
         if check:
             self.status()
         return out

@@ -60,17 +60,22 @@ TSVAD_CASES = {
 TSVAD_NAN_CASES = {
     "tsvad_v1_rs6_nan": ("tsvad_v1_rs6", 1, 300, 17),
     "tsvad_v0_rs4_nan": ("tsvad_v0_rs4_short", 2, 5, 0),
+    # round 5: an infinite fbank value instead (the reference tests isnan on the BatchNorm INPUT, the conv
+    # output, model.py:166-170; these pin what the CAM++ trunk's arithmetic turns the Inf into)
+    "tsvad_v1_rs6_inf": ("tsvad_v1_rs6", 1, 300, 17, np.inf),
+    "tsvad_v0_rs4_inf": ("tsvad_v0_rs4_short", 2, 5, 0, np.inf),
+    "tsvad_v0_rs4_ninf": ("tsvad_v0_rs4_short", 0, 100, 40, -np.inf),
 }
 
 
 def tsvad_case_inputs(name):
     """(case tuple, ref_speech, ts) of a TSVAD_CASES or TSVAD_NAN_CASES name."""
-    base, nan_at = (TSVAD_NAN_CASES[name][0], TSVAD_NAN_CASES[name][1:]) if name in TSVAD_NAN_CASES else (name, None)
+    base, nan_at = (TSVAD_NAN_CASES[name][0], TSVAD_NAN_CASES[name][1:4]) if name in TSVAD_NAN_CASES else (name, None)
     case = TSVAD_CASES[base]
     _, _, B, T_fb, n_lab, iseed, _ = case
     ref_speech, ts = tsvad_inputs(B, T_fb, n_lab, seed=iseed)
     if nan_at is not None:
-        ref_speech[nan_at] = np.nan
+        ref_speech[nan_at] = TSVAD_NAN_CASES[name][4] if len(TSVAD_NAN_CASES[name]) > 4 else np.nan
     return case, ref_speech, ts
 
 

@@ -105,6 +105,30 @@ def test_stream_long_many_key_tiles(gpu):
     np.testing.assert_allclose(out.cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
 
 
+@pytest.mark.parametrize("chunk", [1, 3])
+def test_merge_counters_wrap_to_zero(gpu, chunk):
+    """The decode attention's and the slot block's last-arriver counters: a wrapping increment
+    that is back at 0 after every launch, here with a block count that does not divide 2^32 (1164 frames ->
+    5 blocks per (slot, head)), across graph replays and a reset; the scores stay those of test()."""
+    T = 1100
+    m = _model(804, max_frames=T)
+    x = torch.from_numpy(eda_inputs([T], seed=84)[0]).to(gpu)
+    ref, _, _ = m.test([x], [T], max_nspks=6)
+    s = m.stream(chunk=chunk, max_frames=T + 64, max_nspks=6, use_graph=True)
+    assert (s.debug_counters() == 0).all()
+    for rep in range(2):
+        outs = []
+        for i in range(0, T, chunk):
+            outs.append(s.push(x[i : i + chunk]))
+            if (i // chunk) % 97 == 5:
+                c = s.debug_counters()
+                assert c.size == 6 * 4 + 1 and (c == 0).all(), c
+        outs.append(s.flush())
+        assert (s.debug_counters() == 0).all()
+        np.testing.assert_allclose(torch.cat(outs).cpu().numpy(), ref[0].cpu().numpy(), atol=FP32_ATOL)
+        s.reset()
+
+
 @pytest.mark.parametrize("T", [1, 5, 9, 10, 28])
 def test_short_recordings_flush(gpu, T):
     """Shorter than the 9-frame look-ahead: every score comes out of flush()."""

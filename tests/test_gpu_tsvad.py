@@ -50,8 +50,9 @@ def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("name", list(TSVAD_NAN_CASES))
 def test_tsvad_nan_window_bypasses_batchnorm(gpu, name, precision):
-    """BatchNorm1D's NaN bypass (model.py:161-171) against the reference run on a batch with one NaN fbank
-    value: the NaN window's logits are NaN, every other window matches the reference (whose BatchNorm was
+    """BatchNorm1D's NaN bypass (model.py:161-171) against the reference run on a batch with one NaN (or, the
+    *_inf / *_ninf cases, one +-Inf: the trunk's arithmetic turns it into NaN at the BatchNorm input, so the
+    reference bypasses exactly as for NaN) fbank value: the bad window's logits are NaN, every other window matches the reference (whose BatchNorm was
     skipped for the whole batch) within the usual bound.  Then the scope: with forward_batch = 1 each window
     is its own reference batch, so the others keep their BatchNorm (== the golden without the NaN)."""
     (v, rs, B, T, nl, iseed, wseed), x, ts = tsvad_case_inputs(name)
@@ -72,14 +73,40 @@ def test_tsvad_nan_window_bypasses_batchnorm(gpu, name, precision):
     # variant 1; variant 0's backend_down does, so its batch bypasses there too -- oracle)
     ts2 = ts.copy()
     ts2[keep[0], 1, 3] = np.nan
-    out2 = m.forward(torch.from_numpy(np.nan_to_num(x, nan=0.0)).to(gpu), torch.from_numpy(ts2).to(gpu), nl).cpu().numpy()
+    x0 = np.nan_to_num(x, nan=0.0, posinf=0.0, neginf=0.0)
+    out2 = m.forward(torch.from_numpy(x0).to(gpu), torch.from_numpy(ts2).to(gpu), nl).cpu().numpy()
     assert np.isnan(out2[keep[0]]).all()
     from oracle.tsvad_ref import tsvad_forward
     ref2 = tsvad_forward(to_torch(tsvad_state_dict(_cfg(v, rs), seed=wseed)), _cfg(v, rs),
-                         torch.from_numpy(np.nan_to_num(x, nan=0.0)), torch.from_numpy(ts2), nl).numpy()
+                         torch.from_numpy(x0), torch.from_numpy(ts2), nl).numpy()
     assert np.isnan(ref2[keep[0]]).all()
     others = [i for i in range(B) if i != keep[0]]
     assert np.abs(out2[others] - ref2[others]).max() < tol
+
+
+@pytest.mark.parametrize("name", ["tsvad_v0_rs4_nan", "tsvad_v0_rs4_ninf"])
+def test_tsvad_nan_bypass_scope_across_device_calls(gpu, name):
+    """A call wider than max_batch runs as several device forwards; the bypass scope must still be the
+    reference's batch: forward_batch 0 -> the whole call (every window bypassed: the golden),
+    forward_batch 2 -> windows [0, 2) and [2, 3) are separate reference batches."""
+    (v, rs, B, T, nl, iseed, wseed), x, ts = tsvad_case_inputs(name)
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")["logits"]
+    base = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{TSVAD_NAN_CASES[name][0]}.npz")["logits"]
+    bad = TSVAD_NAN_CASES[name][1]
+    keep = [i for i in range(B) if i != bad]
+    m = TSVADModel(_cfg(v, rs), device=gpu, precision="fp32", max_batch=2)
+    m.load_state_dict(to_torch(tsvad_state_dict(_cfg(v, rs), seed=wseed)))
+    xd, tsd = torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu)
+    out = m.forward(xd, tsd, nl).cpu().numpy()                       # 3 windows over device calls of 2 + 1
+    assert np.isnan(out[bad]).all()
+    assert np.abs(out[keep] - g[keep]).max() < FP32_ATOL
+    out = m.forward(xd, tsd, nl, forward_batch=2).cpu().numpy()      # reference batches [0, 2), [2, 3)
+    grp = [i for i in range(B) if i // 2 == bad // 2 and i != bad]
+    other = [i for i in range(B) if i // 2 != bad // 2]
+    assert np.isnan(out[bad]).all()
+    if grp:
+        assert np.abs(out[grp] - g[grp]).max() < FP32_ATOL
+    assert np.abs(out[other] - base[other]).max() < FP32_ATOL
 
 
 def test_tsvad_strict_load_errors(gpu):
