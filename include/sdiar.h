@@ -44,6 +44,9 @@ double sd_prof_query_steps(int i);
  * no gate arithmetic (same publish / poll / payload loads as lstm_group_bf16_kernel, batch 16) over `steps`
  * steps, timed with HIP events on `stream`; *us_per_step = its time / steps. */
 int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream);
+/* The same 4-workgroup exchange on data-tagged 8-byte granules (no counter, no barrier; MI355X guide
+ * handoff-1to1): the hardware's hand-off price for the recurrence, us per step. */
+int sd_probe_lstm_granule(int steps, float* us_per_step, void* stream);
 
 /* ------------------------------------------------------------------ TS-VAD
  * Replaces TSVADModel (egs/alimeeting/ts_vad2/model.py:179-1142):
@@ -432,6 +435,12 @@ int sd_debug_cam_dense_probe(void* stamps);
  * an event fork / join of a second captured stream) replayed `replays` times; bad_per_replay (host, replays
  * ints) = Y values that were not 0 after each replay. */
 int sd_probe_graph_memset(int n, int replays, int fork, int* bad_per_replay, void* stream);
+/* The conformer self-attention block's in-projection + attention (mha_block.hip; torchaudio MHA with
+ * batch_first, 8 heads of 48, D 384) on LayerNorm'd bf16 rows y (S, T, 384): w (1152, 384) / bias (1152) the
+ * packed in_proj, key_len device int32 (S) or NULL, out bf16 (S, T, 384) = the heads' outputs before out_proj.
+ * variant: the kernel layout (0: one sequence per 4-wave workgroup, 1: two per 8-wave workgroup; tests). */
+int sd_op_mha_block(const void* y, const float* w, const float* bias, int S, int T, const int* key_len, void* out,
+                    int variant, void* stream);
 /* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);

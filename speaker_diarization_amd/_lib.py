@@ -114,6 +114,7 @@ _SIGS = {
     "sd_prof_query": (c_int, [c_int, c_char_p, c_int, POINTER(c_int64), POINTER(ctypes.c_double),
                               POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
     "sd_prof_query_steps": (ctypes.c_double, [c_int]),
+    "sd_probe_lstm_granule": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_probe_lstm_handoff": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_tsvad_create": (c_int, [POINTER(TsvadConfig), POINTER(c_void_p)]),
     "sd_tsvad_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
@@ -192,6 +193,7 @@ _SIGS = {
                                 c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "sd_debug_cam_dense_probe": (c_int, [c_void_p]),
     "sd_probe_graph_memset": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sd_op_mha_block": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "sd_op_cam_dense": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_int, c_void_p]),

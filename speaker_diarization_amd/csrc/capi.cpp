@@ -109,6 +109,13 @@ int sd_prof_query(int i, char* name, int name_len, int64_t* launches, double* fl
 
 double sd_prof_query_steps(int i) { return sd::prof_query_steps(i); }
 
+int sd_probe_lstm_granule(int steps, float* us_per_step, void* stream) {
+  return guard([&] {
+    SD_CHECK(steps >= 1 && us_per_step, sd::kErrInvalid, "probe_lstm_granule: bad argument");
+    *us_per_step = sd::lstm_granule_probe(steps, S(stream));
+  });
+}
+
 int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream) {
   return guard([&] {
     SD_CHECK(steps >= 1 && us_per_step, sd::kErrInvalid, "probe_lstm_handoff: bad argument");
@@ -740,6 +747,20 @@ int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const
     for (int r = 0; r < repeats; ++r)
       sd::cam_dense(x, B, T, ld, cin, dil, s1, h1, wbt.p, a2, b2, wlt.p, bl, w1, c1, w2, c2, out, rec.p,
                     static_cast<unsigned*>(cnt.p), st);
+  });
+}
+
+int sd_op_mha_block(const void* y, const float* w, const float* bias, int nseq, int T, const int* key_len, void* out,
+                    int variant, void* stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    SD_CHECK(nseq >= 1 && sd::mha_block_supported(384, 8, T, true), sd::kErrInvalid, "mha_block: unsupported shape");
+    Scratch wt((size_t)3 * 384 * 384 * 2, st);
+    sd::pack_weight(w, 3 * 384, 384, 1, wt.p, true, st);
+    sd::MhaBlockArgs m;
+    m.y = y; m.W = wt.p; m.bias = bias; m.out = out; m.ldo = 384;
+    m.S = nseq; m.T = T; m.D = 384; m.nh = 8; m.scale = 1.f / std::sqrt(48.f); m.key_len = key_len;
+    sd::mha_block(m, st, variant);
   });
 }
 

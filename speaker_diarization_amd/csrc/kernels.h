@@ -277,7 +277,7 @@ std::vector<uint16_t> rowprog_pack_pre(const std::vector<float>& W, int N, int K
 std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1, const std::vector<float>& W2, int hidden,
                                        const std::vector<float>& ln_g, const std::vector<float>& ln_b,
                                        const std::vector<float>& b1, std::vector<float>& b1_folded);
-void mha_block(const MhaBlockArgs& a, hipStream_t st);
+void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant = -1);   // variant: tests (-1: the env's)
 
 // ---------------------------------------------------------------- ssnd_ops.hip
 // Multi-head attention core on separate fp32 q / k / v row sets (SSND decoder cross and self
@@ -380,6 +380,8 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 int64_t lstm_work_floats(int B, int H, int ndir);
 // Exchange floor of the persistent recurrence (sd_probe_lstm_handoff): us per step of its hand-off alone.
 float lstm_handoff_probe(int steps, hipStream_t st);
+// The same exchange on 8-byte {data, tag} granules (sd_probe_lstm_granule; lstm.hip): us per step.
+float lstm_granule_probe(int steps, hipStream_t st);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr,

@@ -436,6 +436,62 @@ __global__ __launch_bounds__(256) void lstm_handoff_probe_kernel(int steps, uint
   if (tid == 0) sink[blockIdx.x] = hr;
 }
 
+// The same exchange on the guide's data-tagged transport (MI355X_MICROARCH.md, handoff-1to1: naturally aligned
+// 8-byte {data, tag} granules, each written by ONE sc1 store, no counter, no barrier): a lane publishes its 4 units
+// of h as two granules {2 x bf16 | step tag} in one 16-B sc1 store (observed untorn), and every wave polls the 32
+// granules its next MFMA operand needs (16 x 16-B sc1 loads per lane) until each carries the step's tag.  Parity
+// double-buffered: a producer writes step s + 1's granules only after reading everyone's step s, and a consumer
+// reads parity s & 1 for step s, so a granule is never overwritten before every reader has seen it.
+// sd_probe_lstm_granule: us per step of this hand-off alone.
+__global__ __launch_bounds__(256) void lstm_granule_probe_kernel(int steps, uint64_t* __restrict__ gx,
+                                                                 int* __restrict__ err, unsigned spin_limit,
+                                                                 float* __restrict__ sink) {
+  constexpr int H = LS_H, NG = H / 2;                        // granules per batch row and parity
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int ub = 64 * (int)(blockIdx.x & 3) + 16 * w + 4 * g;   // the lane's 4 units (as the recurrence)
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * 16 * NG * 8, 0x00020000);
+  auto goff = [&](int parity, int b, int granule) { return (uint32_t)(((parity * 16 + b) * NG + granule) * 8); };
+  float hr = (float)ub;
+  auto publish = [&](int step_tag) {   // the values of step step_tag - 1 (tag 0 = never written)
+    const uint32_t d = pack_bf16x2(hr, hr);
+    const u32x4_t v = {d, (uint32_t)step_tag, d, (uint32_t)step_tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rg, goff(step_tag & 1, l15, ub / 2), 0, 16);   // sc1
+  };
+  publish(1);
+  int bad = 0;
+  for (int step = 1; step <= steps && !bad; ++step) {
+    // the operand of the next step: units kc * 32 + 8 g .. + 7 of batch row l15 = granules (kc * 32 + 8 g) / 2 ..
+    u32x4_t f[H / 32][2];
+    unsigned spins = 0;
+    for (;;) {
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          f[kc][q] = __builtin_amdgcn_raw_buffer_load_b128(rg, goff(step & 1, l15, (kc * 32 + 8 * g) / 2 + 2 * q), 0, 16);
+      bool ok = true;
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) ok &= f[kc][q][1] == (uint32_t)step && f[kc][q][3] == (uint32_t)step;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (++spins > spin_limit) {
+        bad = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int kc = 0; kc < H / 32; ++kc) x ^= f[kc][0][0] ^ f[kc][1][2];
+    hr = __uint_as_float((x & 0x007fffffu) | 0x3f800000u);   // the next publish depends on every granule
+    publish(step + 1);
+  }
+  if (bad && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) sink[blockIdx.x] = hr;
+}
+
 // Poll bound of the persistent kernel's waits: 2^22 polls (~0.1 s).  Tests only: SDIAR_LSTM_SPIN_LIMIT
 // shrinks it so a test can force the co-residency-lost path and check that it is reported;
 // SDIAR_LSTM_SPIN_LIMIT_LAUNCHES=n applies that limit to the first n persistent launches of the process
@@ -542,6 +598,33 @@ float lstm_handoff_probe(int steps, hipStream_t st) {
   (void)hipEventDestroy(b);
   (void)hipFree(buf);
   SD_CHECK(e == 0, kErrHip, "lstm hand-off probe: a poll timed out");
+  return ms * 1000.f / (float)steps;
+}
+
+float lstm_granule_probe(int steps, hipStream_t st) {
+  const size_t gx_bytes = (size_t)2 * 16 * (LS_H / 2) * 8;
+  void* buf = nullptr;
+  SD_HIP(hipMalloc(&buf, gx_bytes + 256));
+  SD_HIP(hipMemsetAsync(buf, 0, gx_bytes + 256, st));
+  uint64_t* gx = static_cast<uint64_t*>(buf);
+  int* err = reinterpret_cast<int*>(static_cast<char*>(buf) + gx_bytes);
+  float* sink = reinterpret_cast<float*>(static_cast<char*>(buf) + gx_bytes + 64);
+  hipEvent_t a, b;
+  SD_HIP(hipEventCreate(&a));
+  SD_HIP(hipEventCreate(&b));
+  SD_HIP(hipEventRecord(a, st));
+  hipLaunchKernelGGL(lstm_granule_probe_kernel, dim3(4), dim3(256), 0, st, steps, gx, err, lstm_spin_limit(), sink);
+  SD_LAUNCH_CHECK();
+  SD_HIP(hipEventRecord(b, st));
+  SD_HIP(hipEventSynchronize(b));
+  float ms = 0.f;
+  SD_HIP(hipEventElapsedTime(&ms, a, b));
+  int e = 0;
+  SD_HIP(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(buf);
+  SD_CHECK(e == 0, kErrHip, "lstm granule probe: a poll timed out");
   return ms * 1000.f / (float)steps;
 }
 

@@ -33,56 +33,67 @@ constexpr int kD = 384, kHD = 48, kNH = 8;
 constexpr int kKT32 = kD / 32;                 // 32-wide k-steps of the projection
 constexpr int kKC = kD / 64;                   // 64-wide k-blocks of a weight piece
 constexpr int kTP = 160;                       // padded tokens per sequence
-constexpr int kSeq = 2;                        // sequences per workgroup
 constexpr int kTilesPerSeq = kTP / 16;         // 10 row tiles of 16 tokens
-constexpr int kTiles = kSeq * kTilesPerSeq;     // 20
-constexpr int kWaves = 8;
-constexpr int kMaxTiles = (kTiles + kWaves - 1) / kWaves;   // 3 (waves 0-3), others 2
-constexpr int kThreads = kWaves * 64;
 constexpr int kPR = 16;                        // weight rows per piece (one MFMA column tile)
 constexpr int kSlot = kKC * kPR * 64;          // bf16 elements per ring slot (12 KiB)
-constexpr int kNSlot = 3;
 constexpr int kDmaPerPiece = kKC * (kPR / 8);  // 1-KiB DMA instructions per piece (12)
-constexpr int kQS = 64;                        // Q / K row stride (features 48..63 stay zero)
 constexpr int kVS = 48;                        // V row stride
-constexpr int kSeqLds = 2 * kTP * kQS + kTP * kVS;   // bf16 elements of one sequence's Q, K, V images
 constexpr int kPieces = kNH * 3 * (kHD / kPR); // 72
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-constexpr size_t kSmemBytes = sizeof(uint16_t) * ((size_t)kNSlot * kSlot + (size_t)kSeq * kSeqLds) +
-                              sizeof(float) * 3 * kD;
+
+// Two layouts of the same arithmetic (bit-identical outputs):
+//   <2, 8, 3, 64>  two sequences per 8-wave workgroup, 3-slot ring, Q / K rows padded to 64 (151 KiB: one
+//                  workgroup per CU) - rounds 2-4;
+//   <1, 4, 2, 48>  round 5: one sequence per 4-wave workgroup, 2-slot ring, Q / K rows of 48 (73.5 KiB: TWO
+//                  workgroups per CU, so one's HBM prologue, piece waits and softmax VALU overlap the other's
+//                  MFMAs).  With 48-wide rows the second 32-deep QK^T k-step reads features 48..63 from the
+//                  next row (finite values), multiplied by the query fragment's features 48..63, which are
+//                  zeroed in registers.
+template <int SEQ, int W, int NSLOT, int QS>
+struct MhaL {
+  static constexpr int kTiles = SEQ * kTilesPerSeq;
+  static constexpr int kMaxTiles = (kTiles + W - 1) / W;
+  static constexpr int kThreads = W * 64;
+  static constexpr int kSeqLds = 2 * kTP * QS + kTP * kVS;   // bf16 elements of one sequence's Q, K, V images
+  static constexpr size_t kSmem = sizeof(uint16_t) * ((size_t)NSLOT * kSlot + (size_t)SEQ * kSeqLds) +
+                                  sizeof(float) * 3 * kD;
+  static_assert(kMaxTiles == 2 || kMaxTiles == 3, "2 or 3 row tiles per wave (af registers)");
+};
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
+template <int SEQ, int W, int NSLOT, int QS>
+__global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
+  using L = MhaL<SEQ, W, NSLOT, QS>;
+  constexpr int kTiles = L::kTiles, kMaxTiles = L::kMaxTiles, kThreads = L::kThreads, kSeqLds = L::kSeqLds;
   extern __shared__ __attribute__((aligned(1024))) uint16_t sm[];
-  uint16_t* Ws = sm;                                          // [kNSlot][kKC][16][64]
+  uint16_t* Ws = sm;                                          // [NSLOT][kKC][16][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lk = lane >> 4;
-  float* s_bias = reinterpret_cast<float*>(Ws + kNSlot * kSlot + kSeq * kSeqLds);   // [3 * kD]
+  float* s_bias = reinterpret_cast<float*>(Ws + NSLOT * kSlot + SEQ * kSeqLds);   // [3 * kD]
   const int T = a.T;
-  const int ntile = w < kTiles - (kMaxTiles - 1) * kWaves ? kMaxTiles : kMaxTiles - 1;   // wave-uniform
+  const int ntile = w < kTiles - (kMaxTiles - 1) * W ? kMaxTiles : kMaxTiles - 1;   // wave-uniform
   // tile j of this wave: sequence slot sqj[j], token row rowj[j] (this lane's token)
   int sqj[kMaxTiles], rowj[kMaxTiles];
 #pragma unroll
   for (int j = 0; j < kMaxTiles; ++j) {
-    const int t = w + kWaves * j;
+    const int t = w + W * j;
     sqj[j] = min(t, kTiles - 1) / kTilesPerSeq;
     rowj[j] = (min(t, kTiles - 1) % kTilesPerSeq) * 16 + l15;
   }
-  auto qimg = [&](int sq) { return Ws + kNSlot * kSlot + sq * kSeqLds; };   // [kTP][kQS] Q, then K, then V
+  auto qimg = [&](int sq) { return Ws + NSLOT * kSlot + sq * kSeqLds; };   // [kTP][QS] Q, then K, then V
 
   const int lrow = lane >> 3, lch = lane & 7;
   // Piece i: head h = i / 9, component c = (i / 3) % 3, feature tile ft = i % 3 -> in_proj rows
-  // c*D + 48h + 16ft .. +15, all K, as 12 1-KiB DMA instructions (k-block kc, 8-row group) over the
-  // waves (waves 0 and 1 issue two, the others one).
+  // c*D + 48h + 16ft .. +15, all K, as 12 1-KiB DMA instructions (k-block kc, 8-row group) over the waves.
   auto issue_piece = [&](int i) {
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
-    uint16_t* slot = Ws + (i % kNSlot) * kSlot;
-    for (int j = w; j < kDmaPerPiece; j += kWaves) {
+    uint16_t* slot = Ws + (i % NSLOT) * kSlot;
+    for (int j = w; j < kDmaPerPiece; j += W) {
       const int kc = j >> 1, rg = j & 1;
       const int r = rg * 8 + lrow;
       const uint32_t off =
@@ -92,15 +103,17 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
       dma_lds16(reinterpret_cast<const char*>(a.W) + off, (lds_ptr_t)(slot + ((size_t)kc * kPR + rg * 8) * 64));
     }
   };
-  const int my_dma = (w < kDmaPerPiece - kWaves) ? 2 : 1;      // instructions this wave issues per piece
-  issue_piece(0);
-  issue_piece(1);
+  const int my_dma = (kDmaPerPiece - w + W - 1) / W;          // instructions this wave issues per piece
+#pragma unroll
+  for (int i = 0; i < NSLOT - 1; ++i) issue_piece(i);
   for (int i = tid; i < 3 * kD; i += kThreads) s_bias[i] = a.bias[i];
-  for (int i = tid; i < kSeq * kTP * 2; i += kThreads) {   // zero Q/K features 48..63 (never written later)
-    const int q = i / (kTP * 2), r = (i >> 1) % kTP, c = kHD + (i & 1) * 8;
-    uint16_t* qs = Ws + kNSlot * kSlot + q * kSeqLds;
-    *reinterpret_cast<uint4*>(qs + r * kQS + c) = make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(qs + kTP * kQS + r * kQS + c) = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (QS > kHD) {
+    for (int i = tid; i < SEQ * kTP * 2; i += kThreads) {   // zero Q/K features 48..63 (never written later)
+      const int q = i / (kTP * 2), r = (i >> 1) % kTP, c = kHD + (i & 1) * 8;
+      uint16_t* qs = Ws + NSLOT * kSlot + q * kSeqLds;
+      *reinterpret_cast<uint4*>(qs + r * QS + c) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(qs + kTP * QS + r * QS + c) = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
 
   // ---- prologue: af[rt][kk] = y[32kk + 8lk .. +7] of the LayerNorm'd bf16 rows (B-operand fragments)
@@ -108,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
 #pragma unroll
   for (int rt = 0; rt < kMaxTiles; ++rt) {
     const int row = rowj[rt];
-    const int s = blockIdx.x * kSeq + sqj[rt];
+    const int s = blockIdx.x * SEQ + sqj[rt];
     const bool live = rt < ntile && s < a.S && row < T;
     const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + ((int64_t)s * T + row) * kD;
 #pragma unroll
@@ -117,10 +130,10 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
                                                    : make_uint4(0u, 0u, 0u, 0u));
   }
 
-  int klenj[kSeq];
+  int klenj[SEQ];
 #pragma unroll
-  for (int q = 0; q < kSeq; ++q) {
-    const int s = blockIdx.x * kSeq + q;
+  for (int q = 0; q < SEQ; ++q) {
+    const int s = blockIdx.x * SEQ + q;
     klenj[q] = s < a.S ? (a.key_len ? min(a.key_len[s], T) : T) : 0;
   }
   const int tr_off = ((4 * lk + (l15 >> 2)) * kVS + 4 * (l15 & 3)) * 2;
@@ -129,16 +142,22 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   bool drain = true;   // VMEM ops younger than the last DMA issue are pending: wait for everything
 
   for (int i = 0; i < kPieces; ++i) {
-    // Piece i landed: the only younger DMA is piece i+1's (this wave's my_dma instructions), unless
-    // stores were issued after it (attention outputs) -> full drain.
-    if (drain || i + 1 >= kPieces) wait_vm<0>();
-    else if (my_dma == 2) wait_vm<2>();
-    else wait_vm<1>();
+    // Piece i landed: the only younger DMAs are the NSLOT - 2 pieces issued after it (this wave's my_dma
+    // instructions each), unless stores were issued after them (attention outputs) -> full drain.
+    if constexpr (NSLOT == 3) {
+      if (drain || i + 1 >= kPieces) wait_vm<0>();
+      else if (my_dma == 3) wait_vm<3>();
+      else if (my_dma == 2) wait_vm<2>();
+      else wait_vm<1>();
+    } else {
+      static_assert(NSLOT == 2, "ring depth");
+      wait_vm<0>();
+    }
     drain = false;
-    __syncthreads();   // every wave's part of piece i is in LDS; slot (i+2) % 3 (piece i-1) is free
-    if (i + 2 < kPieces) issue_piece(i + 2);
+    __syncthreads();   // every wave's part of piece i is in LDS; the slot of piece i-1 is free
+    if (i + NSLOT - 1 < kPieces) issue_piece(i + NSLOT - 1);
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
-    const uint16_t* slot = Ws + (i % kNSlot) * kSlot;
+    const uint16_t* slot = Ws + (i % NSLOT) * kSlot;
     floatx4 acc[kMaxTiles];
 #pragma unroll
     for (int rt = 0; rt < kMaxTiles; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -158,12 +177,18 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
       if (kk + kWPD < kKT32) wq[kk % kWPD] = wfrag(kk + kWPD);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
-      if (ntile > 2) acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[2][kk], acc[2], 0, 0, 0);
+      // the 4-wave layout does not skip the third tile's MFMA for its two-tile waves (af[2] = 0 there): with the
+      // uniform branch around it the compiler shuttled the accumulators through AGPR copies every k-step and the
+      // results came out wrong (0.1-2.4 off on every tile at T >= 100, tests/test_gpu_mha_block.py; not
+      // root-caused further: the branch-free stream is also the faster one)
+      if constexpr (kMaxTiles > 2) {
+        if (W == 4 || ntile > 2) acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[2][kk], acc[2], 0, 0, 0);
+      }
       asm volatile("" ::: "memory");
     }
     // lane holds features 16ft + 4lk + r of token rowj[rt]
-    const int ld = c == 2 ? kVS : kQS;
-    const int coff = c * kTP * kQS;                 // Q, K or V image within the sequence's block
+    const int ld = c == 2 ? kVS : QS;
+    const int coff = c * kTP * QS;                  // Q, K or V image within the sequence's block
     const float scl = c == 0 ? a.scale : 1.f;
     const int n0 = ft * 16 + 4 * lk;
     const float4 bv = *reinterpret_cast<const float4*>(s_bias + c * kD + h * kHD + n0);
@@ -174,21 +199,24 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
             make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
                        pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2) continue;
-    __syncthreads();   // head h's Q, K, V images complete (both sequences)
+    __syncthreads();   // head h's Q, K, V images complete (every sequence of the workgroup)
 
     // ---- attention of head h for this wave's 16-query tiles
 #pragma unroll 1
     for (int rt = 0; rt < ntile; ++rt) {
       const int row = rowj[rt];
-      const int s = blockIdx.x * kSeq + sqj[rt];
+      const int s = blockIdx.x * SEQ + sqj[rt];
       if (s >= a.S) continue;
       const uint16_t* Qs = qimg(sqj[rt]);
-      const uint16_t* Ks = Qs + kTP * kQS;
-      const uint16_t* Vs = Ks + kTP * kQS;
+      const uint16_t* Ks = Qs + kTP * QS;
+      const uint16_t* Vs = Ks + kTP * QS;
       const int klen = klenj[sqj[rt]];
       bf16x8 qf[2];
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(Qs + row * kQS + kc * 32 + lk * 8);
+      for (int kc = 0; kc < 2; ++kc) qf[kc] = *reinterpret_cast<const bf16x8*>(Qs + row * QS + kc * 32 + lk * 8);
+      if constexpr (QS == kHD) {   // features 48..63 of the second k-step: the next row's (see MhaL), zeroed
+        if (lk >= 2) qf[1] = __builtin_bit_cast(bf16x8, make_uint4(0u, 0u, 0u, 0u));
+      }
       floatx4 o[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       float m_run = -INFINITY, l_run = 0.f;
       for (int k0 = 0; k0 < klen; k0 += 32) {
@@ -198,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
           floatx4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int kc = 0; kc < 2; ++kc) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + st * 16 + l15) * kQS + kc * 32 + lk * 8);
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (k0 + st * 16 + l15) * QS + kc * 32 + lk * 8);
             sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kc], sacc, 0, 0, 0);
           }
           sc[st] = sacc;
@@ -258,6 +286,19 @@ __global__ __launch_bounds__(kThreads) void mha_block_kernel(MhaBlockArgs a) {
   }
 }
 
+template <int SEQ, int W, int NSLOT, int QS>
+void launch_mha(const MhaBlockArgs& a, hipStream_t st) {
+  using L = MhaL<SEQ, W, NSLOT, QS>;
+  static bool attr = false;
+  if (!attr) {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<SEQ, W, NSLOT, QS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::kSmem));
+    attr = true;
+  }
+  hipLaunchKernelGGL((mha_block_kernel<SEQ, W, NSLOT, QS>), dim3((a.S + SEQ - 1) / SEQ), dim3(L::kThreads), L::kSmem, st,
+                     a);
+}
+
 }  // namespace
 
 bool mha_block_supported(int D, int nh, int T, bool bf16) {
@@ -265,22 +306,28 @@ bool mha_block_supported(int D, int nh, int T, bool bf16) {
   return !off && bf16 && D == kD && nh == kNH && T >= 1 && T <= kTP;
 }
 
-void mha_block(const MhaBlockArgs& a, hipStream_t st) {
+void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   SD_CHECK(mha_block_supported(kD, a.nh, a.T, true) && a.D == kD, kErrInvalid, "mha_block: unsupported shape");
   SD_CHECK(a.ldo % 4 == 0, kErrInvalid, "mha_block: output row stride must be a multiple of 4");
   if (a.S <= 0) return;
   SD_CHECK(a.y != nullptr, kErrInvalid, "mha_block: y (LayerNorm'd bf16 rows) is required");
-  static bool attr = false;
-  if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
-    attr = true;
-  }
   const double rows = (double)a.S * a.T;
   const double flops = 2.0 * rows * 3 * kD * kD + 4.0 * a.S * (double)a.T * a.T * kD;
   const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
   ProfScope prof("mha_block", flops, bytes, st);
-  hipLaunchKernelGGL(mha_block_kernel, dim3((a.S + kSeq - 1) / kSeq), dim3(kThreads), kSmemBytes, st, a);
+  // SDIAR_MHA_SEQ2=1: the rounds 2-4 layout (two sequences per 8-wave workgroup, one workgroup per CU);
+  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <2,8,3,48>, 4 <1,4,3,48>
+  static const int var_env = getenv("SDIAR_MHA_SEQ2") ? 1 : getenv("SDIAR_MHA_VARIANT") ? atoi(getenv("SDIAR_MHA_VARIANT")) : 0;
+  const int var = variant >= 0 ? variant : var_env;
+  switch (var) {
+    case 1: launch_mha<2, 8, 3, 64>(a, st); break;
+    case 2: launch_mha<1, 4, 2, 64>(a, st); break;
+    case 3: launch_mha<2, 8, 3, 48>(a, st); break;
+    case 4: launch_mha<1, 4, 3, 48>(a, st); break;
+    case 5: launch_mha<1, 8, 3, 64>(a, st); break;
+    case 6: launch_mha<1, 8, 2, 48>(a, st); break;
+    default: launch_mha<1, 4, 2, 48>(a, st); break;
+  }
   SD_LAUNCH_CHECK();
 }
 

@@ -34,6 +34,20 @@ def _plan_i32(plan: WindowPlan, name: str, arr, dev, w0: int = 0, w1: int = None
     return t
 
 
+def _ts_block(ts, dev, NS: int, B: int):
+    """(B, NS, E) contiguous copy of the meeting's target-speaker embeddings, cached per (tensor, B): every
+    window of a meeting takes the same speakers."""
+    import torch
+    key = ("ts", ts.data_ptr(), tuple(ts.shape), ts._version, B, str(dev))
+    t = _DEV_CACHE.get(key)
+    if t is None:
+        if len(_DEV_CACHE) > 256:
+            _DEV_CACHE.clear()
+        t = ts.to(dev, torch.float32).reshape(1, NS, -1).expand(B, -1, -1).contiguous()
+        _DEV_CACHE[key] = t
+    return t
+
+
 class TSVADPipeline:
     def __init__(self, model: TSVADModel, segment_shift: int = 1, batch_size: int = 64):
         self.model = model
@@ -49,34 +63,46 @@ class TSVADPipeline:
         return plan_windows(n_labels, self.cfg.rs_len, self.segment_shift, self.cfg.label_rate,
                             self.cfg.sample_rate)
 
-    def window_logits(self, wav, ts, plan: WindowPlan, w0: int = 0, w1: int = None, out=None):
+    def window_logits(self, wav, ts, plan: WindowPlan, w0: int = 0, w1: int = None, out=None, check: bool = True):
         """Logits of windows [w0, w1) -> (w1-w0, NS, chunk) (cols >= window len unused).
-        wav: (n_samples,) CUDA float32 covering at least those windows' audio."""
+        wav: (n_samples,) CUDA float32 covering at least those windows' audio.  check: wait for the stream and
+        raise if a persistent recurrence lost co-residency (posteriors() checks once, after its average)."""
         import torch
         dev = self.model.device
         w1 = plan.n_win if w1 is None else w1
         NS, chunk = self.model.max_num_speaker, plan.chunk
         if out is None:
-            out = torch.zeros(w1 - w0, NS, chunk, device=dev, dtype=torch.float32)
+            out = torch.empty(w1 - w0, NS, chunk, device=dev, dtype=torch.float32)
         if w1 <= w0:
             return out
+        # every host-side step (plan slices, device tables, the per-batch target-speaker block) comes before the
+        # first launch, so the fbank -> window CMN -> forward launches reach the GPU back to back (round 4's
+        # trace: 0.59 ms of idle GPU between the fbank and the first window CMN)
         spl = plan.samples_per_label
         s0 = int(plan.starts[w0]) * spl
         s1 = min(wav.numel(), int(plan.ends[w1 - 1]) * spl)
-        feats = kaldi_fbank(wav[s0:s1])
         f0 = int(plan.fbank_start[w0])
         fstart = _plan_i32(plan, "fstart", plan.fbank_start[w0:w1] - f0, dev, w0, w1)
         fn = _plan_i32(plan, "fn", plan.fbank_n[w0:w1], dev, w0, w1)
-        ts_b = ts.to(dev, torch.float32).reshape(1, NS, -1)
-        for b0, b1, T_out, T_lab in self.device_batches(plan, w0, w1):
+        batches = self.device_batches(plan, w0, w1)
+        ts_all = _ts_block(ts, dev, NS, max(b1 - b0 for b0, b1, _, _ in batches))
+        feats = kaldi_fbank(wav[s0:s1])
+        for b0, b1, T_out, T_lab in batches:
             ref = window_cmn(feats, fstart[b0 - w0:b1 - w0], fn[b0 - w0:b1 - w0], T_out)
-            lg = self.model.forward(ref, ts_b.expand(b1 - b0, -1, -1).contiguous(), T_lab, check=False,
-                                    **self._fwd_kw)
-            out[b0 - w0:b1 - w0, :, :T_lab] = lg
+            dst = out[b0 - w0:b1 - w0]
+            if T_lab == chunk:           # whole rows: the forward writes straight into the output
+                self.model.forward(ref, ts_all[: b1 - b0], T_lab, out=dst, check=False, **self._fwd_kw)
+            else:
+                dst[:, :, :T_lab] = self.model.forward(ref, ts_all[: b1 - b0], T_lab, check=False, **self._fwd_kw)
+                dst[:, :, T_lab:] = 0.0
+        if check:
+            self._check()
+        return out
+
+    def _check(self):
         status = getattr(self.model, "status", None)
         if status is not None:
             status()          # one wait per call: a lost LSTM co-residency raises here
-        return out
 
     def device_batches(self, plan: WindowPlan, w0: int, w1: int):
         """Reference batches (batch_size windows, zero-padded to their own max length,
@@ -134,7 +160,9 @@ class TSVADPipeline:
         plan = self.plan(n_labels)
         world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
         if world == 1:
-            return self.average(self.window_logits(wav, ts, plan), plan)
+            post = self.average(self.window_logits(wav, ts, plan, check=False), plan)
+            self._check()      # after the average is enqueued: no idle GPU between the forward and it
+            return post
         rank = dist.get_rank(group)
         w0, w1 = shard_batches(plan, self.batch_size, world, rank)
         local = self.window_logits(wav, ts, plan, w0, w1)
@@ -151,7 +179,13 @@ def gather_windows(local, plan: WindowPlan, batch_size: int, world: int, group=N
     maxn = max(b - a for a, b in ranges)
     pad = torch.zeros(maxn, *local.shape[1:], device=local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local
-    allg = torch.empty(world * maxn, *local.shape[1:], device=local.device, dtype=local.dtype)
-    dist.all_gather_into_tensor(allg, pad, group=group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo gathers host tensors: stage through host memory (RCCL, the multi-GPU backend, gathers in HBM)
+        allg = torch.empty(world * maxn, *local.shape[1:], dtype=local.dtype)
+        dist.all_gather_into_tensor(allg, pad.cpu(), group=group)
+        allg = allg.to(local.device)
+    else:
+        allg = torch.empty(world * maxn, *local.shape[1:], device=local.device, dtype=local.dtype)
+        dist.all_gather_into_tensor(allg, pad, group=group)
     parts = [allg[r * maxn: r * maxn + (b - a)] for r, (a, b) in enumerate(ranges)]
     return torch.cat(parts, 0)

@@ -135,10 +135,10 @@ class StreamingWindowDecoder:
         self.device = model.device
         self.chunk, self.left = decoding_chunk_size, num_decoding_left_chunks
 
-    def forward(self, ref, ts, T_lab: int, check: bool = True):
+    def forward(self, ref, ts, T_lab: int, check: bool = True, out=None):
         """check: accepted for TSVADModel's signature; the streaming model has no LSTM to report."""
         import torch
         n = self.model.subsampling_rate * T_lab
         if ref.shape[1] != n:
             ref = torch.nn.functional.pad(ref, (0, 0, 0, n - ref.shape[1]))
-        return self.model.forward_windows(ref.contiguous(), ts, T_lab, self.chunk, self.left)
+        return self.model.forward_windows(ref.contiguous(), ts, T_lab, self.chunk, self.left, out=out)

@@ -47,7 +47,7 @@ class OraclePipeline(TSVADPipeline):
         self.sd = sd
 
     @torch.no_grad()
-    def window_logits(self, wav, ts, plan, w0=0, w1=None, out=None):
+    def window_logits(self, wav, ts, plan, w0=0, w1=None, out=None, check=True):
         w1 = plan.n_win if w1 is None else w1
         out = torch.zeros(w1 - w0, self.model.max_num_speaker, plan.chunk)
         windows = [(int(plan.starts[i]), int(plan.ends[i])) for i in range(w0, w1)]

@@ -105,3 +105,16 @@ def test_timeout_report_survives_later_clean_forwards(gpu, name, code):
     r = _child(code, 0, launches=1)
     assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-1500:])
     assert "RAISED:" in r.stdout and "co-residency" in r.stdout, r.stdout
+
+
+def test_lstm_exchange_probes(gpu):
+    """Both exchange-floor probes of the persistent recurrence run to completion (no poll times out) and
+    report a plausible per-step time: the recurrence's counter protocol (sd_probe_lstm_handoff) and the
+    data-tagged 8-byte granule transport (sd_probe_lstm_granule, MI355X guide handoff-1to1)."""
+    import ctypes
+    from speaker_diarization_amd import _lib
+    for probe in ("sd_probe_lstm_handoff", "sd_probe_lstm_granule"):
+        v = ctypes.c_float()
+        _lib.call(probe, 2000, ctypes.byref(v), _lib.stream_ptr())
+        print(f"{probe}: {v.value:.3f} us per step")
+        assert 0.05 < v.value < 50.0

@@ -27,7 +27,7 @@ GROUPS = {
                                                         "SDIAR_FCM_STEM_VALU": "1"},
     "fcmband_off+areg_off+ringpersist_off+xremap_off": {
         "SDIAR_NO_FCM_BAND": "1", "SDIAR_NO_AREG_GEMM": "1", "SDIAR_NO_RING_PERSIST": "1",
-        "SDIAR_ATTN_NO_XREMAP": "1", "SDIAR_RP_STAGGER": "0"},
+        "SDIAR_ATTN_NO_XREMAP": "1", "SDIAR_RP_STAGGER": "0", "SDIAR_MHA_SEQ2": "1"},
     "fcmfuse_off+ring_off+stream_off+lstmseq_off": {"SDIAR_NO_FCM_FUSE": "1", "SDIAR_NO_RING_GEMM": "1",
                                                      "SDIAR_NO_STREAM_GEMM": "1", "SDIAR_NO_LSTM_SEQ": "1"},
 }
@@ -173,6 +173,43 @@ def test_cam_two_stream_slices_bit_identical(gpu):
         env.pop("SDIAR_CAM_ONE_STREAM", None)
         if one:
             env["SDIAR_CAM_ONE_STREAM"] = "1"
+        r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
+                           text=True, timeout=110, env=env)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
+        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
+        hashes.append(line[0])
+    assert hashes[0] == hashes[1], hashes
+
+
+def test_mha_block_layouts_bit_identical(gpu):
+    """mha_block's two layouts (round 5: one sequence per 4-wave workgroup, two workgroups per CU, 48-wide Q/K
+    rows; rounds 2-4: two sequences per 8-wave workgroup, SDIAR_MHA_SEQ2=1) do the same arithmetic in the same
+    order: the TS-VAD logits must be bit-identical (both variants, 384 windows: two-stream slices too)."""
+    hashes = []
+    for seq2 in (False, True):
+        env = dict(os.environ)
+        env.pop("SDIAR_MHA_SEQ2", None)
+        if seq2:
+            env["SDIAR_MHA_SEQ2"] = "1"
+        r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
+                           text=True, timeout=110, env=env)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
+        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
+        hashes.append(line[0])
+    assert hashes[0] == hashes[1], hashes
+
+
+@pytest.mark.parametrize("k", ["3", "4"])
+def test_pipelined_slices_bit_identical(gpu, k):
+    """SDIAR_SLICES=K pipelines K window slices over the two streams (trunk i+1 beside conformer stack i,
+    tsvad.cpp); every kernel up to the BiLSTM computes a window independently of its slice, so the logits
+    must equal the default two-slice schedule's bit for bit."""
+    hashes = []
+    for slices in (None, k):
+        env = dict(os.environ)
+        env.pop("SDIAR_SLICES", None)
+        if slices:
+            env["SDIAR_SLICES"] = slices
         r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
                            text=True, timeout=110, env=env)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]

@@ -80,8 +80,12 @@ def main(d):
             ach = r["flops_per_launch"] / (per_launch_ns * 1e-9) / 1e12
         else:
             ach = r["algorithmic_bytes_per_launch"] / (per_launch_ns * 1e-9) / 1e9
+        # steps in the PROFILED run: its rocprof launches / the line's launches per step (the profiled command's
+        # step count differs from the line's steps + warmup: the kernel-timer step, parity legs)
+        per_step = r.get("launches") or 0
+        prof_steps = f"{calls / per_step:.1f} steps of {per_step} launches" if per_step else f"line steps {steps}"
         out.append(f"{wl}: {r['kernel']} ({r['bound']}) rocprof {calls} launches over the profiled run "
-                   f"({calls / max(steps, 1):.0f} per step), {per_launch_ns / 1e6:.4f} ms each -> {ach:.1f} {r['unit']} "
+                   f"({prof_steps}), {per_launch_ns / 1e6:.4f} ms each -> {ach:.1f} {r['unit']} "
                    f"= frac {ach / r['peak']:.4f} (line, live HIP-event timer: {r['avg_launch_ms']} ms, frac {r['frac']})")
     print("\n".join(out))
 

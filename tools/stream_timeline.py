@@ -133,6 +133,16 @@ def main():
             gaps.append(k["s"] - cur_end)
         cur_end = max(cur_end, k["e"])
     print(f"idle gaps (no kernel on any stream): {len(gaps)} totalling {ms(sum(gaps)):.3f} ms, largest {ms(max(gaps) if gaps else 0):.3f}")
+    cur_end, prev = allk[0]["e"], allk[0]
+    big = []
+    for k in allk[1:]:
+        if k["s"] > cur_end:
+            big.append((k["s"] - cur_end, cur_end - t0, prev["name"], k["name"]))
+        if k["e"] >= cur_end:
+            cur_end, prev = k["e"], k
+    short = lambda n: re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))[:48]  # noqa: E731
+    for gap, at, a_, b_ in sorted(big, reverse=True)[:6]:
+        print(f"   gap {ms(gap):.3f} ms at {ms(at):.3f}: after {short(a_)} -> {short(b_)}")
     # per-kernel duration table for the step (name -> n, summed)
     agg = defaultdict(lambda: [0, 0])
     for k in st:
