@@ -234,10 +234,9 @@ def speech_encoder_out(sd, ref_speech):
 
 
 @torch.no_grad()
-def tsvad_forward(sd, cfg, ref_speech, target_speech, max_len, features=None):
+def tsvad_forward(sd, cfg, ref_speech, target_speech, max_len):
     """TSVADModel.forward in eval (model.py:899-921): ref_speech (B, T_fb, 80),
-    target_speech (B, NS, 192) -> logits (B, NS, max_len).  features (a list, tools only): receives the
-    final Linear's input (B, max_len, F) (tools/fit_probe_fc.py)."""
+    target_speech (B, NS, 192) -> logits (B, NS, max_len)."""
     ns = cfg.max_num_speaker
     x = speech_encoder_out(sd, ref_speech)
     if cfg.variant == 1:
@@ -259,8 +258,6 @@ def tsvad_forward(sd, cfg, ref_speech, target_speech, max_len, features=None):
             outs.append(conformer(cat, torch.full((B,), T), sd, "single_backend."))
         cat = torch.cat(outs, dim=-1)
         h, _ = lstm(cat, sd, "multi_backend.", bidirectional=True)
-        if features is not None:
-            features.append(h)
         return F.linear(h, sd["fc.weight"], sd["fc.bias"]).transpose(1, 2)
     # forward_common (model.py:758-897)
     gap = x.size(-1) - max_len
@@ -284,6 +281,4 @@ def tsvad_forward(sd, cfg, ref_speech, target_speech, max_len, features=None):
     cat = positional_encoding(cat.permute(2, 0, 1), sd)
     for l in range(cfg.num_transformer_layer):
         cat = transformer_layer(cat, sd, f"multi_backend.layers.{l}.", nh)
-    if features is not None:
-        features.append(cat.transpose(0, 1))
     return F.linear(cat.transpose(0, 1), sd["fc.weight"], sd["fc.bias"]).transpose(1, 2)
