@@ -268,6 +268,7 @@ struct RowProgArgs {
   // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog(); SDIAR_RP_STAGGER scales it):
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
+  int prio = 0;      // 1: waves 4-7 run at s_setprio 1 (A/B: SDIAR_RP_PRIO)
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

@@ -35,17 +35,11 @@ def _plan_i32(plan: WindowPlan, name: str, arr, dev, w0: int = 0, w1: int = None
 
 
 def _ts_block(ts, dev, NS: int, B: int):
-    """(B, NS, E) contiguous copy of the meeting's target-speaker embeddings, cached per (tensor, B): every
-    window of a meeting takes the same speakers."""
+    """(B, NS, E) contiguous copy of the meeting's target-speaker embeddings (every window of a meeting takes the
+    same speakers).  Not cached: a cache keyed by the tensor's address served a freed-and-reused allocation's
+    stale rows in a later call (tests/test_gpu_shard.py, round 5)."""
     import torch
-    key = ("ts", ts.data_ptr(), tuple(ts.shape), ts._version, B, str(dev))
-    t = _DEV_CACHE.get(key)
-    if t is None:
-        if len(_DEV_CACHE) > 256:
-            _DEV_CACHE.clear()
-        t = ts.to(dev, torch.float32).reshape(1, NS, -1).expand(B, -1, -1).contiguous()
-        _DEV_CACHE[key] = t
-    return t
+    return ts.to(dev, torch.float32).reshape(1, NS, -1).expand(B, -1, -1).contiguous()
 
 
 class TSVADPipeline:
