@@ -465,6 +465,7 @@ __global__ __launch_bounds__(256) void lstm_granule_probe_kernel(int steps, uint
     u32x4_t f[H / 32][2];
     unsigned spins = 0;
     for (;;) {
+      asm volatile("" ::: "memory");   // every poll re-reads the granules (the compiler would hoist the loads)
 #pragma unroll
       for (int kc = 0; kc < H / 32; ++kc)
 #pragma unroll

@@ -3,9 +3,7 @@
 set -uo pipefail
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 O=gpurun_out/r05b; mkdir -p $O
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_der_spread.py tests/test_gpu_fseend_stream.py tests/test_gpu_tsvad.py tests/test_gpu_cam_dense.py \
-  tests/test_gpu_tsvad_graph.py tests/test_gpu_shard.py tests/test_gpu_switches.py tests/test_gpu_mha_block.py tests/test_gpu_two_rank.py tests/test_gpu_lstm_status.py -s > $O/pytest.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 300 python3 -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_lstm_status.py::test_lstm_exchange_probes -s > $O/pytest.log 2>&1; echo "pytest rc=$?"
 tail -3 $O/pytest.log
 timeout -k 10 400 python3 bench.py --workload c2 --steps 10 --warmup 3 --no-c4-ref > $O/bench_c2.json 2> $O/bench_c2.err || { echo bench failed; tail -20 $O/bench_c2.err; exit 1; }
 echo bench ok
@@ -14,6 +12,8 @@ for r in 1; do
   timeout -k 10 300 python3 bench.py --workload c2 --steps 10 --warmup 3 --no-cpu-baseline --no-c4-ref --no-kernel-timing > $O/bench_c2_seq1_$r.json 2>/dev/null || exit 1
 done
 echo ab ok
+SDIAR_RP_PRIO=1 timeout -k 10 300 python3 bench.py --workload c2 --steps 10 --warmup 3 --no-cpu-baseline --no-c4-ref --no-kernel-timing > $O/bench_c2_prio1.json 2>/dev/null || exit 1
+echo prio ok
 for r in 1 2; do
   for k in 3 4; do
     SDIAR_SLICES=$k timeout -k 10 300 python3 bench.py --workload c2 --steps 10 --warmup 3 --no-cpu-baseline --no-c4-ref --no-kernel-timing > $O/bench_c2_slices${k}_$r.json 2>/dev/null || exit 1
