@@ -21,7 +21,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GROUPS = {
     "rowprog_off+tiny_off+hpw2+splitk_off+camdense_off": {"SDIAR_NO_ROWPROG": "1", "SDIAR_NO_ATTN_TINY": "1",
                                                           "SDIAR_ATTN_HPW": "2", "SDIAR_NO_SPLITK": "1",
-                                                          "SDIAR_NO_CAM_DENSE": "1"},
+                                                          "SDIAR_NO_CAM_DENSE": "1", "SDIAR_LSTM_GRANULE": "1"},
     "mha_off+long_off+camfused_off+dwpk_off+stemvalu": {"SDIAR_NO_MHA_BLOCK": "1", "SDIAR_NO_ATTN_LONG": "1",
                                                         "SDIAR_NO_CAM_FUSED": "1", "SDIAR_NO_DWCONV_PK": "1",
                                                         "SDIAR_FCM_STEM_VALU": "1"},
@@ -181,38 +181,24 @@ def test_cam_two_stream_slices_bit_identical(gpu):
     assert hashes[0] == hashes[1], hashes
 
 
-def test_mha_block_layouts_bit_identical(gpu):
-    """mha_block's two layouts (round 5: one sequence per 4-wave workgroup, two workgroups per CU, 48-wide Q/K
-    rows; rounds 2-4: two sequences per 8-wave workgroup, SDIAR_MHA_SEQ2=1) do the same arithmetic in the same
-    order: the TS-VAD logits must be bit-identical (both variants, 384 windows: two-stream slices too)."""
-    hashes = []
-    for seq2 in (False, True):
-        env = dict(os.environ)
-        env.pop("SDIAR_MHA_SEQ2", None)
-        if seq2:
-            env["SDIAR_MHA_SEQ2"] = "1"
-        r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
-                           text=True, timeout=110, env=env)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
-        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
-        hashes.append(line[0])
-    assert hashes[0] == hashes[1], hashes
+def _tsvad_hash(extra_env):
+    env = dict(os.environ)
+    for k in ("SDIAR_MHA_SEQ2", "SDIAR_SLICES", "SDIAR_LSTM_GRANULE"):
+        env.pop(k, None)
+    env.update(extra_env)
+    r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
+                       text=True, timeout=110, env=env)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
+    assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
+    return line[0]
 
 
-@pytest.mark.parametrize("k", ["3", "4"])
-def test_pipelined_slices_bit_identical(gpu, k):
-    """SDIAR_SLICES=K pipelines K window slices over the two streams (trunk i+1 beside conformer stack i,
-    tsvad.cpp); every kernel up to the BiLSTM computes a window independently of its slice, so the logits
-    must equal the default two-slice schedule's bit for bit."""
-    hashes = []
-    for slices in (None, k):
-        env = dict(os.environ)
-        env.pop("SDIAR_SLICES", None)
-        if slices:
-            env["SDIAR_SLICES"] = slices
-        r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
-                           text=True, timeout=110, env=env)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("HASH ")]
-        assert r.returncode == 0 and line, (r.stdout[-2000:], r.stderr[-3000:])
-        hashes.append(line[0])
-    assert hashes[0] == hashes[1], hashes
+@pytest.mark.parametrize("switch", [{"SDIAR_MHA_SEQ2": "1"}, {"SDIAR_SLICES": "3"}, {"SDIAR_SLICES": "4"},
+                                    {"SDIAR_LSTM_GRANULE": "1"}], ids=["mha_seq2", "slices3", "slices4", "lstm_granule"])
+def test_schedule_switches_bit_identical(gpu, switch):
+    """Switches that change only the schedule or the transport, never the arithmetic, must leave the TS-VAD
+    logits (ots_vad v1 with its BiLSTM, and the CAM++/transformer model; 400 windows: two-stream slices) bit
+    for bit unchanged: mha_block's rounds 2-4 layout (two sequences per 8-wave workgroup) vs round 5's (one per
+    4-wave workgroup, two workgroups per CU); K window slices pipelined over the two streams (trunk i+1 beside
+    conformer stack i) vs the default two; the BiLSTM's h exchange on tagged 8-byte granules vs the counter."""
+    assert _tsvad_hash(switch) == _tsvad_hash({})
