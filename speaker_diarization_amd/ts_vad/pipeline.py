@@ -54,8 +54,16 @@ class TSVADPipeline:
         self._fwd_kw = {"forward_batch": self.batch_size} if isinstance(model, TSVADModel) else {}
 
     def plan(self, n_labels: int) -> WindowPlan:
-        return plan_windows(n_labels, self.cfg.rs_len, self.segment_shift, self.cfg.label_rate,
-                            self.cfg.sample_rate)
+        """The meeting's window plan, built once per label count (the host work between two steps: the
+        plan, its fbank counts and the batch grouping are pure functions of n_labels)."""
+        cache = self.__dict__.setdefault("_plans", {})
+        p = cache.get(n_labels)
+        if p is None:
+            if len(cache) > 64:
+                cache.clear()
+            p = cache[n_labels] = plan_windows(n_labels, self.cfg.rs_len, self.segment_shift, self.cfg.label_rate,
+                                               self.cfg.sample_rate)
+        return p
 
     def window_logits(self, wav, ts, plan: WindowPlan, w0: int = 0, w1: int = None, out=None, check: bool = True):
         """Logits of windows [w0, w1) -> (w1-w0, NS, chunk) (cols >= window len unused).
@@ -103,6 +111,10 @@ class TSVADPipeline:
         ts_vad_dataset.py:664-701) of [w0, w1); consecutive batches with the same
         padded shape are fused into one device launch of up to model.max_batch
         windows — identical inputs per window, fewer and larger kernels."""
+        key = ("_batches", self.batch_size, self.model.max_batch, w0, w1)
+        hit = plan.__dict__.get(key)
+        if hit is not None:
+            return list(hit)
         groups = []
         for b0 in range(w0, w1, self.batch_size):
             b1 = min(w1, b0 + self.batch_size)
@@ -111,6 +123,7 @@ class TSVADPipeline:
                 groups[-1] = (groups[-1][0], b1) + key
             else:
                 groups.append((b0, b1) + key)
+        plan.__dict__[("_batches", self.batch_size, self.model.max_batch, w0, w1)] = tuple(groups)
         return groups
 
     @staticmethod
