@@ -52,6 +52,9 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
   sws_ = wsb<float>((size_t)cfg.n_heads * rd * D);
   scnt_ = wsb<unsigned>(1);
   SD_HIP(hipMemset(scnt_, 0, sizeof(unsigned)));
+  fws_ = wsb<float>((size_t)128 * 8 * D);
+  fcnt_ = wsb<unsigned>(1);
+  SD_HIP(hipMemset(fcnt_, 0, sizeof(unsigned)));
   for (int l = 0; l < cfg.enc_n_layers; ++l) kv_enc_.push_back(arena_.alloc((size_t)cap_ * 2 * D * es_));
   for (int a = 0; a < cfg.dec_n_layers; ++a) kv_dec_.push_back(arena_.alloc((size_t)cap_ * C_ * 2 * D * es_));
   hist_ = wsb<float>((size_t)cap_ * D);
@@ -119,6 +122,24 @@ void gemm_fused(ConvGemmArgs p, const PendingLn* ln, const KvEpi* kv, int D, boo
 
 }  // namespace
 
+// linear1 -> relu -> linear2 of a transformer layer on n rows with the pending post-LN folded in: one stream_ffn_pair
+// launch when it applies (SDIAR_NO_FFN_PAIR=1: the two skinny GEMMs, for A/B), the result in T_ either way
+void FsEendStream::ffn(const PackedW& l1, const float* b1, const PackedW& l2, const float* b2, const float* ln_x,
+                       const void* ln_t, const float* ln_g, const float* ln_b, float* ln_out, int n, hipStream_t st) {
+  const int D = m_.cfg_.n_units;
+  FfnPairArgs f;
+  f.ln_x = ln_x; f.ln_t = ln_t; f.t_bf16 = bf_; f.ln_g = ln_g; f.ln_b = ln_b; f.ln_out = ln_out;
+  f.w1 = l1.w; f.b1 = b1; f.w2 = l2.w; f.b2 = b2; f.w_bf16 = bf_;
+  f.out = T_; f.out_bf16 = bf_; f.ws = fws_; f.cnt = fcnt_; f.n = n; f.D = D; f.F = l1.N;
+  if (l1.K == D && l2.K == l1.N && l2.N == D && stream_ffn_pair(f, st)) return;
+  const Tens h{H_, bf_}, t{T_, bf_};
+  const PendingLn ln{ln_x, ln_t, ln_g, ln_b, ln_out};
+  ConvGemmArgs p = lin(Tens{ln_out, false}, n, D, l1, b1, h, l1.N);
+  p.act = kActRelu;
+  gemm_fused(p, &ln, nullptr, D, bf_, st);
+  conv_gemm(lin(h, n, l1.N, l2, b2, t, D), bf_, st);
+}
+
 void FsEendStream::enc_chunk(hipStream_t st) {
   // MaskedTransformerEncoderModel.forward (fs_eend.py:178-204) on the chunk's c rows.  Every
   // post-LN (norm1/norm2, fs_eend.py via nn.TransformerEncoderLayer) is applied while the
@@ -144,12 +165,8 @@ void FsEendStream::enc_chunk(hipStream_t st) {
     a.pos = state_; a.delay = 0; a.max_keys = cap_; a.n_blocks = n_blocks_; a.ws = ws_; a.io_bf16 = bf_; a.cnt = dcnt_;
     attn_decode(a, st);
     conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
-    ln = PendingLn{xb[xi], T_, L.n1g, L.n1b, xb[xi ^ 1]};
     xi ^= 1;
-    ConvGemmArgs p = lin(Tens{xb[xi], false}, c, D, L.l1, L.b1, h, L.l1.N);
-    p.act = kActRelu;
-    gemm_fused(p, &ln, nullptr, D, bf_, st);
-    conv_gemm(lin(h, c, L.l1.N, L.l2, L.b2, t, D), bf_, st);
+    ffn(L.l1, L.b1, L.l2, L.b2, xb[xi ^ 1], T_, L.n1g, L.n1b, xb[xi], c, st);
     ln = PendingLn{xb[xi], T_, L.n2g, L.n2b, xb[xi ^ 1]};
     xi ^= 1;
   }
@@ -247,13 +264,9 @@ void FsEendStream::dec_chunk(hipStream_t st) {
       attention(s, bf_, st);
       conv_gemm(lin(ao, n, D, f.out2, f.out2_b, t, D), bf_, st);
     }
-    ln = PendingLn{ab[ai], T_, f.n21g, f.n21b, ab[ai ^ 1]};
     ai ^= 1;
     // (3) feed-forward
-    ConvGemmArgs p = lin(Tens{ab[ai], false}, n, D, f.l1, f.b1, h, f.l1.N);
-    p.act = kActRelu;
-    gemm_fused(p, &ln, nullptr, D, bf_, st);
-    conv_gemm(lin(h, n, f.l1.N, f.l2, f.b2, t, D), bf_, st);
+    ffn(f.l1, f.b1, f.l2, f.b2, ab[ai ^ 1], T_, f.n21g, f.n21b, ab[ai], n, st);
     ln = PendingLn{ab[ai], T_, f.n22g, f.n22b, ab[ai ^ 1]};
     ai ^= 1;
     pending = true;
@@ -441,6 +454,7 @@ void FsEendStream::reset(hipStream_t st) {
   // also clears what an interrupted launch may have left
   SD_HIP(hipMemsetAsync(dcnt_, 0, (size_t)C_ * m_.cfg_.n_heads * sizeof(unsigned), st));
   SD_HIP(hipMemsetAsync(scnt_, 0, sizeof(unsigned), st));
+  SD_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned), st));
   // wait for the chunks flush() / push*() enqueued: they read bound_ and replay the graphs destroyed below,
   // and set_audio() rewrites bound_ with a synchronous copy that is not ordered after a non-blocking st
   SD_HIP(hipStreamSynchronize(st));

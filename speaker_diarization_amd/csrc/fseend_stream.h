@@ -48,6 +48,8 @@ class FsEendStream {
 
  private:
   void enc_chunk(hipStream_t st);
+  void ffn(const PackedW& l1, const float* b1, const PackedW& l2, const float* b2, const float* ln_x, const void* ln_t,
+           const float* ln_g, const float* ln_b, float* ln_out, int n, hipStream_t st);
   int after_enc(int n, float* preds, int cap, hipStream_t st);   // cursor bookkeeping + decoder chunks
   void dec_chunk(hipStream_t st);
   void run(int which, hipStream_t st);   // 0 encoder, 1 decoder: graph replay or direct launches
@@ -71,6 +73,8 @@ class FsEendStream {
   unsigned* dcnt_ = nullptr;           // attn_decode's per-(sequence, head) block counters (0..nblk-1, wrap)
   float* sws_ = nullptr;               // stream_slot_block's per-head out-projection partials
   unsigned* scnt_ = nullptr;           // its arrival counter (0..n_heads-1, wraps per launch)
+  float* fws_ = nullptr;               // stream_ffn_pair's down-projection partials
+  unsigned* fcnt_ = nullptr;           // its arrival counter (wraps per launch)
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

@@ -525,6 +525,31 @@ struct SlotBlockArgs {
   float scale = 0.125f;
 };
 bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st);
+// FS-EEND streaming feed-forward sub-block (nn.TransformerEncoderLayer linear1 -> relu -> linear2, fs_eend.py:
+// 196-204 / 474-477) for one chunk of n rows, its input post-LN folded in:  y = LN(x + t) (-> ln_out);
+// out = relu(y W1ᵀ + b1) W2ᵀ + b2.  ONE launch: each workgroup owns a slice of the hidden units, its down-projection
+// partial is published write-through and the last workgroup to count itself sums the partials in workgroup order
+// (cnt wraps to 0 per launch, zeroed once).  Supported: D == 256, F == 2048, 1 <= n <= 8, 16-B aligned operands;
+// returns false otherwise (caller runs the two skinny GEMMs).  ws: 128 * 8 * D floats.
+struct FfnPairArgs {
+  const float* ln_x = nullptr;
+  const void* ln_t = nullptr;
+  bool t_bf16 = false;
+  const float *ln_g = nullptr, *ln_b = nullptr;
+  float eps = 1e-5f;
+  float* ln_out = nullptr;
+  const void* w1 = nullptr;   // packed [F][D]
+  const float* b1 = nullptr;
+  const void* w2 = nullptr;   // packed [D][F]
+  const float* b2 = nullptr;
+  bool w_bf16 = false;
+  void* out = nullptr;        // (n, D), bf16 when out_bf16
+  bool out_bf16 = false;
+  float* ws = nullptr;
+  unsigned* cnt = nullptr;
+  int n = 1, D = 256, F = 2048;
+};
+bool stream_ffn_pair(const FfnPairArgs& a, hipStream_t st);
 void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,

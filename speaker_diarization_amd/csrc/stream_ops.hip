@@ -26,6 +26,7 @@
 //                   emb[:ilen] re-pad of fs_eend.py:83-84)
 //   cursor_advance  cursor[i] += c (+ optional mirror), the graph's last node
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -630,6 +631,154 @@ __global__ __launch_bounds__(512) void slot_block_kernel(SlotBlockArgs a) {
 #endif
 }
 
+// stream_ffn_pair (kernels.h).  grid G = F / FC, 256 threads; workgroup g owns hidden units [g FC, (g + 1) FC):
+//   y = LN(x + t) (every workgroup; workgroup 0 stores it as the next residual), h_u = relu(y . W1[u] + b1[u]) for
+//   its FC units (LPU = 256 / FC lanes per unit, packed K pieces of 4 so the LDS reads are conflict-free), then
+//   thread j's partial of output feature j over those units, published write-through; the last workgroup to count
+//   itself sums the G partials in workgroup order (4 g-parts per column quad, then the parts in order) + b2.
+// One launch per FFN instead of two: the hidden layer never leaves the workgroup (fp32; the two-launch path
+// stores it as the activation dtype), and the down-projection's split-K seam is a last-arriver merge.
+template <bool WBF, int NR, int FC, int G>
+__global__ __launch_bounds__(256) void ffn_pair_kernel(FfnPairArgs a) {
+  using V = WVec<WBF>;
+  constexpr int D = kSlotD, VE = V::VE;
+  constexpr int LPU = 256 / FC;          // lanes per hidden unit
+  constexpr int NJ = D / 4 / LPU;        // K pieces of 4 per lane
+  constexpr int W2V = FC / VE;           // 16-B vectors of a thread's W2 slice
+  constexpr int GP = G / 4;              // partials per thread and row in the merge
+  constexpr int RB = GP >= 48 ? 1 : 48 / GP;   // rows merged per round trip (<= 48 loads in flight)
+  static_assert(FC * LPU == 256 && NJ * LPU * 4 == D && W2V * VE == FC && G % 4 == 0, "ffn_pair geometry");
+  typedef std::conditional_t<WBF, uint2, uint4> P4;
+  __shared__ float ys[NR][D];
+  __shared__ float hs[NR][FC];
+  __shared__ float4 red[4][RB][64];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = blockIdx.x, n = a.n;
+  const int u = tid / LPU, kp = tid % LPU;
+  // the thread's weights first, as one batch: W1 pieces (unit u, K = 4 (kp + j LPU) ..) and its W2 slice (row tid)
+  const int64_t urow = (int64_t)(g * FC + u) * D;
+  P4 w1[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    w1[j] = *reinterpret_cast<const P4*>(static_cast<const char*>(a.w1) + (urow + 4 * (kp + j * LPU)) * (WBF ? 2 : 4));
+  uint4 w2[W2V];
+#pragma unroll
+  for (int v = 0; v < W2V; ++v) w2[v] = V::load(a.w2, (int64_t)tid * a.F + g * FC + v * VE);
+  const float b1u = a.b1[g * FC + u];
+  __builtin_amdgcn_sched_barrier(0);
+  // y = LN(x + t), one wave per row (rows n..NR-1 repeat row n - 1: no uninitialised LDS is ever read)
+  for (int r = wid; r < NR; r += 4) {
+    const int rr = min(r, n - 1);
+    float4 y[4];
+    ln_row(a.ln_x + (int64_t)rr * D, a.ln_t, a.t_bf16, (int64_t)rr * D, a.ln_g, a.ln_b, a.eps, D, lane, y);
+    *reinterpret_cast<float4*>(&ys[r][lane * 4]) = y[0];
+    if (g == 0 && r < n) *reinterpret_cast<float4*>(a.ln_out + (int64_t)r * D + lane * 4) = y[0];
+  }
+  __syncthreads();
+  // hidden units of the chunk
+  float acc[NR];
+#pragma unroll
+  for (int m = 0; m < NR; ++m) acc[m] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float wv[4];
+    if constexpr (WBF) {
+      wv[0] = __uint_as_float(w1[j].x << 16); wv[1] = __uint_as_float(w1[j].x & 0xffff0000u);
+      wv[2] = __uint_as_float(w1[j].y << 16); wv[3] = __uint_as_float(w1[j].y & 0xffff0000u);
+    } else {
+      wv[0] = __uint_as_float(w1[j].x); wv[1] = __uint_as_float(w1[j].y);
+      wv[2] = __uint_as_float(w1[j].z); wv[3] = __uint_as_float(w1[j].w);
+    }
+    const int k = 4 * (kp + j * LPU);
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+      const float4 y = *reinterpret_cast<const float4*>(&ys[m][k]);
+      acc[m] = fmaf(y.x, wv[0], acc[m]);
+      acc[m] = fmaf(y.y, wv[1], acc[m]);
+      acc[m] = fmaf(y.z, wv[2], acc[m]);
+      acc[m] = fmaf(y.w, wv[3], acc[m]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NR; ++m) {
+#pragma unroll
+    for (int o = 1; o < LPU; o <<= 1) acc[m] += __shfl_xor(acc[m], o, 64);
+    if (kp == 0) hs[m][u] = fmaxf(acc[m] + b1u, 0.f);
+  }
+  __syncthreads();
+  // partial of output feature tid over the chunk's units, published write-through
+  float pr[NR];
+#pragma unroll
+  for (int m = 0; m < NR; ++m) pr[m] = 0.f;
+#pragma unroll
+  for (int v = 0; v < W2V; ++v)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      const float w = V::at(w2[v], e);
+#pragma unroll
+      for (int m = 0; m < NR; ++m) pr[m] = fmaf(hs[m][v * VE + e], w, pr[m]);
+    }
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < NR; ++m)   // rows >= n: an offset past the buffer's range, the store is dropped (no branch)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pr[m]), rw,
+                                          m < n ? (uint32_t)((((int64_t)g * n + m) * D + tid) * 4) : 0xfffffff0u, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)   // wrapping increment: back at 0 after every complete launch
+    last = __builtin_amdgcn_atomic_inc32(a.cnt, (unsigned)G - 1, __ATOMIC_RELAXED, "agent") == (unsigned)G - 1;
+  __syncthreads();
+  if (!last) return;
+  // merge: thread (gp, q) sums column quad q over workgroups [gp GP, (gp + 1) GP) for RB rows per round trip
+  const int q = tid & 63, gp = tid >> 6;
+  for (int m0 = 0; m0 < n; m0 += RB) {
+    u32x4_t pv[RB][GP];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int mr = min(m0 + r, n - 1);
+#pragma unroll
+      for (int i = 0; i < GP; ++i)
+        pv[r][i] = __builtin_amdgcn_raw_buffer_load_b128(
+            rw, (uint32_t)((((int64_t)(gp * GP + i) * n + mr) * D + q * 4) * 4), 0, 16);
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < GP; ++i) {
+        s.x += __uint_as_float(pv[r][i][0]); s.y += __uint_as_float(pv[r][i][1]);
+        s.z += __uint_as_float(pv[r][i][2]); s.w += __uint_as_float(pv[r][i][3]);
+      }
+      red[gp][r][q] = s;
+    }
+    __syncthreads();
+    if (tid < 64 * RB) {
+      const int r = tid >> 6, m = m0 + r;
+      if (m < n) {
+        const float4 bb = *reinterpret_cast<const float4*>(a.b2 + q * 4);
+        float4 v = red[0][r][q];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const float4 t = red[k][r][q];
+          v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+        }
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        const int64_t o = (int64_t)m * D + q * 4;
+        if (a.out_bf16) {
+          uint2 hv;
+          hv.x = (uint32_t)f2bf_bits(v.x) | ((uint32_t)f2bf_bits(v.y) << 16);
+          hv.y = (uint32_t)f2bf_bits(v.z) | ((uint32_t)f2bf_bits(v.w) << 16);
+          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out) + o) = hv;
+        } else {
+          *reinterpret_cast<float4*>(static_cast<float*>(a.out) + o) = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void cursor_advance_kernel(int* cursor, int by, int* mirror) {
   if (threadIdx.x == 0) {
     const int v = *cursor + by;
@@ -716,6 +865,31 @@ bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st) {
   else if (n <= 6) launch_slot_block<6>(a, st);
   else if (n <= 8) launch_slot_block<8>(a, st);
   else launch_slot_block<kSlotRows>(a, st);
+  return true;
+}
+
+template <bool WBF, int NR, int FC, int G>
+static void launch_ffn_pair_t(const FfnPairArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((ffn_pair_kernel<WBF, NR, FC, G>), dim3(G), dim3(256), 0, st, a);
+  SD_LAUNCH_CHECK();
+}
+
+template <int NR, int FC, int G>
+static void launch_ffn_pair(const FfnPairArgs& a, hipStream_t st) {
+  if (a.w_bf16) launch_ffn_pair_t<true, NR, FC, G>(a, st);
+  else launch_ffn_pair_t<false, NR, FC, G>(a, st);
+}
+
+bool stream_ffn_pair(const FfnPairArgs& a, hipStream_t st) {
+  static const bool off = getenv("SDIAR_NO_FFN_PAIR") != nullptr;   // A/B switch: l1 and l2 as two skinny GEMMs
+  if (off || a.D != kSlotD || a.F != 2048 || a.n < 1 || a.n > 8 || !a.ws || !a.cnt || !a.ln_g || !a.ln_b || !a.ln_out)
+    return false;
+  auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (!al(a.w1) || !al(a.w2) || !al(a.ln_x) || !al(a.ln_out) || !al(a.out) || !al(a.ws) || !al(a.b2)) return false;
+  ProfScope prof("ffn_pair", 4.0 * a.n * a.D * a.F, (a.w_bf16 ? 2.0 : 4.0) * 2 * a.D * a.F, st);
+  // one row (the encoder's chunk of 1): 128 workgroups of 16 units; more rows: 64 of 32 (half the partials to merge)
+  if (a.n == 1) launch_ffn_pair<1, 16, 128>(a, st);
+  else launch_ffn_pair<8, 32, 64>(a, st);
   return true;
 }
 

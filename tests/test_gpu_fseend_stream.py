@@ -420,3 +420,47 @@ def test_audio_fusions_bit_identical(gpu, precision, tmp_path):
         res.append(torch.load(path, weights_only=True))
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
+
+
+FFN = r"""
+import sys, torch
+sys.path.insert(0, {repo!r})
+import tests.test_gpu_fseend_stream as t
+from tests.golden.make_golden import eda_inputs
+m = t._model(810, {prec!r}, max_frames=400)
+x = torch.from_numpy(eda_inputs([400], seed=89)[0]).cuda()
+outs = [t._stream_all(m, x, c)[0].cpu() for c in (1, 2)]
+ref, _, _ = m.test([x], [400], max_nspks=6)
+torch.save((outs, ref[0].cpu()), {path!r})
+"""
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_ffn_pair_matches_two_launches(gpu, precision, tmp_path):
+    """stream_ffn_pair (LN + linear1 + relu + linear2 in one launch, the down-projection's split-K partials merged
+    by the last workgroup in workgroup order) against the two skinny GEMMs (SDIAR_NO_FFN_PAIR=1, child processes):
+    chunk 1 runs it for the encoder (1 row, 128 workgroups) and the decoder (6 rows, 64 workgroups), chunk 2 for the
+    encoder's 2 rows (the decoder's 12 rows take the two-launch path); every stream matches test() within the stream
+    tolerances and the two paths agree within 1e-5 (fp32: another summation order) / 2e-2 (bf16: the fused hidden
+    layer stays fp32, the two-launch path stores it as bf16)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for off in (None, "1"):
+        env = dict(os.environ)
+        env.pop("SDIAR_NO_FFN_PAIR", None)
+        if off:
+            env["SDIAR_NO_FFN_PAIR"] = off
+        path = str(tmp_path / f"f_{off}.pt")
+        r = subprocess.run([sys.executable, "-c", FFN.format(repo=repo, prec=precision, path=path)], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(torch.load(path, weights_only=True))
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    for outs, ref in res:
+        for o in outs:
+            np.testing.assert_allclose(o.numpy(), ref.numpy(), atol=tol)
+    for a, b in zip(res[0][0], res[1][0]):
+        d = float((a - b).abs().max())
+        assert d <= (1e-5 if precision == "fp32" else 2e-2), d
