@@ -200,14 +200,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   const int T2 = CamTrunk::out_frames(Tf);
   const bool two = !one_stream && B >= 384;
   if (two && !side_) {
-    // SDIAR_SIDE_PRIO=1 (A/B): the second slice's stream at the device's highest priority -- its CAM++ trunk is
-    // the critical path while it shares the GPU with the first slice's conformer (which has ~10 ms of slack)
-    static const bool side_prio = getenv("SDIAR_SIDE_PRIO") && atoi(getenv("SDIAR_SIDE_PRIO")) > 0;
-    int lo = 0, hi = 0;
-    if (side_prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-      SD_HIP(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
-    else
-      SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     SD_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     SD_HIP(hipEventCreateWithFlags(&ev_gates_, hipEventDisableTiming));
@@ -259,7 +252,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   // first slice's projection cannot touch what the second slice's conformer is using.  SDIAR_LSTM_GATES_TAIL:
   // the projection as one GEMM on the step's tail (A/B switch).
   static const bool one_slice_gates = getenv("SDIAR_LSTM_GATES_TAIL") != nullptr;
-  static const bool side_after_cam = getenv("SDIAR_SIDE_AFTER_CAM") && atoi(getenv("SDIAR_SIDE_AFTER_CAM")) > 0;
   const bool gates_fit = (int64_t)8 * cfg_.lstm_hidden * 4 <= (int64_t)NS * 3 * E * 2;
   bool gates_in_slices = false;
   float* gates = QKV_;
@@ -302,9 +294,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
       BnRelu sb = sd_bn;
       sb.win0 = b0;
       gsp_fc(mx, Bh * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_ + (int64_t)b0 * T3 * SE, SE, s, sb, T3);
-      // SDIAR_SIDE_AFTER_CAM=1 (A/B): the second slice starts once the first slice's trunk is done, so its trunk
-      // pairs with the first slice's conformer only (never with the first trunk, both HBM-bound)
-      if (side_after_cam && b0 == 0) SD_HIP(hipEventRecord(ev_fork_, s));
       conformer_slice(b0, Bh, s);
       if (gates_in_slices) {
         // the BiLSTM's input projection of this slice's rows, on the slice's stream: the first slice's runs
@@ -319,7 +308,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
       }
     };
     slice(0, B1, st);
-    if (side_after_cam) SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
     slice(B1, B - B1, side_);
     SD_HIP(hipEventRecord(ev_join_, side_));
     SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
