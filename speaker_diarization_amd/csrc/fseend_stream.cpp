@@ -53,6 +53,9 @@ FsEendStream::FsEendStream(FsEendModel& m, int chunk, int max_frames, int C, boo
   scnt_ = wsb<unsigned>(1);
   SD_HIP(hipMemset(scnt_, 0, sizeof(unsigned)));
   fws_ = wsb<float>((size_t)128 * 8 * D);
+  ows_ = wsb<float>((size_t)C_ * cfg.n_heads * c_ * D);
+  ocnt_ = wsb<unsigned>((size_t)C_);
+  SD_HIP(hipMemset(ocnt_, 0, (size_t)C_ * sizeof(unsigned)));
   fcnt_ = wsb<unsigned>(1);
   SD_HIP(hipMemset(fcnt_, 0, sizeof(unsigned)));
   for (int l = 0; l < cfg.enc_n_layers; ++l) kv_enc_.push_back(arena_.alloc((size_t)cap_ * 2 * D * es_));
@@ -163,8 +166,10 @@ void FsEendStream::enc_chunk(hipStream_t st) {
     a.out = AO_; a.o_tok = D;
     a.nseq = 1; a.nq = c; a.nh = nh; a.hd = D / nh; a.scale = 1.f / std::sqrt((float)(D / nh));
     a.pos = state_; a.delay = 0; a.max_keys = cap_; a.n_blocks = n_blocks_; a.ws = ws_; a.io_bf16 = bf_; a.cnt = dcnt_;
-    attn_decode(a, st);
-    conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
+    if (L.out_proj.K == D && L.out_proj.N == D) {   // the out-projection inside the attention's merge
+      a.wo = L.out_proj.w; a.bo = L.out_b; a.o2 = T_; a.ws2 = ows_; a.cnt2 = ocnt_;
+    }
+    if (!attn_decode(a, st)) conv_gemm(lin(ao, c, D, L.out_proj, L.out_b, t, D), bf_, st);
     xi ^= 1;
     ffn(L.l1, L.b1, L.l2, L.b2, xb[xi ^ 1], T_, L.n1g, L.n1b, xb[xi], c, st);
     ln = PendingLn{xb[xi], T_, L.n2g, L.n2b, xb[xi ^ 1]};
@@ -245,9 +250,11 @@ void FsEendStream::dec_chunk(hipStream_t st) {
       d.out = AO_; d.o_tok = (int64_t)C * D; d.o_seq = D;
       d.nseq = C; d.nq = c; d.nh = nh; d.hd = D / nh; d.scale = scale;
       d.pos = state_ + 2; d.delay = 0; d.max_keys = cap_; d.n_blocks = n_blocks_; d.ws = ws_; d.io_bf16 = bf_; d.cnt = dcnt_;
-      attn_decode(d, st);
+      if (f.out1.K == D && f.out1.N == D) {
+        d.wo = f.out1.w; d.bo = f.out1_b; d.o2 = T_; d.ws2 = ows_; d.cnt2 = ocnt_;
+      }
+      if (!attn_decode(d, st)) conv_gemm(lin(ao, n, D, f.out1, f.out1_b, t, D), bf_, st);
     }
-    conv_gemm(lin(ao, n, D, f.out1, f.out1_b, t, D), bf_, st);
     ln = PendingLn{ab[ai], T_, f.n11g, f.n11b, ab[ai ^ 1]};
     ai ^= 1;
     // (2) attention over the C slots of each frame: one launch (stream_slot_block) when the chunk is small
@@ -455,6 +462,7 @@ void FsEendStream::reset(hipStream_t st) {
   SD_HIP(hipMemsetAsync(dcnt_, 0, (size_t)C_ * m_.cfg_.n_heads * sizeof(unsigned), st));
   SD_HIP(hipMemsetAsync(scnt_, 0, sizeof(unsigned), st));
   SD_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned), st));
+  SD_HIP(hipMemsetAsync(ocnt_, 0, (size_t)C_ * sizeof(unsigned), st));
   // wait for the chunks flush() / push*() enqueued: they read bound_ and replay the graphs destroyed below,
   // and set_audio() rewrites bound_ with a synchronous copy that is not ordered after a non-blocking st
   SD_HIP(hipStreamSynchronize(st));

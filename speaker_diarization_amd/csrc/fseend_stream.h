@@ -75,6 +75,8 @@ class FsEendStream {
   unsigned* scnt_ = nullptr;           // its arrival counter (0..n_heads-1, wraps per launch)
   float* fws_ = nullptr;               // stream_ffn_pair's down-projection partials
   unsigned* fcnt_ = nullptr;           // its arrival counter (wraps per launch)
+  float* ows_ = nullptr;               // attn_decode's out-projection head partials
+  unsigned* ocnt_ = nullptr;           // their per-sequence arrival counters (0..n_heads-1, wrap)
   void *QKV_ = nullptr, *AO_ = nullptr, *T_ = nullptr, *H_ = nullptr;
   // histories
   std::vector<void*> kv_enc_, kv_dec_;

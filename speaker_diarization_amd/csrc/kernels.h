@@ -495,6 +495,14 @@ struct DecodeAttnArgs {
   // optional: nseq*nh counters, zeroed once when allocated and shared only by launches that run one after
   // another -- the last block of each (sequence, head) then merges the partials (no combine launch)
   unsigned* cnt = nullptr;
+  // optional, with cnt: the out-projection in the same launch (o2 = o W_outᵀ + b_out, rows laid out as out's, D =
+  // nh * 64 <= 256): each (sequence, head)'s merging block publishes its head's partial write-through to ws2
+  // (nseq*nh*nq*D floats) and the last head of a sequence (cnt2: nseq counters, zeroed once) sums them in head order
+  const void* wo = nullptr;   // packed [D][D], io dtype
+  const float* bo = nullptr;
+  void* o2 = nullptr;
+  float* ws2 = nullptr;
+  unsigned* cnt2 = nullptr;
 };
 int attn_decode_blocks(int max_keys);
 // FS-EEND streaming decoder, slot-attention sub-block of the fusion layer (fs_eend.py:468-471) for one chunk:
@@ -550,7 +558,8 @@ struct FfnPairArgs {
   int n = 1, D = 256, F = 2048;
 };
 bool stream_ffn_pair(const FfnPairArgs& a, hipStream_t st);
-void attn_decode(const DecodeAttnArgs& a, hipStream_t st);
+// returns true when it also ran the out-projection (wo set, the fused merge taken; SDIAR_NO_ATTN_OUTPROJ=1: never)
+bool attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,
                const int* cursor, int mult, hipStream_t st);

@@ -75,13 +75,29 @@ __device__ __forceinline__ void load_row64(const act_t<IOBF>* p, float* v) {
   }
 }
 
+// Weight rows as 16-B vectors: 8 bf16 or 4 fp32 values per vector.  The fused slot block below issues a thread's
+// whole weight slice as one batch before it needs any of it (one memory latency per slice, not one per vector).
+template <bool WBF>
+struct WVec {
+  static constexpr int VE = WBF ? 8 : 4;
+  __device__ __forceinline__ static uint4 load(const void* w, int64_t elem) {
+    if constexpr (WBF) return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(w) + elem);
+    else return *reinterpret_cast<const uint4*>(static_cast<const float*>(w) + elem);
+  }
+  __device__ __forceinline__ static float at(const uint4& u, int e) {
+    const uint32_t w = e < (WBF ? 2 : 1) ? u.x : e < (WBF ? 4 : 2) ? u.y : e < (WBF ? 6 : 3) ? u.z : u.w;
+    if constexpr (WBF) return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+    else return __uint_as_float(w);
+  }
+  // weights 2p, 2p + 1 of the vector as an f32 pair (one v_pk_fma_f32 operand)
+  __device__ __forceinline__ static f32x2 pair(const uint4& u, int p) { return f32x2{at(u, 2 * p), at(u, 2 * p + 1)}; }
+};
+
 // The nblk partials of one (sequence, head), merged: wave -> query, lane -> head dim (lane-parallel max /
 // weights, shuffled weights for o).  SC1: the partials were handed over inside this launch (write-through
 // stores, read back with L1-bypassing sc1 loads).
-template <bool IOBF, bool SC1>
-__device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh, int qi, int lane, int nblk) {
-  using io_t = act_t<IOBF>;
-  const int s = sh / a.nh, h = sh % a.nh;
+template <bool SC1>
+__device__ __forceinline__ float combine_value(const DecodeAttnArgs& a, int sh, int qi, int lane, int nblk) {
   const int64_t bstride = (int64_t)a.nq * (2 + kHD);
   const int64_t base = (int64_t)sh * nblk * bstride + qi * (2 + kHD);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.ws, (short)0, 0x7fffffff, 0x00020000);
@@ -104,8 +120,16 @@ __device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh
   float o = 0.f;
 #pragma unroll
   for (int b = 0; b < kMaxBlk; ++b) o = fmaf(__shfl(w, b, 64), ov[b], o);
+  return o / L;
+}
+
+template <bool IOBF, bool SC1>
+__device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh, int qi, int lane, int nblk) {
+  using io_t = act_t<IOBF>;
+  const int s = sh / a.nh, h = sh % a.nh;
+  const float o = combine_value<SC1>(a, sh, qi, lane, nblk);
   io_t* ob = reinterpret_cast<io_t*>(a.out) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq + h * kHD;
-  st_act(ob, lane, o / L);
+  st_act(ob, lane, o);
 }
 
 // grid (nblk, nseq*nh), 256 threads.  Wave w of block b walks the 64-key tiles
@@ -117,7 +141,7 @@ __device__ __forceinline__ void combine_partials(const DecodeAttnArgs& a, int sh
 // block whose add completes the launch's nblk merges them (MI355X guide hand-off row 1) -- the
 // separate combine launch (a dependent kernel boundary + its own ramp per attention) is gone.
 // The counters are monotonic: each launch adds exactly nblk per (sequence, head).
-template <bool IOBF, int QMAX, bool FUSED>
+template <bool IOBF, int QMAX, bool FUSED, bool OP = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
   using io_t = act_t<IOBF>;
   __shared__ float qs[QMAX][kHD];
@@ -255,7 +279,63 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeAttnArgs a) {
     }
     __syncthreads();
     if (!last) return;
-    for (int qi = wid; qi < nq; qi += 4) combine_partials<IOBF, true>(a, sh, qi, lane, gridDim.x);
+    if constexpr (!OP) {
+      for (int qi = wid; qi < nq; qi += 4) combine_partials<IOBF, true>(a, sh, qi, lane, gridDim.x);
+    } else {
+      // OP: the out-projection as a second hand-off.  The (sequence, head)'s merged output stays in LDS (qs), the
+      // thread's slice of W_out (row tid, the head's 64 inputs) is loaded in the same round trip as the
+      // partials, the head's out-projection partial of feature tid is published write-through, and the last
+      // head of the sequence to count itself sums the nh partials in head order + b_out (slot block pattern).
+      using V = WVec<IOBF>;
+      constexpr int NWV = kHD / V::VE;
+      const int D = a.nh * kHD;
+      uint4 wv[NWV];
+      const int64_t wrow = (int64_t)min(tid, D - 1) * D + h * kHD;
+#pragma unroll
+      for (int v = 0; v < NWV; ++v) wv[v] = V::load(a.wo, wrow + v * V::VE);
+      for (int qi = wid; qi < nq; qi += 4) qs[qi][lane] = combine_value<true>(a, sh, qi, lane, gridDim.x);
+      __syncthreads();
+      float pr[QMAX];
+#pragma unroll
+      for (int qi = 0; qi < QMAX; ++qi) pr[qi] = 0.f;
+#pragma unroll
+      for (int v = 0; v < NWV; ++v)
+#pragma unroll
+        for (int e = 0; e < V::VE; ++e) {
+          const float w = V::at(wv[v], e);
+#pragma unroll
+          for (int qi = 0; qi < QMAX; ++qi) pr[qi] = fmaf(qs[qi][v * V::VE + e], w, pr[qi]);
+        }
+      const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(a.ws2, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int qi = 0; qi < QMAX; ++qi)   // rows >= nq and threads >= D: dropped (offset past the range)
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __float_as_uint(pr[qi]), r2,
+            qi < nq && tid < D ? (uint32_t)((((int64_t)sh * nq + qi) * D + tid) * 4) : 0xfffffff0u, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned nh = a.nh;
+        last = __builtin_amdgcn_atomic_inc32(a.cnt2 + s, nh - 1, __ATOMIC_RELAXED, "agent") == nh - 1;
+      }
+      __syncthreads();
+      if (!last || tid >= D) return;
+      const float bo = a.bo[tid];
+      using io_t = act_t<IOBF>;
+      for (int qi = 0; qi < nq; ++qi) {
+        float hv[4];
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)   // nh <= 4 (D = nh * 64 <= 256); heads past nh re-read head nh - 1
+          hv[hh] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              r2, (uint32_t)((((int64_t)(s * a.nh + min(hh, a.nh - 1))) * nq + qi) * D + tid) * 4, 0, 16));
+        float v = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)
+          if (hh < a.nh) v += hv[hh];
+        io_t* ob = reinterpret_cast<io_t*>(a.o2) + (int64_t)qi * a.o_tok + (int64_t)s * a.o_seq;
+        st_act(ob, tid, v + bo);
+      }
+    }
   }
 }
 
@@ -378,24 +458,6 @@ __global__ __launch_bounds__(256) void dec_finish_kernel(const float* __restrict
   sq = warp_sum(sq);
   if (lane == 0) scores[r] = dot / sqrtf(sq);
 }
-
-// Weight rows as 16-B vectors: 8 bf16 or 4 fp32 values per vector.  The fused slot block below issues a thread's
-// whole weight slice as one batch before it needs any of it (one memory latency per slice, not one per vector).
-template <bool WBF>
-struct WVec {
-  static constexpr int VE = WBF ? 8 : 4;
-  __device__ __forceinline__ static uint4 load(const void* w, int64_t elem) {
-    if constexpr (WBF) return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(w) + elem);
-    else return *reinterpret_cast<const uint4*>(static_cast<const float*>(w) + elem);
-  }
-  __device__ __forceinline__ static float at(const uint4& u, int e) {
-    const uint32_t w = e < (WBF ? 2 : 1) ? u.x : e < (WBF ? 4 : 2) ? u.y : e < (WBF ? 6 : 3) ? u.z : u.w;
-    if constexpr (WBF) return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
-    else return __uint_as_float(w);
-  }
-  // weights 2p, 2p + 1 of the vector as an f32 pair (one v_pk_fma_f32 operand)
-  __device__ __forceinline__ static f32x2 pair(const uint4& u, int p) { return f32x2{at(u, 2 * p), at(u, 2 * p + 1)}; }
-};
 
 // acc += w . y over VE consecutive inputs as VE / 2 packed-pair FMAs (even / odd inputs in the pair's halves)
 template <int VE>
@@ -821,20 +883,31 @@ static void launch_decode_q(const DecodeAttnArgs& a, dim3 g1, hipStream_t st) {
 }
 
 template <bool IOBF>
-static void launch_decode(const DecodeAttnArgs& a, int nblk, hipStream_t st) {
+static bool launch_decode(const DecodeAttnArgs& a, int nblk, hipStream_t st) {
   static const bool split = getenv("SDIAR_DECODE_SPLIT") != nullptr;   // A/B: the separate combine launch
+  static const bool no_op = getenv("SDIAR_NO_ATTN_OUTPROJ") != nullptr;   // A/B: the out-projection's own GEMM
   const int nsh = a.nseq * a.nh;
   const dim3 g1(nblk, nsh), g2(nsh, cdiv(a.nq, 4));
   if (a.cnt && !split) {
-    launch_decode_q<IOBF, true>(a, g1, st);
-    return;
+    // the out-projection merge for one query per sequence (the 1-frame chunks of the latency mode; with more
+    // queries its per-query partials push the kernel past the register budget)
+    const bool op = !no_op && a.nq == 1 && a.wo && a.bo && a.o2 && a.ws2 && a.cnt2 && a.nh * kHD <= 256 &&
+                    reinterpret_cast<uintptr_t>(a.wo) % 16 == 0;
+    if (op) {
+      hipLaunchKernelGGL((attn_decode_kernel<IOBF, 1, true, true>), g1, dim3(256), 0, st, a);
+      SD_LAUNCH_CHECK();
+    } else {
+      launch_decode_q<IOBF, true>(a, g1, st);
+    }
+    return op;
   }
   launch_decode_q<IOBF, false>(a, g1, st);
   hipLaunchKernelGGL(attn_combine_kernel<IOBF>, g2, dim3(256), 0, st, a, nblk);
   SD_LAUNCH_CHECK();
+  return false;
 }
 
-void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
+bool attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
   SD_CHECK(a.hd == kHD, kErrInvalid, "attn_decode: head dim must be 64");
   SD_CHECK(a.nq >= 1 && a.nq <= kMaxQ, kErrInvalid, "attn_decode: 1..32 queries per sequence");
   const int nblk = attn_decode_blocks(a.max_keys);
@@ -843,8 +916,7 @@ void attn_decode(const DecodeAttnArgs& a, hipStream_t st) {
   // bytes: upper bound (full history), the graph does not know the cursor
   ProfScope prof("attn_decode", 4.0 * a.max_keys * kHD * nsh * a.nq,
                  2.0 * a.max_keys * kHD * nsh * (a.io_bf16 ? 2 : 4), st);
-  if (a.io_bf16) launch_decode<true>(a, nblk, st);
-  else launch_decode<false>(a, nblk, st);
+  return a.io_bf16 ? launch_decode<true>(a, nblk, st) : launch_decode<false>(a, nblk, st);
 }
 
 template <int NR>

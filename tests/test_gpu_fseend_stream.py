@@ -300,6 +300,7 @@ def test_decode_attention_fused_combine_bit_identical(gpu, precision, tmp_path):
     for split in (None, "1"):
         env = dict(os.environ)
         env.pop("SDIAR_DECODE_SPLIT", None)
+        env["SDIAR_NO_ATTN_OUTPROJ"] = "1"   # the out-projection's own GEMM in both (its fused merge: test below)
         if split:
             env["SDIAR_DECODE_SPLIT"] = split
         path = str(tmp_path / f"o_{split}.pt")
@@ -464,3 +465,35 @@ def test_ffn_pair_matches_two_launches(gpu, precision, tmp_path):
     for a, b in zip(res[0][0], res[1][0]):
         d = float((a - b).abs().max())
         assert d <= (1e-5 if precision == "fp32" else 2e-2), d
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_attn_outproj_matches_gemm(gpu, precision, tmp_path):
+    """attn_decode with the out-projection in its merge (1-query chunks: each (sequence, head)'s merging block
+    publishes its head's out-projection partial, the last head of the sequence sums them in head order + bias)
+    against the attention followed by the skinny out-projection GEMM (SDIAR_NO_ATTN_OUTPROJ=1, child processes):
+    chunk 1 takes it in all 4 encoder layers and both decoder applications, chunk 2 never; every stream matches
+    test() within the stream tolerances and the two paths agree within 1e-5 (fp32) / 2e-2 (bf16: the fused
+    path projects the fp32 attention output, the GEMM path its bf16 copy)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for off in (None, "1"):
+        env = dict(os.environ)
+        env.pop("SDIAR_NO_ATTN_OUTPROJ", None)
+        if off:
+            env["SDIAR_NO_ATTN_OUTPROJ"] = off
+        path = str(tmp_path / f"o_{off}.pt")
+        r = subprocess.run([sys.executable, "-c", FFN.format(repo=repo, prec=precision, path=path)], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(torch.load(path, weights_only=True))
+    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    for outs, ref in res:
+        for o in outs:
+            np.testing.assert_allclose(o.numpy(), ref.numpy(), atol=tol)
+    for a, b in zip(res[0][0], res[1][0]):
+        d = float((a - b).abs().max())
+        assert d <= (1e-5 if precision == "fp32" else 2e-2), d
+    assert torch.equal(res[0][0][1], res[1][0][1])   # chunk 2: the same launches in both runs
