@@ -120,7 +120,6 @@ TsvadModel::~TsvadModel() {
   for (hipEvent_t e : ev_slice_) (void)hipEventDestroy(e);
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
-  if (ev_gates_) (void)hipEventDestroy(ev_gates_);
   if (side_) (void)hipStreamDestroy(side_);
 }
 
@@ -203,7 +202,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     SD_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     SD_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-    SD_HIP(hipEventCreateWithFlags(&ev_gates_, hipEventDisableTiming));
   }
   // ---------------- BatchNorm1D's NaN bypass: which windows hold a non-finite input, which reference forwards
   // (groups of forward_batch windows) therefore skip the BatchNorm (from the inputs alone, so first: the window
@@ -247,14 +245,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   // stack once slice i's trunk is done (an event per slice), so slice i's MFMA-bound conformer overlaps slice
   // i + 1's HBM-bound trunk and only the first trunk and the last conformer run alone.
   static const int n_slices = getenv("SDIAR_SLICES") ? std::max(0, atoi(getenv("SDIAR_SLICES"))) : 0;
-  // The BiLSTM gates (B*Tl rows of 8*H fp32) of the two-slice path live in QKV_: a slice's rows of it are the
-  // slice's own bf16 QKV rows (NS*3E*2 bytes per window-row >= 8*H*4), dead once its conformer is done, so the
-  // first slice's projection cannot touch what the second slice's conformer is using.  SDIAR_LSTM_GATES_TAIL:
-  // the projection as one GEMM on the step's tail (A/B switch).
-  static const bool one_slice_gates = getenv("SDIAR_LSTM_GATES_TAIL") != nullptr;
-  const bool gates_fit = (int64_t)8 * cfg_.lstm_hidden * 4 <= (int64_t)NS * 3 * E * 2;
-  bool gates_in_slices = false;
-  float* gates = QKV_;
   if (fused_v1 && two && n_slices >= 2) {
     const int K = std::min(n_slices, 8);
     while ((int)ev_slice_.size() < K) {
@@ -279,7 +269,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     SD_HIP(hipEventRecord(ev_join_, side_));
     SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
   } else if (fused_v1 && two) {
-    gates_in_slices = gates_fit && !one_slice_gates;
     // Two window slices, each through the whole per-window part of the model on its own stream: CAM++ trunk,
     // speech_down conv, gsp_fc, conformer stack.  Nothing joins between the trunk and the conformer, so one
     // slice's HBM-bound CAM++ kernels overlap the other's MFMA-bound conformer programs (bit-identical per
@@ -295,17 +284,6 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
       sb.win0 = b0;
       gsp_fc(mx, Bh * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_ + (int64_t)b0 * T3 * SE, SE, s, sb, T3);
       conformer_slice(b0, Bh, s);
-      if (gates_in_slices) {
-        // the BiLSTM's input projection of this slice's rows, on the slice's stream: the first slice's runs
-        // under the second slice's conformer instead of on the step's serial tail.  The second slice's gate
-        // rows begin inside the first slice's QKV rows (8H*4 < NS*3E*2 bytes per window-row), so they wait
-        // for the first slice's conformer (done ~10 ms earlier on the C2 timeline: a free wait).
-        if (b0 == 0) SD_HIP(hipEventRecord(ev_gates_, s));
-        else SD_HIP(hipStreamWaitEvent(s, ev_gates_, 0));
-        const int64_t r = (int64_t)b0 * Tl;
-        conv_gemm(lin(act_at(Tens{X2_, bf}, r * NS * E), Bh * Tl, NS * E, lstm_ih_, lstm_b_,
-                      Tens{gates + r * 8 * cfg_.lstm_hidden, false}, 8 * cfg_.lstm_hidden), bf, s);
-      }
     };
     slice(0, B1, st);
     slice(B1, B - B1, side_);
@@ -366,13 +344,10 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
   }
   {
     const int Hh = cfg_.lstm_hidden;
-    if (!gates_in_slices) {
-      gates = H_;
-      conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{gates, false}, 8 * Hh), bf, st);
-    }
+    conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     // SDIAR_LSTM_FP32 (diagnostic, tools/parity_stages.py): the exact-fp32 recurrence in bf16 mode too
     static const bool lstm_fp32 = getenv("SDIAR_LSTM_FP32") != nullptr;
-    lstm_recurrence(gates, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
+    lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
                     nullptr, lstm_work_, st, lstm_fp32 ? nullptr : lstm_hh_bf_, lstm_err_.get(0));
     ConvGemmArgs f = cam_conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
