@@ -144,7 +144,15 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
   for (int i = 0; i < kPieces; ++i) {
     // Piece i landed: the only younger DMAs are the NSLOT - 2 pieces issued after it (this wave's my_dma
     // instructions each), unless stores were issued after them (attention outputs) -> full drain.
-    if constexpr (NSLOT == 3) {
+    if constexpr (NSLOT == 4) {
+      // two younger pieces in flight, except at the end of the ring (one, then none)
+      if (drain || i + 1 >= kPieces) wait_vm<0>();
+      else if (i + 2 >= kPieces) {
+        if (my_dma == 3) wait_vm<3>(); else if (my_dma == 2) wait_vm<2>(); else wait_vm<1>();
+      } else {
+        if (my_dma == 3) wait_vm<6>(); else if (my_dma == 2) wait_vm<4>(); else wait_vm<2>();
+      }
+    } else if constexpr (NSLOT == 3) {
       if (drain || i + 1 >= kPieces) wait_vm<0>();
       else if (my_dma == 3) wait_vm<3>();
       else if (my_dma == 2) wait_vm<2>();
@@ -316,7 +324,7 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
   ProfScope prof("mha_block", flops, bytes, st);
   // SDIAR_MHA_SEQ2=1: the rounds 2-4 layout (two sequences per 8-wave workgroup, one workgroup per CU);
-  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <2,8,3,48>, 4 <1,4,3,48>
+  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <2,8,3,48>, 4 <1,4,3,48>, 5 <1,8,3,64>, 6 <1,8,2,48>, 7 <2,8,4,48>
   static const int var_env = getenv("SDIAR_MHA_SEQ2") ? 1 : getenv("SDIAR_MHA_VARIANT") ? atoi(getenv("SDIAR_MHA_VARIANT")) : 0;
   const int var = variant >= 0 ? variant : var_env;
   switch (var) {
@@ -326,6 +334,7 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
     case 4: launch_mha<1, 4, 3, 48>(a, st); break;
     case 5: launch_mha<1, 8, 3, 64>(a, st); break;
     case 6: launch_mha<1, 8, 2, 48>(a, st); break;
+    case 7: launch_mha<2, 8, 4, 48>(a, st); break;
     default: launch_mha<1, 4, 2, 48>(a, st); break;
   }
   SD_LAUNCH_CHECK();

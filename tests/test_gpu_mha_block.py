@@ -44,9 +44,10 @@ def test_mha_block_layouts(gpu, S, T, lens):
     b = (torch.randn(1152, generator=g) * 0.1).to(gpu)
     key_len = torch.randint(1, T + 1, (S,), generator=g, dtype=torch.int32).to(gpu) if lens else None
     ref = _ref(y, w.to(torch.bfloat16).float(), b, key_len)
-    outs = [_run(y, w, b, key_len, v) for v in (0, 1)]
+    outs = [_run(y, w, b, key_len, v) for v in range(8)]   # every layout mha_block() can launch
     for v, o in enumerate(outs):
         err = (o.float() - ref).abs()
         print(f"layout {v}: max err {err.max().item():.3e}; worst (seq, token, feature) {np.unravel_index(int(err.argmax()), err.shape)}")
         assert err.max().item() < 3e-2, v
-    assert torch.equal(outs[0], outs[1])
+    for v in range(1, 8):
+        assert torch.equal(outs[0], outs[v]), v
