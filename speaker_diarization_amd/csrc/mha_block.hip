@@ -41,14 +41,15 @@ constexpr int kVS = 48;                        // V row stride
 constexpr int kPieces = kNH * 3 * (kHD / kPR); // 72
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// Two layouts of the same arithmetic (bit-identical outputs):
+// Layouts of the same arithmetic (bit-identical outputs, tests/test_gpu_mha_block.py), <SEQ, W, NSLOT, QS>:
 //   <2, 8, 3, 64>  two sequences per 8-wave workgroup, 3-slot ring, Q / K rows padded to 64 (151 KiB: one
 //                  workgroup per CU) - rounds 2-4;
-//   <1, 4, 2, 48>  round 5: one sequence per 4-wave workgroup, 2-slot ring, Q / K rows of 48 (73.5 KiB: TWO
-//                  workgroups per CU, so one's HBM prologue, piece waits and softmax VALU overlap the other's
-//                  MFMAs).  With 48-wide rows the second 32-deep QK^T k-step reads features 48..63 from the
-//                  next row (finite values), multiplied by the query fragment's features 48..63, which are
-//                  zeroed in registers.
+//   <2, 8, 3, 48>  round 5, shipped: the same with Q / K rows of 48 (133 KiB).  With 48-wide rows the second
+//                  32-deep QK^T k-step reads features 48..63 from the next row (finite values), multiplied by the
+//                  query fragment's features 48..63, which are zeroed in registers; the 96-B row stride also
+//                  spreads the K-fragment reads over more LDS banks than the 128-B one (0.4-0.7 ms per C2 step);
+//   <1, 4, 2, 48>  one sequence per 4-wave workgroup, 2-slot ring (73.5 KiB: two workgroups per CU, so one's
+//                  HBM prologue, piece waits and softmax overlap the other's MFMAs) - 0.1-0.2 ms behind.
 template <int SEQ, int W, int NSLOT, int QS>
 struct MhaL {
   static constexpr int kTiles = SEQ * kTilesPerSeq;
@@ -324,18 +325,21 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
   ProfScope prof("mha_block", flops, bytes, st);
   // SDIAR_MHA_SEQ2=1: the rounds 2-4 layout (two sequences per 8-wave workgroup, one workgroup per CU);
-  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <2,8,3,48>, 4 <1,4,3,48>, 5 <1,8,3,64>, 6 <1,8,2,48>, 7 <2,8,4,48>
+  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <1,4,2,48>, 4 <1,4,3,48>, 5 <1,8,3,64>, 6 <1,8,2,48>, 7 <2,8,4,48>
+  // Round 5 sweep on C2 (ms per step, one box, 2-3 rounds): <2,8,3,48> 26.39-26.79 (shipped), <1,4,2,48> 26.53-26.97,
+  // <2,8,4,48> 26.55-26.61, <2,8,3,64> 27.15-27.18, <1,8,2,48> 28.35-28.42, <1,8,3,64> 28.83-28.90,
+  // <1,4,2,64> / <1,4,3,48> 29.26-29.36 (over 80 KiB: one 4-wave workgroup per CU)
   static const int var_env = getenv("SDIAR_MHA_SEQ2") ? 1 : getenv("SDIAR_MHA_VARIANT") ? atoi(getenv("SDIAR_MHA_VARIANT")) : 0;
   const int var = variant >= 0 ? variant : var_env;
   switch (var) {
     case 1: launch_mha<2, 8, 3, 64>(a, st); break;
     case 2: launch_mha<1, 4, 2, 64>(a, st); break;
-    case 3: launch_mha<2, 8, 3, 48>(a, st); break;
+    case 3: launch_mha<1, 4, 2, 48>(a, st); break;
     case 4: launch_mha<1, 4, 3, 48>(a, st); break;
     case 5: launch_mha<1, 8, 3, 64>(a, st); break;
     case 6: launch_mha<1, 8, 2, 48>(a, st); break;
     case 7: launch_mha<2, 8, 4, 48>(a, st); break;
-    default: launch_mha<1, 4, 2, 48>(a, st); break;
+    default: launch_mha<2, 8, 3, 48>(a, st); break;
   }
   SD_LAUNCH_CHECK();
 }

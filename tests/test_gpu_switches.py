@@ -198,7 +198,6 @@ def _tsvad_hash(extra_env):
 def test_schedule_switches_bit_identical(gpu, switch):
     """Switches that change only the schedule or the transport, never the arithmetic, must leave the TS-VAD
     logits (ots_vad v1 with its BiLSTM, and the CAM++/transformer model; 400 windows: two-stream slices) bit
-    for bit unchanged: mha_block's rounds 2-4 layout (two sequences per 8-wave workgroup) vs round 5's (one per
-    4-wave workgroup, two workgroups per CU); K window slices pipelined over the two streams (trunk i+1 beside
+    for bit unchanged: mha_block's rounds 2-4 layout (Q / K rows padded to 64) vs the shipped one (rows of 48); K window slices pipelined over the two streams (trunk i+1 beside
     conformer stack i) vs the default two; the BiLSTM's h exchange on tagged 8-byte granules vs the counter."""
     assert _tsvad_hash(switch) == _tsvad_hash({})
