@@ -840,6 +840,85 @@ __global__ __launch_bounds__(256) void glu_dwconv_kernel(const act_t<BF>* __rest
 // halves.  The tile's staged rows are all requested before the first LDS store (one HBM latency per
 // tile).  Per output element and tap the FMA order is the runtime kernel's (bias, then taps in order),
 // so the conv values are bit-identical to it; only the GroupNorm partial sums' summation order differs.
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// R output rows of a half-wave run from the staged rows g[(r0 + i) * 32 + cp] (i < R + K - 1): per tap one packed
+// FMA over the lane's channel pair, bias first, taps in order; optional SiLU; bf16 stores of the valid rows and
+// their GroupNorm partial sums (lsum, lsq).
+template <int K, int R>
+__device__ __forceinline__ void dw_run(const uint32_t* g, int r0, int cp, int nout, const float2v (&wr)[K], float2v bv,
+                                       bool fused_silu, uint16_t* yrow, int C, float& lsum, float& lsq) {
+  float2v acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = bv;
+  constexpr int kN = R + K - 1, kPf = 4;   // window elements; LDS reads issued kPf elements ahead
+  uint32_t uw[kN];
+#pragma unroll
+  for (int i = 0; i < kPf; ++i) uw[i] = g[(r0 + i) * 32 + cp];
+#pragma unroll
+  for (int i = 0; i < kN; ++i) {
+    if (i + kPf < kN) uw[i + kPf] = g[(r0 + i + kPf) * 32 + cp];
+    const uint32_t u = uw[i];
+    const float2v xv = float2v{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = i - r;
+      if (j >= 0 && j < K) acc[r] = __builtin_elementwise_fma(wr[j], xv, acc[r]);
+    }
+    // keep the FMAs of one window element together: left alone the scheduler emits each
+    // accumulator's 31-FMA dependent chain back to back (a dependency stall per FMA)
+#pragma unroll
+    for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float2v v = acc[r];
+    if (fused_silu) v = float2v{v.x * sigmoid_rcp(v.x), v.y * sigmoid_rcp(v.y)};
+    if (r < nout) {
+      *reinterpret_cast<uint32_t*>(yrow + (int64_t)r * C) = pack_bf16x2(v.x, v.y);
+      lsum += v.x + v.y;
+      lsq = fmaf(v.x, v.x, lsq);
+      lsq = fmaf(v.y, v.y, lsq);
+    }
+  }
+}
+
+// The block's (sum, sum of squares) over its 256 threads, in the order of a halving tree (t += t + o for
+// o = 128 .. 1): the two cross-wave levels through LDS, the six in-wave ones as shfl_down (same operands, same
+// association, 2 barriers instead of 8).  Thread 0 stores them at out[0], out[1].
+__device__ __forceinline__ void dw_gn_partial(float (&red)[2][256], int tid, float lsum, float lsq, float* out) {
+  __syncthreads();   // red may still be read by the previous call's wave 0
+  red[0][tid] = lsum;
+  red[1][tid] = lsq;
+  __syncthreads();
+  if (tid < 128) {
+    red[0][tid] += red[0][tid + 128];
+    red[1][tid] += red[1][tid + 128];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float a = red[0][tid] + red[0][tid + 64], b = red[1][tid] + red[1][tid + 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, 64);
+      b += __shfl_down(b, o, 64);
+    }
+    if (tid == 0) {
+      out[0] = a;
+      out[1] = b;
+    }
+  }
+}
+
+// bf16 depthwise conv with the tap count K and the run length R fixed at compile time (the conformer
+// kernels 15 and 31): a lane owns a channel PAIR and produces R consecutive output rows, so every tap is
+// one packed FMA (v_pk_fma_f32) over the pair, the window element arrives as one 4-B LDS read (the pair's
+// bf16x2) + two bit ops, and nothing in the unrolled body branches (the runtime-k kernel above predicates
+// every window element).  A wave is two half-waves of 32 pairs = the block's 64 channels; the 8 half-waves
+// of the block take runs 0..7 of an 8R-row tile, rows of 128 B so the halves (R odd) read opposite bank
+// halves.  The tile's staged rows are all requested before the first LDS store (one HBM latency per
+// tile).  Per output element and tap the FMA order is the runtime kernel's (bias, then taps in order),
+// so the conv values are bit-identical to it; only the GroupNorm partial sums' summation order differs.
 template <int K, int R>
 __global__ __launch_bounds__(256) void dwconv_pk_kernel(const uint16_t* __restrict__ x, int T, int C,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
@@ -851,15 +930,14 @@ __global__ __launch_bounds__(256) void dwconv_pk_kernel(const uint16_t* __restri
   constexpr int pad = (K - 1) / 2;
   __shared__ uint32_t g[kRows * 32];                    // [row][32 channel pairs] bf16x2
   __shared__ float red[2][256];
-  typedef float f2 __attribute__((ext_vector_type(2)));
   const int s = blockIdx.y, c0 = blockIdx.x * kDwCB, nblk = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int cp = lane & 31, slot = wv * 2 + (lane >> 5);
   const int c = c0 + 2 * cp;                            // C % 64 == 0 (host check): both channels exist
-  f2 wr[K];
+  float2v wr[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) wr[j] = f2{w[(int64_t)c * K + j], w[(int64_t)(c + 1) * K + j]};
-  const f2 bv = bias ? f2{bias[c], bias[c + 1]} : f2{0.f, 0.f};
+  for (int j = 0; j < K; ++j) wr[j] = float2v{w[(int64_t)c * K + j], w[(int64_t)(c + 1) * K + j]};
+  const float2v bv = bias ? float2v{bias[c], bias[c + 1]} : float2v{0.f, 0.f};
   const uint16_t* xs = x + (int64_t)s * T * (glu_in ? 2 : 1) * C;
   uint16_t* ys = y + (int64_t)s * T * C;
   float lsum = 0.f, lsq = 0.f;
@@ -901,56 +979,64 @@ __global__ __launch_bounds__(256) void dwconv_pk_kernel(const uint16_t* __restri
     }
     __syncthreads();
     const int r0 = slot * R, nout = min(8 * R, T - t0) - r0;   // valid rows of this run
-    if (nout > 0) {
-      f2 acc[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = bv;
-      constexpr int kN = R + K - 1, kPf = 4;   // window elements; LDS reads issued kPf elements ahead
-      uint32_t uw[kN];
-#pragma unroll
-      for (int i = 0; i < kPf; ++i) uw[i] = g[(r0 + i) * 32 + cp];
-#pragma unroll
-      for (int i = 0; i < kN; ++i) {
-        if (i + kPf < kN) uw[i + kPf] = g[(r0 + i + kPf) * 32 + cp];
-        const uint32_t u = uw[i];
-        const f2 xv = f2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int j = i - r;
-          if (j >= 0 && j < K) acc[r] = __builtin_elementwise_fma(wr[j], xv, acc[r]);
-        }
-        // keep the FMAs of one window element together: left alone the scheduler emits each
-        // accumulator's 31-FMA dependent chain back to back (a dependency stall per FMA)
-#pragma unroll
-        for (int r = 0; r < R; ++r) asm volatile("" : "+v"(acc[r]));
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        f2 v = acc[r];
-        if (fused_silu) v = f2{v.x * sigmoid_rcp(v.x), v.y * sigmoid_rcp(v.y)};
-        if (r < nout) {
-          *reinterpret_cast<uint32_t*>(ys + (int64_t)(t0 + r0 + r) * C + c) = pack_bf16x2(v.x, v.y);
-          lsum += v.x + v.y;
-          lsq = fmaf(v.x, v.x, lsq);
-          lsq = fmaf(v.y, v.y, lsq);
-        }
-      }
-    }
+    if (nout > 0) dw_run<K, R>(g, r0, cp, nout, wr, bv, fused_silu, ys + (int64_t)(t0 + r0) * C + c, C, lsum, lsq);
   }
   if (fused_silu) return;   // uniform across the block
-  red[0][tid] = lsum;
-  red[1][tid] = lsq;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      red[0][tid] += red[0][tid + o];
-      red[1][tid] += red[1][tid + o];
+  dw_gn_partial(red, tid, lsum, lsq, partial + ((int64_t)s * nblk + blockIdx.x) * 2);
+}
+
+// The same conv for sequences of one tile (T <= 8R, no GLU input), PERSISTENT: workgroup b keeps channel block
+// b % (C / 64) (its taps stay in registers) and walks sequences b / (C / 64), + gridDim.x / (C / 64), ...; the
+// next sequence's rows are requested as soon as the current ones are in LDS, so their HBM latency runs under
+// the current sequence's taps, stores and GroupNorm sums (the one-tile-per-workgroup kernel above exposes one
+// HBM latency per 64 channels x T rows).  Values and partial sums bit-identical to dwconv_pk_kernel.
+template <int K, int R>
+__global__ __launch_bounds__(256) void dwconv_pp_kernel(const uint16_t* __restrict__ x, int S, int T, int C,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        uint16_t* __restrict__ y, float* __restrict__ partial,
+                                                        int fused_silu) {
+  constexpr int kRows = 8 * R + K - 1;
+  constexpr int kItems = kRows * 8;
+  constexpr int kIters = (kItems + 255) / 256;
+  constexpr int pad = (K - 1) / 2;
+  __shared__ uint32_t g[kRows * 32];
+  __shared__ float red[2][256];
+  const int ncb = C / kDwCB, cb = blockIdx.x % ncb, c0 = cb * kDwCB, sstep = gridDim.x / ncb;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cp = lane & 31, slot = wv * 2 + (lane >> 5);
+  const int c = c0 + 2 * cp;
+  float2v wr[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) wr[j] = float2v{w[(int64_t)c * K + j], w[(int64_t)(c + 1) * K + j]};
+  const float2v bv = bias ? float2v{bias[c], bias[c + 1]} : float2v{0.f, 0.f};
+  uint4 va[kIters];
+  auto fetch = [&](int s) {
+    const uint16_t* xs = x + (int64_t)s * T * C + c0;
+#pragma unroll
+    for (int u = 0; u < kIters; ++u) {
+      const int i = tid + u * 256, tt = i >> 3, ch = (i & 7) * 8, t = tt - pad;
+      // rows outside [0, T) and chunks past the tile read row 0 (any finite data) and are zeroed below
+      const bool in = i < kItems && t >= 0 && t < T;
+      va[u] = *reinterpret_cast<const uint4*>(xs + (int64_t)(in ? t : 0) * C + ch);
+      if (!in) va[u] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  int s = blockIdx.x / ncb;
+  if (s < S) fetch(s);
+  for (; s < S; s += sstep) {
+    __syncthreads();   // the previous sequence's reads of g are done
+#pragma unroll
+    for (int u = 0; u < kIters; ++u) {
+      const int i = tid + u * 256;
+      if (i < kItems) *reinterpret_cast<uint4*>(g + (i >> 3) * 32 + (i & 7) * 4) = va[u];
     }
     __syncthreads();
-  }
-  if (tid == 0) {
-    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 0] = red[0][0];
-    partial[((int64_t)s * nblk + blockIdx.x) * 2 + 1] = red[1][0];
+    if (s + sstep < S) fetch(s + sstep);   // in flight during this sequence's conv
+    float lsum = 0.f, lsq = 0.f;
+    const int r0 = slot * R, nout = T - r0;
+    if (nout > 0)
+      dw_run<K, R>(g, r0, cp, nout, wr, bv, fused_silu, y + ((int64_t)s * T + r0) * C + c, C, lsum, lsq);
+    if (!fused_silu) dw_gn_partial(red, tid, lsum, lsq, partial + ((int64_t)s * ncb + cb) * 2);
   }
 }
 
@@ -976,6 +1062,32 @@ static void launch_dwconv_pk(int R, dim3 grid, hipStream_t st, const uint16_t* x
     hipLaunchKernelGGL((dwconv_pk_kernel<K, 19>), grid, dim3(256), 0, st, x, T, C, w, bias, y, partial, fused_silu, glu_in);
 }
 
+// persistent grid: as many workgroups as fit on the device at once, a multiple of the channel blocks
+template <int K, int R>
+static void launch_dwconv_pp_r(int S, int T, int C, hipStream_t st, const uint16_t* x, const float* w, const float* bias,
+                               uint16_t* y, float* partial, int fused_silu) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, dwconv_pp_kernel<K, R>, 256, 0));
+    resident = std::max(1, cus * std::max(1, per));
+  }
+  const int ncb = C / kDwCB;
+  const int per_cb = std::max(1, std::min(S, resident / ncb));
+  hipLaunchKernelGGL((dwconv_pp_kernel<K, R>), dim3(per_cb * ncb), dim3(256), 0, st, x, S, T, C, w, bias, y, partial,
+                     fused_silu);
+}
+
+template <int K>
+static void launch_dwconv_pp(int R, int S, int T, int C, hipStream_t st, const uint16_t* x, const float* w,
+                             const float* bias, uint16_t* y, float* partial, int fused_silu) {
+  if (R == 9) launch_dwconv_pp_r<K, 9>(S, T, C, st, x, w, bias, y, partial, fused_silu);
+  else if (R == 13) launch_dwconv_pp_r<K, 13>(S, T, C, st, x, w, bias, y, partial, fused_silu);
+  else launch_dwconv_pp_r<K, 19>(S, T, C, st, x, w, bias, y, partial, fused_silu);
+}
+
 void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
                 void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st) {
   SD_CHECK(fused_silu || partial, kErrInvalid, "glu_dwconv: GroupNorm partials buffer required");
@@ -985,7 +1097,14 @@ void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
   const double eb = io_bf16 ? 2.0 : 4.0;
   ProfScope prof(glu_in ? "glu_dwconv" : "dwconv", 2.0 * S * T * C * k, eb * S * T * (glu_in ? 3.0 : 2.0) * C, st);
   static const bool no_pk = getenv("SDIAR_NO_DWCONV_PK") != nullptr;   // A/B switch: the runtime-k kernel
-  if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk) {
+  static const bool no_pp = getenv("SDIAR_NO_DWCONV_PP") != nullptr;   // A/B switch: one workgroup per sequence
+  if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk && !no_pp && !glu_in && T <= 8 * 19) {
+    auto xp = reinterpret_cast<const uint16_t*>(x);
+    auto yp = reinterpret_cast<uint16_t*>(y);
+    const int R = T <= 8 * 9 ? 9 : T <= 8 * 13 ? 13 : 19;
+    if (k == 31) launch_dwconv_pp<31>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
+    else launch_dwconv_pp<15>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
+  } else if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk) {
     const int R = dwconv_pk_runlen(T, k);
     auto xp = reinterpret_cast<const uint16_t*>(x);
     auto yp = reinterpret_cast<uint16_t*>(y);
