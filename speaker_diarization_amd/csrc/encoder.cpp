@@ -258,6 +258,10 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   // [pw2 + residual + ffn2 + final LN (+ next layer's ffn1 + attn-LN)].  X stays the fp32 residual stream.
   const int rows = S * T;
   const Tens y{w.Y, true}, qkv{w.QKV, true}, ao{w.AO, true}, h{w.H, true};
+  // the residual stream between the row programs in their MFMA-tiled layout (kernels.h RowProgArgs::x_tiled);
+  // the caller sees X row-major (or only the speaker-layout output).  SDIAR_RP_ROWMAJOR_X=1: row-major throughout.
+  static const bool rowmajor = getenv("SDIAR_RP_ROWMAJOR_X") != nullptr;
+  const int tiled = !rowmajor && rows % 16 == 0;
   auto ffn = [](const ConformerL& L, bool second) {
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
@@ -276,6 +280,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     }
     r.n_ffn = 1; r.ffn[0] = ffn(Ls[0], false);
     r.y = y.p; r.y_g = Ls[0].at_lng; r.y_b = Ls[0].at_lnb;
+    r.xo_tiled = tiled;
     rowprog(r, "rowprog_ffn", st);
   }
   for (size_t li = 0; li < Ls.size(); ++li) {
@@ -300,6 +305,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.X = X; r.Xo = X; r.M = rows;
       r.A = ao.p; r.w0 = L.rp_out; r.b0 = L.out_b;
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
+      r.x_tiled = r.xo_tiled = tiled;
       rowprog(r, "rowprog_out", st);
     }
     {
@@ -319,13 +325,15 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
         r.gn_partial = w.partial; r.gn_nblk = (E + 63) / 64; r.gn_T = T; r.gn_g = L.gn_g; r.gn_b = L.gn_b;
       }
       r.n_ffn = 1; r.ffn[0] = ffn(L, true);
+      r.x_tiled = tiled;
       if (li + 1 < Ls.size()) {
         const ConformerL& Ln = Ls[li + 1];
         r.n_ffn = 2; r.ffn[1] = ffn(Ln, false);
         r.y = y.p; r.y_g = Ln.at_lng; r.y_b = Ln.at_lnb;
+        r.xo_tiled = tiled;
       } else if (io) {
         r.Xo = nullptr; r.yt = io->out; r.yt_NS = io->NS; r.T_seq = T;
-      }
+      }   // else: the stack's output X, row-major (in place over the tiled input: a tile is read whole first)
       rowprog(r, "rowprog_pw2_ffn", st);
     }
   }

@@ -269,6 +269,11 @@ struct RowProgArgs {
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
   int prio = 0;      // 1: waves 4-7 run at s_setprio 1 (A/B: SDIAR_RP_PRIO)
+  // X / Xo in the MFMA-tiled layout (M % 16 == 0): 16-row group g, feature f = 16 ft + 4 q + r of row 16 g + l at
+  // float ((g * 24 + ft) * 64 + l + 16 q) * 4 + r -- each wave's 16 x 384 fp32 residual block is 24 contiguous
+  // 1-KiB runs, one per load / store instruction (row-major it is 16 scattered 64-B pieces per instruction).  The
+  // residual stream between row programs is private to them (run_conformer_stack), so it stays tiled in between.
+  int x_tiled = 0, xo_tiled = 0;
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

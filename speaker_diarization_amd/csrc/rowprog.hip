@@ -261,10 +261,12 @@ void rowprog_kernel(RowProgArgs a) {
           acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
         }
       } else {
-        const float* xr = a.X + row[tt] * kD + g4;
+        // row-major: feature 16 ft + g4 of the row; tiled: run ft of the row's 16-row group, this lane's 16 B
+        const float* xr = a.x_tiled ? a.X + (row[tt] - l15) * kD + lane * 4 : a.X + row[tt] * kD + g4;
+        const int fs = a.x_tiled ? 256 : 16;
 #pragma unroll
         for (int ft = 0; ft < kFT; ++ft) {
-          const float4 v = live[tt] ? *reinterpret_cast<const float4*>(xr + 16 * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 v = live[tt] ? *reinterpret_cast<const float4*>(xr + fs * ft) : make_float4(0.f, 0.f, 0.f, 0.f);
           acc[ft][tt] = floatx4{v.x, v.y, v.z, v.w};
         }
       }
@@ -451,10 +453,11 @@ void rowprog_kernel(RowProgArgs a) {
                                                               pack_bf16x2(acc[ft][tt][2], acc[ft][tt][3]));
       }
       if (a.Xo && live[tt]) {
-        float* xo = a.Xo + row[tt] * kD + g4;
+        float* xo = a.xo_tiled ? a.Xo + (row[tt] - l15) * kD + lane * 4 : a.Xo + row[tt] * kD + g4;
+        const int fs = a.xo_tiled ? 256 : 16;
 #pragma unroll
         for (int ft = 0; ft < kFT; ++ft)
-          *reinterpret_cast<float4*>(xo + 16 * ft) =
+          *reinterpret_cast<float4*>(xo + fs * ft) =
               make_float4(acc[ft][tt][0], acc[ft][tt][1], acc[ft][tt][2], acc[ft][tt][3]);
       }
       if (a.y) {
@@ -556,6 +559,7 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(!a.x_ts || (a.x_mix && a.x_NS > 0 && a.T_seq > 0 && a.x_Tmix > 0 && a.x_ldmix % 4 == 0), kErrInvalid,
            "rowprog: speaker-input source arguments");
   SD_CHECK(!a.yt || (a.yt_NS > 0 && a.T_seq > 0), kErrInvalid, "rowprog: channel-layout output arguments");
+  SD_CHECK(!(a.x_tiled || a.xo_tiled) || a.M % 16 == 0, kErrInvalid, "rowprog: the tiled X layout needs M % 16 == 0");
   if (a.M <= 0) return;
   static int grid_max = 0;
   if (!grid_max) {
