@@ -291,6 +291,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       m.ln_g = L.at_lng; m.ln_b = L.at_lnb; m.eps = 1e-5f;
       m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
       m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
+      m.out_tiled = tiled;   // read only by the out-projection program below
       mha_block(m, st);
     } else {
       conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), true, st);
@@ -306,6 +307,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.A = ao.p; r.w0 = L.rp_out; r.b0 = L.out_b;
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
       r.x_tiled = r.xo_tiled = tiled;
+      r.a_tiled = tiled && mha_block_supported(E, nh, T, true);
       rowprog(r, "rowprog_out", st);
     }
     {

@@ -224,6 +224,9 @@ struct MhaBlockArgs {
   int S = 0, T = 0, D = 0, nh = 0;
   float scale = 1.f;
   const int* key_len = nullptr;
+  // out in the row programs' tiled A layout (RowProgArgs::a_tiled; needs S * T % 16 == 0, ldo == D) instead of
+  // row-major rows of stride ldo
+  int out_tiled = 0;
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
 
@@ -274,6 +277,10 @@ struct RowProgArgs {
   // 1-KiB runs, one per load / store instruction (row-major it is 16 scattered 64-B pieces per instruction).  The
   // residual stream between row programs is private to them (run_conformer_stack), so it stays tiled in between.
   int x_tiled = 0, xo_tiled = 0;
+  // A in the tiled layout of the pre-GEMM's B-operand fragments (M % 16 == 0): row 16 g + l, feature
+  // f = 32 kk + 8 q + j at bf16 ((g * 12 + kk) * 64 + l + 16 q) * 8 + j, so fragment kk of a 16-row group is one
+  // contiguous 1-KiB run (mha_block writes it with out_tiled)
+  int a_tiled = 0;
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

@@ -284,11 +284,17 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
       }
       if (row < T) {
         const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-        uint16_t* orow = reinterpret_cast<uint16_t*>(a.out) + ((int64_t)s * T + row) * a.ldo + h * kHD;
+        const int64_t r = (int64_t)s * T + row;
+        uint16_t* ob = reinterpret_cast<uint16_t*>(a.out);
 #pragma unroll
-        for (int dt = 0; dt < 3; ++dt)
-          *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * lk) =
+        for (int dt = 0; dt < 3; ++dt) {
+          const int f = h * kHD + dt * 16 + 4 * lk;   // this lane's 4 features f .. f + 3 of row r
+          // tiled (RowProgArgs::a_tiled): fragment f / 32 of the row's 16-row group, lane (r % 16) + 16 ((f % 32) / 8)
+          const int64_t off = a.out_tiled ? (((r >> 4) * kKT32 + (f >> 5)) * 64 + (r & 15) + 16 * ((f & 31) >> 3)) * 8 + (f & 7)
+                                          : r * a.ldo + f;
+          *reinterpret_cast<uint2*>(ob + off) =
               make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv), pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+        }
         drain = true;
       }
     }
@@ -318,6 +324,8 @@ bool mha_block_supported(int D, int nh, int T, bool bf16) {
 void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   SD_CHECK(mha_block_supported(kD, a.nh, a.T, true) && a.D == kD, kErrInvalid, "mha_block: unsupported shape");
   SD_CHECK(a.ldo % 4 == 0, kErrInvalid, "mha_block: output row stride must be a multiple of 4");
+  SD_CHECK(!a.out_tiled || ((int64_t)a.S * a.T % 16 == 0 && a.ldo == kD), kErrInvalid,
+           "mha_block: the tiled output layout needs S * T % 16 == 0 and ldo == D");
   if (a.S <= 0) return;
   SD_CHECK(a.y != nullptr, kErrInvalid, "mha_block: y (LayerNorm'd bf16 rows) is required");
   const double rows = (double)a.S * a.T;

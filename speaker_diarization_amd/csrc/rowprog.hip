@@ -277,11 +277,14 @@ void rowprog_kernel(RowProgArgs a) {
       bf16x8 af[TT][kKK];
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
-        const uint16_t* ar = static_cast<const uint16_t*>(a.A) + row[tt] * kD + 2 * g4;
+        // row-major: features 32 kk + 8 q of the row; tiled: fragment kk of the row's 16-row group, this lane's 16 B
+        const uint16_t* ar = a.a_tiled ? static_cast<const uint16_t*>(a.A) + (row[tt] - l15) * kD + lane * 8
+                                       : static_cast<const uint16_t*>(a.A) + row[tt] * kD + 2 * g4;
+        const int ks = a.a_tiled ? 512 : 32;
 #pragma unroll
         for (int kk = 0; kk < kKK; ++kk)
           af[tt][kk] = __builtin_bit_cast(
-              bf16x8, live[tt] ? *reinterpret_cast<const uint4*>(ar + 32 * kk) : make_uint4(0u, 0u, 0u, 0u));
+              bf16x8, live[tt] ? *reinterpret_cast<const uint4*>(ar + ks * kk) : make_uint4(0u, 0u, 0u, 0u));
       }
       if (a.gn_partial) {
         // A = silu(GroupNorm(A)): the conformer conv module's GroupNorm(1 group) + SiLU, applied on load
@@ -559,7 +562,8 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(!a.x_ts || (a.x_mix && a.x_NS > 0 && a.T_seq > 0 && a.x_Tmix > 0 && a.x_ldmix % 4 == 0), kErrInvalid,
            "rowprog: speaker-input source arguments");
   SD_CHECK(!a.yt || (a.yt_NS > 0 && a.T_seq > 0), kErrInvalid, "rowprog: channel-layout output arguments");
-  SD_CHECK(!(a.x_tiled || a.xo_tiled) || a.M % 16 == 0, kErrInvalid, "rowprog: the tiled X layout needs M % 16 == 0");
+  SD_CHECK(!(a.x_tiled || a.xo_tiled || a.a_tiled) || a.M % 16 == 0, kErrInvalid,
+           "rowprog: the tiled X / A layouts need M % 16 == 0");
   if (a.M <= 0) return;
   static int grid_max = 0;
   if (!grid_max) {
