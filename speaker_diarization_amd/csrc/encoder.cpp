@@ -262,6 +262,8 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   // the caller sees X row-major (or only the speaker-layout output).  SDIAR_RP_ROWMAJOR_X=1: row-major throughout.
   static const bool rowmajor = getenv("SDIAR_RP_ROWMAJOR_X") != nullptr;
   const int tiled = !rowmajor && rows % 16 == 0;
+  static const bool rowmajor_a = getenv("SDIAR_RP_ROWMAJOR_A") != nullptr;   // A/B: the attention output row-major
+  const int tiled_a = tiled && !rowmajor_a && mha_block_supported(E, nh, T, true);
   auto ffn = [](const ConformerL& L, bool second) {
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
@@ -291,7 +293,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       m.ln_g = L.at_lng; m.ln_b = L.at_lnb; m.eps = 1e-5f;
       m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
       m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
-      m.out_tiled = tiled;   // read only by the out-projection program below
+      m.out_tiled = tiled_a;   // read only by the out-projection program below
       mha_block(m, st);
     } else {
       conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), true, st);
@@ -307,7 +309,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.A = ao.p; r.w0 = L.rp_out; r.b0 = L.out_b;
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
       r.x_tiled = r.xo_tiled = tiled;
-      r.a_tiled = tiled && mha_block_supported(E, nh, T, true);
+      r.a_tiled = tiled_a;
       rowprog(r, "rowprog_out", st);
     }
     {

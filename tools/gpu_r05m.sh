@@ -2,20 +2,20 @@
 # round 5: tiled residual stream + tiled attention output (mha_block -> out-projection program): bit identity, C2 A/B
 set -uo pipefail
 O=gpurun_out/r05m; mkdir -p $O
-timeout -k 10 500 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_switches.py tests/test_gpu_tsvad.py tests/test_gpu_mha_block.py tests/test_gpu_shard.py -k "rowmajor_x or two_stream or group or tsvad or mha or shard" > $O/t.log 2>&1; r=$?
+timeout -k 10 500 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_switches.py tests/test_gpu_tsvad.py tests/test_gpu_mha_block.py tests/test_gpu_shard.py -k "rowmajor or two_stream or group or tsvad or mha or shard" > $O/t.log 2>&1; r=$?
 echo "tests rc=$r"; tail -4 $O/t.log
 [ $r -eq 0 ] || exit 1
 for i in 1 2 3; do
-for g in tiled rowmajor; do
-  unset SDIAR_RP_ROWMAJOR_X
-  [ $g = rowmajor ] && export SDIAR_RP_ROWMAJOR_X=1
+for g in tiled rowa rowmajor; do
+  unset SDIAR_RP_ROWMAJOR_X SDIAR_RP_ROWMAJOR_A
+  [ $g = rowmajor ] && export SDIAR_RP_ROWMAJOR_X=1; [ $g = rowa ] && export SDIAR_RP_ROWMAJOR_A=1
   timeout -k 10 300 python3 bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline --no-c4-ref > $O/c2_$g$i.json 2> $O/c2_$g$i.err || { echo "c2 $g failed"; tail -5 $O/c2_$g$i.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'])" $O/c2_$g$i.json
 done
 done
 unset SDIAR_RP_ROWMAJOR_X
-for g in tiled rowmajor; do
-  [ $g = rowmajor ] && export SDIAR_RP_ROWMAJOR_X=1
+for g in tiled rowa rowmajor; do
+  [ $g = rowmajor ] && export SDIAR_RP_ROWMAJOR_X=1; [ $g = rowa ] && export SDIAR_RP_ROWMAJOR_A=1
   SDIAR_CAM_ONE_STREAM=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p$g -o run -- python3 bench.py --workload c2 --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-c4-ref > $O/p$g.log 2>&1 || { echo "prof failed"; exit 1; }
   f=$(find $O/p$g -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats_$g.csv; rm -rf $O/p$g
   python3 - "$O/kernel_stats_$g.csv" <<'PY'
