@@ -481,6 +481,19 @@ __device__ __forceinline__ float xor32_max(float x) {
   return vmax(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// Small grids (fewer (sequence, head) pairs than XCDs: the FS-EEND encoder's 4 heads of one recording): each pair's
+// query blocks go to 8 / nsh XCDs (block b runs on XCD b % 8), alternating between them in heaviest-first order so
+// the XCDs of a pair get the same mix of long and short blocks, and a pair's K/V prefix is fetched into 8 / nsh
+// L2s instead of all eight (round 5: FETCH_SIZE 55 MB per C5 encoder launch for 12.3 MB of Q, K, V and O).
+// Identity when the split is not exact.
+__device__ __forceinline__ int xcd_group_remap(int lin, int nqb, int nsh) {
+  if (nsh >= 8 || 8 % nsh != 0) return lin;
+  const int per = 8 / nsh;
+  if (nqb % per != 0) return lin;
+  const int x = lin & 7, k = lin >> 3;
+  return (x / per) * nqb + k * per + x % per;
+}
+
 template <int HD, int HOIST>   // 0: reads next to their MFMAs; 1: K + first V half hoisted; 2: all hoisted
 __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   // row strides (bf16) HD + 16: the only padding up to 32 with conflict-free ds_read_b128 K fragments
@@ -509,7 +522,8 @@ __global__ __launch_bounds__(512) void attn_long_kernel(AttnArgs a) {
   const int nqb = (int)gridDim.x;
   // (large grids only: a small grid's heads would land whole on few XCDs, heavy query blocks together)
   const int lin = (int)(blockIdx.y * nqb + (int)blockIdx.x);
-  const int lid = HOIST == 2 ? lin : xcd_remap(lin, nqb * (int)gridDim.y);
+  const int lid = HOIST == 2 ? (a.xcd_small ? xcd_group_remap(lin, nqb, (int)gridDim.y) : lin)
+                             : xcd_remap(lin, nqb * (int)gridDim.y);
   const int sh = lid / nqb, s = sh / a.nh, h = sh % a.nh;
   const int T = a.T, D = a.D;
   const int qbi = lid - sh * nqb;
@@ -868,7 +882,10 @@ bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
     // (a split of each query block's key pairs over two workgroups measured 60 -> 54 us here, but the split
     // depends on the grid, so sharded runs — EDA chunk shards, bit-identical for any world size — would
     // differ by world size; not kept)
-    hipLaunchKernelGGL((attn_long_kernel<HD, 2>), grid, dim3(512), 0, st, a);
+    static const bool no_group = getenv("SDIAR_ATTN_NO_GROUP_REMAP") != nullptr;   // A/B switch
+    AttnArgs b = a;
+    b.xcd_small = !no_group;
+    hipLaunchKernelGGL((attn_long_kernel<HD, 2>), grid, dim3(512), 0, st, b);
   } else {
     // large grids: K and the first V half hoisted (126 VGPRs, still 4 waves per SIMD): 187 -> 178 us on the
     // FS-EEND decoder shape against the unhoisted variant (116 VGPRs)

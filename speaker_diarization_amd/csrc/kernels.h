@@ -205,6 +205,7 @@ struct AttnArgs {
   // Test probe (sd_probe_attention_mask): mask_dump (T*T int32, zeroed) receives 1/2 = visible/masked
   // for each visited pair of seq 0, head 0.
   int* mask_dump = nullptr;
+  int xcd_small = 0;   // set by the launcher: the small-grid XCD grouping of attn_long (attention.hip)
 };
 void attention(const AttnArgs& a, bool bf16, hipStream_t st);
 

@@ -21,7 +21,7 @@ FAMILIES = [
     ("frontend", r"fbank_kernel|window_cmn|nonfinite_windows|zero_fill"),
     ("campp", r"fcm_conv3x3|cam_dense|cam_local|cam_context|gemm_ring_kernel<true|gemm_dma_kernel|stats_pool"),
     ("down+gsp", r"gemm_bf16_kernel|gsp_fc"),
-    ("conformer", r"rowprog_kernel|mha_block|gemm_areg|dwconv_pk|glu_dwconv"),
+    ("conformer", r"rowprog_kernel|mha_block|gemm_areg|dwconv_pk|dwconv_pp|glu_dwconv"),
     ("lstm", r"lstm_group|lstm_step|gemm_ring_kernel<false"),
     ("tail", r"poison_windows|overlap_average|overlap_mean|elementwise|FillFunctor|medfilt|run_segments"),
     ("copy", r"__amd_rocclr"),
