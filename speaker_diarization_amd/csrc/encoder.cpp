@@ -264,6 +264,9 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   const int tiled = !rowmajor && rows % 16 == 0;
   static const bool rowmajor_a = getenv("SDIAR_RP_ROWMAJOR_A") != nullptr;   // A/B: the attention output row-major
   const int tiled_a = tiled && !rowmajor_a && mha_block_supported(E, nh, T, true);
+  // the attention LayerNorm's rows (y of the FFN programs) go only to mha_block: tiled as well
+  static const bool rowmajor_y = getenv("SDIAR_RP_ROWMAJOR_Y") != nullptr;   // A/B switch
+  const int tiled_y = tiled_a && !rowmajor_y;
   auto ffn = [](const ConformerL& L, bool second) {
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
@@ -283,6 +286,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     r.n_ffn = 1; r.ffn[0] = ffn(Ls[0], false);
     r.y = y.p; r.y_g = Ls[0].at_lng; r.y_b = Ls[0].at_lnb;
     r.xo_tiled = tiled;
+    r.y_tiled = tiled_y;
     rowprog(r, "rowprog_ffn", st);
   }
   for (size_t li = 0; li < Ls.size(); ++li) {
@@ -294,6 +298,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       m.W = L.in_proj.w; m.bias = L.in_b; m.out = ao.p; m.ldo = E;
       m.S = S; m.T = T; m.D = E; m.nh = nh; m.scale = 1.f / std::sqrt((float)(E / nh)); m.key_len = key_len;
       m.out_tiled = tiled_a;   // read only by the out-projection program below
+      m.y_tiled = tiled_y;
       mha_block(m, st);
     } else {
       conv_gemm(lin(y, rows, E, L.in_proj, L.in_b, qkv, 3 * E), true, st);
@@ -335,6 +340,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
         r.n_ffn = 2; r.ffn[1] = ffn(Ln, false);
         r.y = y.p; r.y_g = Ln.at_lng; r.y_b = Ln.at_lnb;
         r.xo_tiled = tiled;
+        r.y_tiled = tiled_y;
       } else if (io) {
         r.Xo = nullptr; r.yt = io->out; r.yt_NS = io->NS; r.T_seq = T;
       }   // else: the stack's output X, row-major (in place over the tiled input: a tile is read whole first)

@@ -228,6 +228,7 @@ struct MhaBlockArgs {
   // out in the row programs' tiled A layout (RowProgArgs::a_tiled; needs S * T % 16 == 0, ldo == D) instead of
   // row-major rows of stride ldo
   int out_tiled = 0;
+  int y_tiled = 0;   // y in that layout too (RowProgArgs::y_tiled)
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
 
@@ -282,6 +283,7 @@ struct RowProgArgs {
   // f = 32 kk + 8 q + j at bf16 ((g * 12 + kk) * 64 + l + 16 q) * 8 + j, so fragment kk of a 16-row group is one
   // contiguous 1-KiB run (mha_block writes it with out_tiled)
   int a_tiled = 0;
+  int y_tiled = 0;   // y written in the a_tiled layout (for mha_block, MhaBlockArgs::y_tiled)
 };
 bool rowprog_supported(int D, int hidden, bool bf16);
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st);

@@ -124,10 +124,15 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
     const int row = rowj[rt];
     const int s = blockIdx.x * SEQ + sqj[rt];
     const bool live = rt < ntile && s < a.S && row < T;
-    const uint16_t* yr = reinterpret_cast<const uint16_t*>(a.y) + ((int64_t)s * T + row) * kD;
+    const int64_t r = (int64_t)s * T + row;
+    // row-major: features 32 kk + 8 lk of row r; tiled (RowProgArgs::a_tiled layout): fragment kk of r's 16-row
+    // group, lane (r % 16) + 16 lk
+    const uint16_t* yr = a.y_tiled ? reinterpret_cast<const uint16_t*>(a.y) + (r >> 4) * (16 * kD) + ((r & 15) + 16 * lk) * 8
+                                   : reinterpret_cast<const uint16_t*>(a.y) + r * kD + 8 * lk;
+    const int ks = a.y_tiled ? 512 : 32;
 #pragma unroll
     for (int kk = 0; kk < kKT32; ++kk)
-      af[rt][kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(yr + 32 * kk + 8 * lk)
+      af[rt][kk] = __builtin_bit_cast(bf16x8, live ? *reinterpret_cast<const uint4*>(yr + ks * kk)
                                                    : make_uint4(0u, 0u, 0u, 0u));
   }
 
@@ -324,8 +329,8 @@ bool mha_block_supported(int D, int nh, int T, bool bf16) {
 void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   SD_CHECK(mha_block_supported(kD, a.nh, a.T, true) && a.D == kD, kErrInvalid, "mha_block: unsupported shape");
   SD_CHECK(a.ldo % 4 == 0, kErrInvalid, "mha_block: output row stride must be a multiple of 4");
-  SD_CHECK(!a.out_tiled || ((int64_t)a.S * a.T % 16 == 0 && a.ldo == kD), kErrInvalid,
-           "mha_block: the tiled output layout needs S * T % 16 == 0 and ldo == D");
+  SD_CHECK(!(a.out_tiled || a.y_tiled) || ((int64_t)a.S * a.T % 16 == 0 && a.ldo == kD), kErrInvalid,
+           "mha_block: the tiled layouts need S * T % 16 == 0 and ldo == D");
   if (a.S <= 0) return;
   SD_CHECK(a.y != nullptr, kErrInvalid, "mha_block: y (LayerNorm'd bf16 rows) is required");
   const double rows = (double)a.S * a.T;

@@ -467,12 +467,16 @@ void rowprog_kernel(RowProgArgs a) {
         float mean, rstd;
         ln_stats<TT>(acc, tt, a.eps, mean, rstd);
         if (live[tt]) {
-          uint16_t* yo = static_cast<uint16_t*>(a.y) + row[tt] * kD + g4;
+          // row-major: features 16 ft + g4 of the row; tiled (a_tiled layout): fragment ft / 2 of the row's 16-row
+          // group, lane l15 + 16 (2 (ft % 2) + g4 / 8), elements g4 % 8 .. + 3
+          uint16_t* yo = a.y_tiled ? static_cast<uint16_t*>(a.y) + (row[tt] - l15) * kD + (l15 + 16 * (g4 >> 3)) * 8 + (g4 & 7)
+                                   : static_cast<uint16_t*>(a.y) + row[tt] * kD + g4;
 #pragma unroll
           for (int ft = 0; ft < kFT; ++ft) {
             const float4 gq = *reinterpret_cast<const float4*>(prm + kPrmY + 16 * ft + g4);
             const float4 bq = *reinterpret_cast<const float4*>(prm + kPrmY + kD + 16 * ft + g4);
-            *reinterpret_cast<uint2*>(yo + 16 * ft) =
+            const int fo = a.y_tiled ? (ft >> 1) * 512 + (ft & 1) * 256 : 16 * ft;
+            *reinterpret_cast<uint2*>(yo + fo) =
                 make_uint2(pack_bf16x2((acc[ft][tt][0] - mean) * rstd * gq.x + bq.x,
                                        (acc[ft][tt][1] - mean) * rstd * gq.y + bq.y),
                            pack_bf16x2((acc[ft][tt][2] - mean) * rstd * gq.z + bq.z,
@@ -562,7 +566,7 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(!a.x_ts || (a.x_mix && a.x_NS > 0 && a.T_seq > 0 && a.x_Tmix > 0 && a.x_ldmix % 4 == 0), kErrInvalid,
            "rowprog: speaker-input source arguments");
   SD_CHECK(!a.yt || (a.yt_NS > 0 && a.T_seq > 0), kErrInvalid, "rowprog: channel-layout output arguments");
-  SD_CHECK(!(a.x_tiled || a.xo_tiled || a.a_tiled) || a.M % 16 == 0, kErrInvalid,
+  SD_CHECK(!(a.x_tiled || a.xo_tiled || a.a_tiled || a.y_tiled) || a.M % 16 == 0, kErrInvalid,
            "rowprog: the tiled X / A layouts need M % 16 == 0");
   if (a.M <= 0) return;
   static int grid_max = 0;
