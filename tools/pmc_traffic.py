@@ -33,7 +33,7 @@ CATEGORIES = {
     "fcm_conv3x3_band": r"fcm_conv3x3_kernel|fcm_conv3x3_band_kernel<(4, 1|2, 2|10, 2), false|fcm_conv3x3_ring_kernel",
     "attention_bf16": r"attn_\w*kernel|attention\w*kernel",
     "lstm_recurrence": r"lstm_(?!handoff)\w*kernel",   # not the hand-off floor probe
-    "dwconv": r"glu_dwconv_kernel|dwconv_pk_kernel",
+    "dwconv": r"glu_dwconv_kernel|dwconv_pk_kernel|dwconv_pp_kernel",
     "groupnorm_silu": r"groupnorm\w*kernel",
     "cam_context": r"cam_context\w*kernel",
     "cam_dense": r"cam_dense_kernel",
