@@ -266,6 +266,9 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(!p.gate || p.gate_seg > 0, kErrInvalid, "conv_gemm: gate_seg must be > 0");
   SD_CHECK(!p.glu || (bf16 && gemm_stream_supported(p)), kErrInvalid,
            "conv_gemm: the GLU epilogue exists on the bf16 streaming path only");
+  SD_CHECK(!p.a_tiled || (bf16 && p.a_bf16 && p.lda == p.K && p.a_coff == 0 && (p.B * p.Ho * p.Wo) % 16 == 0 &&
+                           gemm_areg_supported(p)),
+           kErrInvalid, "conv_gemm: the tiled A layout exists on the register-A GEMM only");
   if (gemm_skinny_supported(p)) {   // <= 16 rows: weight streaming (streaming FS-EEND chunks)
     conv_gemm_skinny(p, bf16, st);
     return;

@@ -308,6 +308,13 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       a.key_len = key_len;
       attention(a, true, st);
     }
+    // pw1 (+ GLU) reads the conv-LN rows the out-projection program writes: tiled when the register-A GEMM
+    // takes it (SDIAR_RP_ROWMAJOR_Y: row-major, A/B)
+    ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
+    p1.glu = 1;
+    const bool glu_epi = gemm_stream_supported(p1);
+    if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
+    p1.a_tiled = tiled && !rowmajor_y && gemm_areg_supported(p1);
     {
       RowProgArgs r;
       r.X = X; r.Xo = X; r.M = rows;
@@ -315,13 +322,10 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       r.y = y.p; r.y_g = L.cv_lng; r.y_b = L.cv_lnb;
       r.x_tiled = r.xo_tiled = tiled;
       r.a_tiled = tiled_a;
+      r.y_tiled = p1.a_tiled;
       rowprog(r, "rowprog_out", st);
     }
     {
-      ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
-      p1.glu = 1;
-      const bool glu_epi = gemm_stream_supported(p1);
-      if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
       conv_gemm(p1, true, st);
       glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
                  !glu_epi, true, st);

@@ -127,7 +127,10 @@ __global__ __launch_bounds__(512) void gemm_areg_kernel(ConvGemmArgs p) {
   bf16x8 af[MT][KT32];
   auto load_a = [&](int tile, int mt, int kk) {
     const int m = tile * RB + wid * 32 + mt * 16 + l15;
-    const uint32_t off = m < M ? (uint32_t)(((int64_t)m * p.lda + p.a_coff + kk * 32 + lk * 8) * 2) : kOOB;
+    // tiled: fragment kk of row m's 16-row group, lane l15 + 16 lk (one contiguous 1-KiB run per instruction)
+    const int64_t e = p.a_tiled ? ((int64_t)((m >> 4) * KT32 + kk) * 64 + l15 + 16 * lk) * 8
+                                : (int64_t)m * p.lda + p.a_coff + kk * 32 + lk * 8;
+    const uint32_t off = m < M ? (uint32_t)(e * 2) : kOOB;
     const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0);
     af[mt][kk] = __builtin_bit_cast(bf16x8, v);
   };

@@ -13,6 +13,9 @@ struct ConvGemmArgs {
   const void* A = nullptr;
   bool a_bf16 = false;
   int B = 1, H = 1, W = 1, Cin = 0, lda = 0, a_coff = 0;
+  // A (bf16, lda == K, M % 16 == 0) in the row programs' tiled fragment layout (RowProgArgs::a_tiled): only the
+  // register-A GEMM takes it (conv_gemm refuses it otherwise)
+  int a_tiled = 0;
   int Ho = 1, Wo = 1;
   int kh = 1, kw = 1, sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
   // Packed weights Wt[N][K] (bf16 bits or fp32), K = kh*kw*Cin, tap-major.
