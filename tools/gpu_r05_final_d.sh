@@ -4,6 +4,6 @@ set -uo pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 O=gpurun_out/r05
 mkdir -p $O
-FULL=1 bash tools/profile_round.sh $O c2 || { echo "profile_round failed"; exit 1; }
+FULL=1 bash tools/profile_round.sh $O c2 c5 || { echo "profile_round failed"; exit 1; }
 timeout -k 10 600 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo "default bench failed"; exit 1; }
 echo done
