@@ -267,7 +267,6 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   // the attention LayerNorm's rows (y of the FFN programs) go only to mha_block: tiled as well
   static const bool rowmajor_y = getenv("SDIAR_RP_ROWMAJOR_Y") != nullptr;   // A/B switch
   const int tiled_y = tiled_a && !rowmajor_y;
-  static const bool rowmajor_dw = getenv("SDIAR_RP_ROWMAJOR_DW") != nullptr;   // A/B: the dwconv output row-major
   auto ffn = [](const ConformerL& L, bool second) {
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
@@ -330,7 +329,7 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     {
       conv_gemm(p1, true, st);
       dw_tiled = glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr,
-                            !L.group_norm, !glu_epi, true, st, tiled && !rowmajor_a && !rowmajor_dw);
+                            !L.group_norm, !glu_epi, true, st, tiled && !rowmajor_a);
     }
     {
       RowProgArgs r;

@@ -184,7 +184,7 @@ def test_cam_two_stream_slices_bit_identical(gpu):
 def _tsvad_hash(extra_env):
     env = dict(os.environ)
     for k in ("SDIAR_MHA_SEQ2", "SDIAR_SLICES", "SDIAR_LSTM_GRANULE", "SDIAR_NO_DWCONV_PP", "SDIAR_RP_ROWMAJOR_X",
-              "SDIAR_RP_ROWMAJOR_A", "SDIAR_RP_ROWMAJOR_Y", "SDIAR_RP_ROWMAJOR_DW"):
+              "SDIAR_RP_ROWMAJOR_A", "SDIAR_RP_ROWMAJOR_Y"):
         env.pop(k, None)
     env.update(extra_env)
     r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
@@ -196,10 +196,9 @@ def _tsvad_hash(extra_env):
 
 @pytest.mark.parametrize("switch", [{"SDIAR_MHA_SEQ2": "1"}, {"SDIAR_SLICES": "3"}, {"SDIAR_SLICES": "4"},
                                     {"SDIAR_LSTM_GRANULE": "1"}, {"SDIAR_NO_DWCONV_PP": "1"}, {"SDIAR_RP_ROWMAJOR_X": "1"},
-                                    {"SDIAR_RP_ROWMAJOR_A": "1"}, {"SDIAR_RP_ROWMAJOR_Y": "1"},
-                                    {"SDIAR_RP_ROWMAJOR_DW": "1"}],
+                                    {"SDIAR_RP_ROWMAJOR_A": "1"}, {"SDIAR_RP_ROWMAJOR_Y": "1"}],
                          ids=["mha_seq2", "slices3", "slices4", "lstm_granule", "dwconv_pp", "rowmajor_x", "rowmajor_a",
-                              "rowmajor_y", "rowmajor_dw"])
+                              "rowmajor_y"])
 def test_schedule_switches_bit_identical(gpu, switch):
     """Switches that change only the schedule or the transport, never the arithmetic, must leave the TS-VAD
     logits (ots_vad v1 with its BiLSTM, and the CAM++/transformer model; 400 windows: two-stream slices) bit
