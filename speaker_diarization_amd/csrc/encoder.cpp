@@ -310,7 +310,6 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     }
     // pw1 (+ GLU) reads the conv-LN rows the out-projection program writes: tiled when the register-A GEMM
     // takes it (SDIAR_RP_ROWMAJOR_Y: row-major, A/B)
-    bool dw_tiled = false;
     ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
     p1.glu = 1;
     const bool glu_epi = gemm_stream_supported(p1);
@@ -328,14 +327,13 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
     }
     {
       conv_gemm(p1, true, st);
-      dw_tiled = glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr,
-                            !L.group_norm, !glu_epi, true, st, tiled && !rowmajor_a);
+      glu_dwconv(h.p, S, T, E, L.dw_w, L.dw_b, kernel, ao.p, L.group_norm ? w.partial : nullptr, !L.group_norm,
+                 !glu_epi, true, st);
     }
     {
       RowProgArgs r;
       r.X = X; r.Xo = X; r.M = rows;
       r.A = ao.p; r.w0 = L.rp_pw2; r.b0 = L.pw2_b;
-      r.a_tiled = dw_tiled;   // the depthwise conv's rows in the fragment layout (persistent kernel only)
       if (L.group_norm) {   // GroupNorm + SiLU applied by the program as it loads A (no separate pass)
         r.gn_partial = w.partial; r.gn_nblk = (E + 63) / 64; r.gn_T = T; r.gn_g = L.gn_g; r.gn_b = L.gn_b;
       }

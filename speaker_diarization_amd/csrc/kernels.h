@@ -376,11 +376,9 @@ void speakers_to_channels(const float* x, int B, int NS, int T, int E, void* out
 // (glu_interleave_row) and the GLU is applied on load; else x is already gated (S, T, C).
 // Writes per (sequence, channel-block) partial sums for GroupNorm(1, C), or with
 // fused_silu (BatchNorm already folded into w/bias) stores SiLU(y) and no partials.
-// y_tiled: write y in the row programs' tiled fragment layout (RowProgArgs::a_tiled) when the persistent kernel
-// takes the call; returns whether it did (the caller's reader must then take a_tiled).
-bool glu_dwconv(const void* x, int S, int T, int C, const float* w /*C x k*/,
+void glu_dwconv(const void* x, int S, int T, int C, const float* w /*C x k*/,
                 const float* bias, int k, void* y, float* partial /*S x nblk x 2*/, bool fused_silu,
-                bool glu_in, bool io_bf16, hipStream_t st, bool y_tiled = false);
+                bool glu_in, bool io_bf16, hipStream_t st);
 // GroupNorm(num_groups=1) over (T, C) of each sequence, affine, then SiLU (in place).
 void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const float* g,
                     const float* b, float eps, bool io_bf16, hipStream_t st);

@@ -847,8 +847,7 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 // their GroupNorm partial sums (lsum, lsq).
 template <int K, int R>
 __device__ __forceinline__ void dw_run(const uint32_t* g, int r0, int cp, int nout, const float2v (&wr)[K], float2v bv,
-                                       bool fused_silu, uint16_t* yrow, int C, float& lsum, float& lsq,
-                                       uint16_t* ytile = nullptr, int64_t R0 = 0, int c = 0) {
+                                       bool fused_silu, uint16_t* yrow, int C, float& lsum, float& lsq) {
   float2v acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = bv;
@@ -876,12 +875,7 @@ __device__ __forceinline__ void dw_run(const uint32_t* g, int r0, int cp, int no
     float2v v = acc[r];
     if (fused_silu) v = float2v{v.x * sigmoid_rcp(v.x), v.y * sigmoid_rcp(v.y)};
     if (r < nout) {
-      // ytile: the row programs' tiled fragment layout (RowProgArgs::a_tiled) for absolute row R0 + r, channels
-      // c, c + 1: fragment c / 32 of the row's 16-row group, lane (row % 16) + 16 ((c % 32) / 8)
-      const int64_t ra = R0 + r;
-      uint16_t* dst = ytile ? ytile + (((ra >> 4) * (C >> 5) + (c >> 5)) * 64 + (ra & 15) + 16 * ((c & 31) >> 3)) * 8 + (c & 7)
-                            : yrow + (int64_t)r * C;
-      *reinterpret_cast<uint32_t*>(dst) = pack_bf16x2(v.x, v.y);
+      *reinterpret_cast<uint32_t*>(yrow + (int64_t)r * C) = pack_bf16x2(v.x, v.y);
       lsum += v.x + v.y;
       lsq = fmaf(v.x, v.x, lsq);
       lsq = fmaf(v.y, v.y, lsq);
@@ -1000,7 +994,7 @@ template <int K, int R>
 __global__ __launch_bounds__(256) void dwconv_pp_kernel(const uint16_t* __restrict__ x, int S, int T, int C,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         uint16_t* __restrict__ y, float* __restrict__ partial,
-                                                        int fused_silu, int y_tiled) {
+                                                        int fused_silu) {
   constexpr int kRows = 8 * R + K - 1;
   constexpr int kItems = kRows * 8;
   constexpr int kIters = (kItems + 255) / 256;
@@ -1041,8 +1035,7 @@ __global__ __launch_bounds__(256) void dwconv_pp_kernel(const uint16_t* __restri
     float lsum = 0.f, lsq = 0.f;
     const int r0 = slot * R, nout = T - r0;
     if (nout > 0)
-      dw_run<K, R>(g, r0, cp, nout, wr, bv, fused_silu, y + ((int64_t)s * T + r0) * C + c, C, lsum, lsq,
-                   y_tiled ? y : nullptr, (int64_t)s * T + r0, c);
+      dw_run<K, R>(g, r0, cp, nout, wr, bv, fused_silu, y + ((int64_t)s * T + r0) * C + c, C, lsum, lsq);
     if (!fused_silu) dw_gn_partial(red, tid, lsum, lsq, partial + ((int64_t)s * ncb + cb) * 2);
   }
 }
@@ -1072,7 +1065,7 @@ static void launch_dwconv_pk(int R, dim3 grid, hipStream_t st, const uint16_t* x
 // persistent grid: as many workgroups as fit on the device at once, a multiple of the channel blocks
 template <int K, int R>
 static void launch_dwconv_pp_r(int S, int T, int C, hipStream_t st, const uint16_t* x, const float* w, const float* bias,
-                               uint16_t* y, float* partial, int fused_silu, int y_tiled) {
+                               uint16_t* y, float* partial, int fused_silu) {
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per = 0;
@@ -1084,19 +1077,19 @@ static void launch_dwconv_pp_r(int S, int T, int C, hipStream_t st, const uint16
   const int ncb = C / kDwCB;
   const int per_cb = std::max(1, std::min(S, resident / ncb));
   hipLaunchKernelGGL((dwconv_pp_kernel<K, R>), dim3(per_cb * ncb), dim3(256), 0, st, x, S, T, C, w, bias, y, partial,
-                     fused_silu, y_tiled);
+                     fused_silu);
 }
 
 template <int K>
 static void launch_dwconv_pp(int R, int S, int T, int C, hipStream_t st, const uint16_t* x, const float* w,
-                             const float* bias, uint16_t* y, float* partial, int fused_silu, int y_tiled) {
-  if (R == 9) launch_dwconv_pp_r<K, 9>(S, T, C, st, x, w, bias, y, partial, fused_silu, y_tiled);
-  else if (R == 13) launch_dwconv_pp_r<K, 13>(S, T, C, st, x, w, bias, y, partial, fused_silu, y_tiled);
-  else launch_dwconv_pp_r<K, 19>(S, T, C, st, x, w, bias, y, partial, fused_silu, y_tiled);
+                             const float* bias, uint16_t* y, float* partial, int fused_silu) {
+  if (R == 9) launch_dwconv_pp_r<K, 9>(S, T, C, st, x, w, bias, y, partial, fused_silu);
+  else if (R == 13) launch_dwconv_pp_r<K, 13>(S, T, C, st, x, w, bias, y, partial, fused_silu);
+  else launch_dwconv_pp_r<K, 19>(S, T, C, st, x, w, bias, y, partial, fused_silu);
 }
 
-bool glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
-                void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st, bool y_tiled) {
+void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float* bias, int k,
+                void* y, float* partial, bool fused_silu, bool glu_in, bool io_bf16, hipStream_t st) {
   SD_CHECK(fused_silu || partial, kErrInvalid, "glu_dwconv: GroupNorm partials buffer required");
   SD_CHECK(k >= 1 && k <= kDwMaxK && k % 2 == 1, kErrInvalid, "glu_dwconv: kernel size must be odd and <= 31");
   SD_CHECK(C % 16 == 0, kErrInvalid, "glu_dwconv: channels must be a multiple of 16");
@@ -1109,11 +1102,8 @@ bool glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
     auto xp = reinterpret_cast<const uint16_t*>(x);
     auto yp = reinterpret_cast<uint16_t*>(y);
     const int R = T <= 8 * 9 ? 9 : T <= 8 * 13 ? 13 : 19;
-    const int yt = y_tiled && C % 32 == 0 && ((int64_t)S * T) % 16 == 0;
-    if (k == 31) launch_dwconv_pp<31>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu, yt);
-    else launch_dwconv_pp<15>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu, yt);
-    SD_LAUNCH_CHECK();
-    return yt != 0;
+    if (k == 31) launch_dwconv_pp<31>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
+    else launch_dwconv_pp<15>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
   } else if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk) {
     const int R = dwconv_pk_runlen(T, k);
     auto xp = reinterpret_cast<const uint16_t*>(x);
@@ -1127,7 +1117,6 @@ bool glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
     hipLaunchKernelGGL(glu_dwconv_kernel<false>, grid, dim3(256), 0, st, reinterpret_cast<const float*>(x), T, C,
                        w, bias, k, reinterpret_cast<float*>(y), partial, (int)fused_silu, (int)glu_in);
   SD_LAUNCH_CHECK();
-  return false;
 }
 
 // GroupNorm(1 group) statistics from the dwconv partials, then y = silu(GN(y)) in place.
