@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
     float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
     uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err,
-    unsigned spin_limit, int* __restrict__ host_err, int out_early) {
+    unsigned spin_limit, int* __restrict__ host_err) {
   constexpr int H = LS_H, BB = 16 * MT;
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -386,7 +386,9 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+      const int b = b0 + mt * 16 + l15;
       if (step >= len[mt]) continue;
+      const int t = d == 0 ? step : len[mt] - 1 - step;
       const float gi[4] = {gxv[mt][0].x, gxv[mt][0].y, gxv[mt][0].z, gxv[mt][0].w};
       const float gf[4] = {gxv[mt][1].x, gxv[mt][1].y, gxv[mt][1].z, gxv[mt][1].w};
       const float gg[4] = {gxv[mt][2].x, gxv[mt][2].y, gxv[mt][2].z, gxv[mt][2].w};
@@ -404,23 +406,11 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
         c[mt][r] = fg * c[mt][r] + ig * cg;
         hr[mt][r] = og * tnh(c[mt][r]);
       }
-    }
-    // the step's output rows AFTER the hand-off: publish's vmcnt(0) then waits for the h payload only, not for
-    // these HBM stores (they complete under the next step's poll).  out_early (A/B, SDIAR_LSTM_OUT_EARLY=1): before.
-    auto store_out = [&] {
-      if (!out) return;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        if (step >= len[mt]) continue;
-        const int b = b0 + mt * 16 + l15;
-        const int t = d == 0 ? step : len[mt] - 1 - step;
+      if (out)
         *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) =
             make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
-      }
-    };
-    if (out_early) store_out();
+    }
     publish(GR ? step + 2 : (step + 1) & 1);   // h_step
-    if (!out_early) store_out();
   }
   // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
   // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
@@ -568,7 +558,6 @@ void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* wh
                          const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                          uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-  static const bool out_early = getenv("SDIAR_LSTM_OUT_EARLY") != nullptr;   // A/B: output rows before the hand-off
   static bool attr = false;
   if (!attr) {
     SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, GR>),
@@ -578,7 +567,7 @@ void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* wh
   const int groups = ndir * cdiv(B, 16 * MT);
   hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, GR>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
-                     counters, err, lstm_spin_limit(), host_err, out_early ? 1 : 0);
+                     counters, err, lstm_spin_limit(), host_err);
   SD_LAUNCH_CHECK();
 }
 
