@@ -66,7 +66,9 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int SEQ, int W, int NSLOT, int QS>
+// PROBE (timing diagnostics, SDIAR_MHA_VARIANT 8-10, wrong outputs): bit 0 skips the attention phase, bit 1 the
+// projection MFMAs
+template <int SEQ, int W, int NSLOT, int QS, int PROBE = 0>
 __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
   using L = MhaL<SEQ, W, NSLOT, QS>;
   constexpr int kTiles = L::kTiles, kMaxTiles = L::kMaxTiles, kThreads = L::kThreads, kSeqLds = L::kSeqLds;
@@ -189,6 +191,10 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
     for (int kk = 0; kk < kKT32; ++kk) {
       const bf16x8 wcur = wq[kk % kWPD];
       if (kk + kWPD < kKT32) wq[kk % kWPD] = wfrag(kk + kWPD);
+      if constexpr (PROBE & 2) {
+        asm volatile("" :: "v"(wcur));
+        continue;
+      }
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[0][kk], acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wcur, af[1][kk], acc[1], 0, 0, 0);
       // the 4-wave layout does not skip the third tile's MFMA for its two-tile waves (af[2] = 0 there): with the
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
         *reinterpret_cast<uint2*>(qimg(sqj[rt]) + coff + rowj[rt] * ld + n0) =
             make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
                        pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
-    if (c != 2 || ft != 2) continue;
+    if (c != 2 || ft != 2 || (PROBE & 1)) continue;
     __syncthreads();   // head h's Q, K, V images complete (every sequence of the workgroup)
 
     // ---- attention of head h for this wave's 16-query tiles
@@ -306,17 +312,17 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
   }
 }
 
-template <int SEQ, int W, int NSLOT, int QS>
+template <int SEQ, int W, int NSLOT, int QS, int PROBE = 0>
 void launch_mha(const MhaBlockArgs& a, hipStream_t st) {
   using L = MhaL<SEQ, W, NSLOT, QS>;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<SEQ, W, NSLOT, QS>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mha_block_kernel<SEQ, W, NSLOT, QS, PROBE>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::kSmem));
     attr = true;
   }
-  hipLaunchKernelGGL((mha_block_kernel<SEQ, W, NSLOT, QS>), dim3((a.S + SEQ - 1) / SEQ), dim3(L::kThreads), L::kSmem, st,
-                     a);
+  hipLaunchKernelGGL((mha_block_kernel<SEQ, W, NSLOT, QS, PROBE>), dim3((a.S + SEQ - 1) / SEQ), dim3(L::kThreads),
+                     L::kSmem, st, a);
 }
 
 }  // namespace
@@ -352,6 +358,9 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
     case 5: launch_mha<1, 8, 3, 64>(a, st); break;
     case 6: launch_mha<1, 8, 2, 48>(a, st); break;
     case 7: launch_mha<2, 8, 4, 48>(a, st); break;
+    case 8: launch_mha<2, 8, 3, 48, 1>(a, st); break;    // probes: no attention
+    case 9: launch_mha<2, 8, 3, 48, 2>(a, st); break;    //         no projection MFMAs
+    case 10: launch_mha<2, 8, 3, 48, 3>(a, st); break;   //         neither (prologue, weight stream, barriers)
     default: launch_mha<2, 8, 3, 48>(a, st); break;
   }
   SD_LAUNCH_CHECK();
