@@ -883,19 +883,23 @@ __device__ __forceinline__ void dw_run(const uint32_t* g, int r0, int cp, int no
   }
 }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads()' release fence also waits for vmcnt(0), which would
+// drain the persistent kernel's next-sequence prefetch at every barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // The block's (sum, sum of squares) over its 256 threads, in the order of a halving tree (t += t + o for
 // o = 128 .. 1): the two cross-wave levels through LDS, the six in-wave ones as shfl_down (same operands, same
 // association, 2 barriers instead of 8).  Thread 0 stores them at out[0], out[1].
 __device__ __forceinline__ void dw_gn_partial(float (&red)[2][256], int tid, float lsum, float lsq, float* out) {
-  __syncthreads();   // red may still be read by the previous call's wave 0
+  lds_barrier();   // red may still be read by the previous call's wave 0
   red[0][tid] = lsum;
   red[1][tid] = lsq;
-  __syncthreads();
+  lds_barrier();
   if (tid < 128) {
     red[0][tid] += red[0][tid + 128];
     red[1][tid] += red[1][tid + 128];
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 64) {
     float a = red[0][tid] + red[0][tid + 64], b = red[1][tid] + red[1][tid + 64];
 #pragma unroll
@@ -1024,13 +1028,13 @@ __global__ __launch_bounds__(256) void dwconv_pp_kernel(const uint16_t* __restri
   int s = blockIdx.x / ncb;
   if (s < S) fetch(s);
   for (; s < S; s += sstep) {
-    __syncthreads();   // the previous sequence's reads of g are done
+    lds_barrier();   // the previous sequence's reads of g are done
 #pragma unroll
     for (int u = 0; u < kIters; ++u) {
       const int i = tid + u * 256;
       if (i < kItems) *reinterpret_cast<uint4*>(g + (i >> 3) * 32 + (i & 7) * 4) = va[u];
     }
-    __syncthreads();
+    lds_barrier();
     if (s + sstep < S) fetch(s + sstep);   // in flight during this sequence's conv
     float lsum = 0.f, lsq = 0.f;
     const int r0 = slot * R, nout = T - r0;
