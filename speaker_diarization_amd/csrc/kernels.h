@@ -232,7 +232,6 @@ struct MhaBlockArgs {
   // row-major rows of stride ldo
   int out_tiled = 0;
   int y_tiled = 0;   // y in that layout too (RowProgArgs::y_tiled)
-  int full_barrier = 0;   // set by mha_block(): SDIAR_MHA_FULL_BARRIER A/B
 };
 bool mha_block_supported(int D, int nh, int T, bool bf16);
 

@@ -170,12 +170,7 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
       wait_vm<0>();
     }
     drain = false;
-    // every wave's part of piece i is in LDS (each wave waited for its own DMAs above); the slot of piece i-1 is
-    // free (each wave's reads of it are done: lgkmcnt(0)).  A plain s_barrier: __syncthreads()' workgroup release
-    // fence waits for vmcnt(0), which drained the pieces still in flight at every piece (round 5 probe: 213 of 777 us
-    // per C2 launch were prologue, weight waits and barriers); SDIAR_MHA_FULL_BARRIER=1 restores it (A/B).
-    if (a.full_barrier) __syncthreads();
-    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __syncthreads();   // every wave's part of piece i is in LDS; the slot of piece i-1 is free
     if (i + NSLOT - 1 < kPieces) issue_piece(i + NSLOT - 1);
     const int h = i / 9, c = (i / 3) % 3, ft = i % 3;
     const uint16_t* slot = Ws + (i % NSLOT) * kSlot;
@@ -224,9 +219,7 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
             make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
                        pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2 || (PROBE & 1)) continue;
-    // head h's Q, K, V images complete (every sequence of the workgroup): LDS stores only
-    if (a.full_barrier) __syncthreads();
-    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __syncthreads();   // head h's Q, K, V images complete (every sequence of the workgroup)
 
     // ---- attention of head h for this wave's 16-query tiles
 #pragma unroll 1
@@ -346,9 +339,6 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
            "mha_block: the tiled layouts need S * T % 16 == 0 and ldo == D");
   if (a.S <= 0) return;
   SD_CHECK(a.y != nullptr, kErrInvalid, "mha_block: y (LayerNorm'd bf16 rows) is required");
-  static const bool full_barrier = getenv("SDIAR_MHA_FULL_BARRIER") != nullptr;
-  MhaBlockArgs b = a;
-  b.full_barrier = full_barrier ? 1 : 0;
   const double rows = (double)a.S * a.T;
   const double flops = 2.0 * rows * 3 * kD * kD + 4.0 * a.S * (double)a.T * a.T * kD;
   const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
@@ -361,17 +351,17 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   static const int var_env = getenv("SDIAR_MHA_SEQ2") ? 1 : getenv("SDIAR_MHA_VARIANT") ? atoi(getenv("SDIAR_MHA_VARIANT")) : 0;
   const int var = variant >= 0 ? variant : var_env;
   switch (var) {
-    case 1: launch_mha<2, 8, 3, 64>(b, st); break;
-    case 2: launch_mha<1, 4, 2, 64>(b, st); break;
-    case 3: launch_mha<1, 4, 2, 48>(b, st); break;
-    case 4: launch_mha<1, 4, 3, 48>(b, st); break;
-    case 5: launch_mha<1, 8, 3, 64>(b, st); break;
-    case 6: launch_mha<1, 8, 2, 48>(b, st); break;
-    case 7: launch_mha<2, 8, 4, 48>(b, st); break;
-    case 8: launch_mha<2, 8, 3, 48, 1>(b, st); break;    // probes: no attention
-    case 9: launch_mha<2, 8, 3, 48, 2>(b, st); break;    //         no projection MFMAs
-    case 10: launch_mha<2, 8, 3, 48, 3>(b, st); break;   //         neither (prologue, weight stream, barriers)
-    default: launch_mha<2, 8, 3, 48>(b, st); break;
+    case 1: launch_mha<2, 8, 3, 64>(a, st); break;
+    case 2: launch_mha<1, 4, 2, 64>(a, st); break;
+    case 3: launch_mha<1, 4, 2, 48>(a, st); break;
+    case 4: launch_mha<1, 4, 3, 48>(a, st); break;
+    case 5: launch_mha<1, 8, 3, 64>(a, st); break;
+    case 6: launch_mha<1, 8, 2, 48>(a, st); break;
+    case 7: launch_mha<2, 8, 4, 48>(a, st); break;
+    case 8: launch_mha<2, 8, 3, 48, 1>(a, st); break;    // probes: no attention
+    case 9: launch_mha<2, 8, 3, 48, 2>(a, st); break;    //         no projection MFMAs
+    case 10: launch_mha<2, 8, 3, 48, 3>(a, st); break;   //         neither (prologue, weight stream, barriers)
+    default: launch_mha<2, 8, 3, 48>(a, st); break;
   }
   SD_LAUNCH_CHECK();
 }
