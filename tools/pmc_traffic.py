@@ -32,7 +32,7 @@ CATEGORIES = {
     "gemm_bf16_reg": r"gemm_bf16_kernel",
     "fcm_conv3x3_band": r"fcm_conv3x3_kernel|fcm_conv3x3_band_kernel<(4, 1|2, 2|10, 2), false|fcm_conv3x3_ring_kernel",
     "attention_bf16": r"attn_\w*kernel|attention\w*kernel",
-    "lstm_recurrence": r"lstm_(?!handoff)\w*kernel",   # not the hand-off floor probe
+    "lstm_recurrence": r"lstm_(?!handoff|granule)\w*kernel",   # not the hand-off floor probes
     "dwconv": r"glu_dwconv_kernel|dwconv_pk_kernel|dwconv_pp_kernel",
     "groupnorm_silu": r"groupnorm\w*kernel",
     "cam_context": r"cam_context\w*kernel",
