@@ -627,7 +627,9 @@ int lstm_group_mt(int B, int ndir) {
   // Smallest row block (16 * MT) whose 4 x groups fit one workgroup per CU, provided the occupancy
   // query admits the kernel at all (co-residency of every workgroup of the grid); else 0 and the
   // caller takes the per-step launches.
-  for (int m = 1; m <= LS_MAXMT; ++m)
+  // SDIAR_LSTM_MT=<m> (diagnostic A/B): at least m row tiles per group
+  static const int mt_min = getenv("SDIAR_LSTM_MT") ? std::max(1, std::min(LS_MAXMT, atoi(getenv("SDIAR_LSTM_MT")))) : 1;
+  for (int m = mt_min; m <= LS_MAXMT; ++m)
     if (4 * ndir * cdiv(B, 16 * m) <= n_cu) return lstm_group_capacity(m) >= 1 ? m : 0;
   return 0;
 }
