@@ -215,16 +215,22 @@ constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (25
 // lstm_granule_probe_kernel -- a lane publishes its 4 units as two 8-byte {bf16 x 2, tag} granules in one 16-B
 // sc1 store, every wave polls exactly the granules of its next MFMA operand until they carry the step's tag; no
 // counter, no barrier, no vmcnt(0) drain in the step loop.  hx then holds [parity][d][Bp][H / 2] granules.
-template <int MT, bool GR = false>
-__global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
+// WV (round 5, default for an even MT): 8 waves per workgroup instead of 4 -- two waves per 16-unit tile, each on half of
+// the group's row tiles (tile j * 2 + (w >> 2)), so every SIMD holds two waves of the step and one's gx loads,
+// transcendentals and stores overlap the other's MFMAs; the W slice, the counters and the exchange are unchanged.
+template <int MT, bool GR = false, int WV = 4>
+__global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
     float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
     uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err,
     unsigned spin_limit, int* __restrict__ host_err) {
-  constexpr int H = LS_H, BB = 16 * MT;
+  constexpr int H = LS_H, BB = 16 * MT, NT = 64 * WV, WPU = WV / 4, MTW = MT / WPU;
+  static_assert(WV == 4 || WV == 8, "4 or 8 waves");
+  static_assert(MT % WPU == 0, "the row tiles split evenly over the waves of a unit tile");
+  static_assert(!GR || WV == 4, "granule transport: 4 waves");
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, wt = tid >> 8;
   const int l15 = lane & 15, g = lane >> 4;
   const int q = blockIdx.x & 3;                 // unit quarter
   const int grp = blockIdx.x >> 2;
@@ -233,11 +239,12 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   const int G4 = ndir * 4 * H;
   unsigned* cnt = counters + grp * LS_CNT_STRIDE;   // one cache line per group (no false sharing)
   const int ub = 64 * q + 16 * w + 4 * g;       // first of this lane's 4 units
+  auto rb = [&](int j) { return b0 + (j * WPU + wt) * 16 + l15; };   // batch row of the lane in its j-th tile
 
   // W slice -> LDS: slice row (gate, j) = W_hh row gate*H + 64q + j.
   {
     const uint16_t* wd = whh + (int64_t)d * 4 * H * H;
-    for (int i = tid; i < 256 * (H / 8); i += 256) {
+    for (int i = tid; i < 256 * (H / 8); i += NT) {
       const int row = i / (H / 8), k8 = (i % (H / 8)) * 8;
       const int gate = row >> 6, j = row & 63;
       *reinterpret_cast<uint4*>(&wsl[row * LS_WS + k8]) =
@@ -251,11 +258,11 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   auto hx_off = [&](int parity, int b, int u) {   // byte offset
     return (uint32_t)(((int64_t)parity * plane + ((int64_t)d * Bp + b) * H + u) * EB);
   };
-  float c[MT][4], hr[MT][4];
-  int len[MT];
+  float c[MTW][4], hr[MTW][4];
+  int len[MTW];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int b = b0 + mt * 16 + l15;
+  for (int mt = 0; mt < MTW; ++mt) {
+    const int b = rb(mt);
     len[mt] = b < B ? (lengths ? lengths[b] : T) : 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -277,16 +284,16 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
     if constexpr (GR) {
       const uint32_t tag = (uint32_t)parity;   // GR: the argument is the tag
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mt = 0; mt < MTW; ++mt) {
         const u32x4_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), tag, pack_bf16x2(hr[mt][2], hr[mt][3]), tag};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rg, g_off(tag & 1, b0 + mt * 16 + l15, ub / 2), 0, 16);   // sc1
+        __builtin_amdgcn_raw_buffer_store_b128(v, rg, g_off(tag & 1, rb(mt), ub / 2), 0, 16);   // sc1
       }
       return;
     }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
       const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
-      __builtin_amdgcn_raw_buffer_store_b64(v, rh, hx_off(parity, b0 + mt * 16 + l15, ub), 0, 16);   // sc1
+      __builtin_amdgcn_raw_buffer_store_b64(v, rh, hx_off(parity, rb(mt), ub), 0, 16);   // sc1
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -315,10 +322,10 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   publish(GR ? 1 : 0);   // h_{-1}
   for (int step = 0; step < max_len; ++step) {
     // gx of this step for the lane's rows: 4 gates x 4 units (float4), issued before the wait.
-    float4 gxv[MT][4];
+    float4 gxv[MTW][4];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int b = b0 + mt * 16 + l15;
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int b = rb(mt);
       const bool live = step < len[mt];
       const int t = d == 0 ? step : len[mt] - 1 - step;
       const float* gr = gx + ((int64_t)(live ? b : 0) * T + (live ? t : 0)) * G4 + d * 4 * H + ub;
@@ -327,12 +334,12 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
         gxv[mt][gate] = live ? *reinterpret_cast<const float4*>(gr + gate * H) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const int pin = step & 1;
-    floatx4 acc[MT][4];
+    floatx4 acc[MTW][4];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 hfa[MT][H / 32];
+    bf16x8 hfa[MTW][H / 32];
     if constexpr (GR) {
       // poll exactly this lane's operand granules (units kc * 32 + 8 g .. + 7 of its rows) for h_{step-1}'s tag
       const uint32_t want = (uint32_t)step + 1u;
@@ -343,9 +350,9 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
 #pragma unroll
         for (int kc = 0; kc < H / 32; ++kc)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const u32x4_t lo = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, b0 + mt * 16 + l15, (kc * 32 + 8 * g) / 2), 0, 16);
-            const u32x4_t hi = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, b0 + mt * 16 + l15, (kc * 32 + 8 * g) / 2 + 2), 0, 16);
+          for (int mt = 0; mt < MTW; ++mt) {
+            const u32x4_t lo = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, rb(mt), (kc * 32 + 8 * g) / 2), 0, 16);
+            const u32x4_t hi = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, rb(mt), (kc * 32 + 8 * g) / 2 + 2), 0, 16);
             ok &= lo[1] == want && lo[3] == want && hi[1] == want && hi[3] == want;
             const u32x4_t v = {lo[0], lo[2], hi[0], hi[2]};
             hfa[mt][kc] = __builtin_bit_cast(bf16x8, v);
@@ -367,26 +374,26 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
 #pragma unroll
     for (int kc = 0; kc < H / 32; ++kc)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MTW; ++mt)
         hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rh, hx_off(pin, b0 + mt * 16 + l15, kc * 32 + 8 * g), 0, 16));
+                                                     rh, hx_off(pin, rb(mt), kc * 32 + 8 * g), 0, 16));
     }
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
-      bf16x8 hf[MT];
+      bf16x8 hf[MTW];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) hf[mt] = hfa[mt][k0 / 32];
+      for (int mt = 0; mt < MTW; ++mt) hf[mt] = hfa[mt][k0 / 32];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) {
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MTW; ++mt)
           acc[mt][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mt], acc[mt][gate], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int b = b0 + mt * 16 + l15;
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int b = rb(mt);
       if (step >= len[mt]) continue;
       const int t = d == 0 ? step : len[mt] - 1 - step;
       const float gi[4] = {gxv[mt][0].x, gxv[mt][0].y, gxv[mt][0].z, gxv[mt][0].w};
@@ -403,7 +410,9 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
         const float fg = sig(acc[mt][1][r] + gf[r]);
         const float cg = tnh(acc[mt][2][r] + gg[r]);
         const float og = sig(acc[mt][3][r] + go[r]);
-        c[mt][r] = fg * c[mt][r] + ig * cg;
+        // one explicit fma: left to -ffp-contract, the instantiations for different row-tile counts fused
+        // different products and their results differed in the last bit
+        c[mt][r] = fmaf(fg, c[mt][r], __fmul_rn(ig, cg));
         hr[mt][r] = og * tnh(c[mt][r]);
       }
       if (out)
@@ -419,8 +428,8 @@ __global__ __launch_bounds__(256) void lstm_group_bf16_kernel(
   if (bad && host_err && tid == 0) __hip_atomic_store(host_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const float qnan = __int_as_float(0x7fc00000);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int b = b0 + mt * 16 + l15;
+  for (int mt = 0; mt < MTW; ++mt) {
+    const int b = rb(mt);
     if (b >= B) continue;
     if (bad) {
 #pragma unroll
@@ -553,19 +562,19 @@ unsigned lstm_spin_limit() {
   return launches++ < n_forced ? v : (1u << 22);
 }
 
-template <int MT, bool GR>
+template <int MT, bool GR, int WV = 4>
 void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                          const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                          uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, GR>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, GR, WV>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, GR>), dim3(4 * groups), dim3(256), smem, st, gx, B, T, ndir,
+  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, GR, WV>), dim3(4 * groups), dim3(64 * WV), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
                      counters, err, lstm_spin_limit(), host_err);
   SD_LAUNCH_CHECK();
@@ -576,34 +585,54 @@ bool lstm_granule_mode() {
   return v;
 }
 
+// Workgroups of lstm_group_bf16_kernel<MT, false, WV> the occupancy query admits per CU (0 if none fit).
+// This is the check hipLaunchCooperativeKernel would make (MI355X guide, "Residency and
+// cooperative launch": a plain launch of the same grid has the same residency); a cooperative
+// launch itself is avoided because its queue's teardown crashes rocprofv3's exit path here.
+template <int MT, int WV = 4>
+int lstm_group_blocks_per_cu() {
+  static int nb = -1;
+  if (nb < 0) {
+    const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, false, WV>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    int v = 0;
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, false, WV>, 64 * WV, smem));
+    nb = v;
+  }
+  return nb;
+}
+
+// 8 waves per workgroup (the default; SDIAR_LSTM_WV=4 keeps 4): only for an even row-tile count and the counter
+// exchange, and only when the occupancy query admits the 512-thread workgroup.  C2 (600 windows x 2 directions,
+// 2 row tiles per group): recurrence 929 -> 777 us per launch (tools/gpu_r05y.sh).
+template <int MT>
+bool lstm_group_wv8() {
+  if constexpr (MT % 2 != 0) {
+    return false;
+  } else {
+    static const int wv = getenv("SDIAR_LSTM_WV") ? atoi(getenv("SDIAR_LSTM_WV")) : 8;
+    return wv == 8 && !lstm_granule_mode() && lstm_group_blocks_per_cu<MT, 8>() >= 1;
+  }
+}
+
 template <int MT>
 void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                        const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                        uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
+  if constexpr (MT % 2 == 0) {
+    if (lstm_group_wv8<MT>()) {
+      launch_lstm_group_t<MT, false, 8>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters,
+                                        err, host_err, st);
+      return;
+    }
+  }
   if (lstm_granule_mode())
     launch_lstm_group_t<MT, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err,
                                   host_err, st);
   else
     launch_lstm_group_t<MT, false>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err,
                                    host_err, st);
-}
-
-// Workgroups of lstm_group_bf16_kernel<MT> the occupancy query admits per CU (0 if none fit).
-// This is the check hipLaunchCooperativeKernel would make (MI355X guide, "Residency and
-// cooperative launch": a plain launch of the same grid has the same residency); a cooperative
-// launch itself is avoided because its queue's teardown crashes rocprofv3's exit path here.
-template <int MT>
-int lstm_group_blocks_per_cu() {
-  static int nb = -1;
-  if (nb < 0) {
-    const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    int v = 0;
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT>, 256, smem));
-    nb = v;
-  }
-  return nb;
 }
 
 int lstm_group_capacity(int mt) {

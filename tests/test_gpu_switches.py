@@ -184,7 +184,7 @@ def test_cam_two_stream_slices_bit_identical(gpu):
 def _tsvad_hash(extra_env):
     env = dict(os.environ)
     for k in ("SDIAR_MHA_SEQ2", "SDIAR_SLICES", "SDIAR_LSTM_GRANULE", "SDIAR_NO_DWCONV_PP", "SDIAR_RP_ROWMAJOR_X",
-              "SDIAR_RP_ROWMAJOR_A", "SDIAR_RP_ROWMAJOR_Y"):
+              "SDIAR_RP_ROWMAJOR_A", "SDIAR_RP_ROWMAJOR_Y", "SDIAR_LSTM_MT", "SDIAR_LSTM_WV"):
         env.pop(k, None)
     env.update(extra_env)
     r = subprocess.run([sys.executable, "-c", TSVAD_BITS_CHILD.format(repo=REPO)], capture_output=True,
@@ -196,9 +196,11 @@ def _tsvad_hash(extra_env):
 
 @pytest.mark.parametrize("switch", [{"SDIAR_MHA_SEQ2": "1"}, {"SDIAR_SLICES": "3"}, {"SDIAR_SLICES": "4"},
                                     {"SDIAR_LSTM_GRANULE": "1"}, {"SDIAR_NO_DWCONV_PP": "1"}, {"SDIAR_RP_ROWMAJOR_X": "1"},
-                                    {"SDIAR_RP_ROWMAJOR_A": "1"}, {"SDIAR_RP_ROWMAJOR_Y": "1"}],
+                                    {"SDIAR_RP_ROWMAJOR_A": "1"}, {"SDIAR_RP_ROWMAJOR_Y": "1"}, {"SDIAR_LSTM_MT": "2"},
+                                    {"SDIAR_LSTM_MT": "2", "SDIAR_LSTM_WV": "4"},
+                                    {"SDIAR_LSTM_MT": "2", "SDIAR_LSTM_WV": "8"}, {"SDIAR_LSTM_MT": "4", "SDIAR_LSTM_WV": "8"}],
                          ids=["mha_seq2", "slices3", "slices4", "lstm_granule", "dwconv_pp", "rowmajor_x", "rowmajor_a",
-                              "rowmajor_y"])
+                              "rowmajor_y", "lstm_mt2", "lstm_mt2_wv4", "lstm_wv8_mt2", "lstm_wv8_mt4"])
 def test_schedule_switches_bit_identical(gpu, switch):
     """Switches that change only the schedule or the transport, never the arithmetic, must leave the TS-VAD
     logits (ots_vad v1 with its BiLSTM, and the CAM++/transformer model; 400 windows: two-stream slices) bit
@@ -206,5 +208,6 @@ def test_schedule_switches_bit_identical(gpu, switch):
     conformer stack i) vs the default two; the BiLSTM's h exchange on tagged 8-byte granules vs the counter; the
     persistent depthwise conv (next sequence's rows in flight) vs one workgroup per (sequence, 64 channels); the
     row programs' residual stream in the MFMA-tiled layout vs row-major; the attention output handed to the
-    out-projection program tiled vs row-major; the attention LayerNorm rows handed to mha_block tiled vs row-major."""
+    out-projection program tiled vs row-major; the attention LayerNorm rows handed to mha_block tiled vs row-major;
+    the BiLSTM at 2 / 4 row tiles per group, on 4 waves per workgroup or 8 (two waves per unit tile)."""
     assert _tsvad_hash(switch) == _tsvad_hash({})
