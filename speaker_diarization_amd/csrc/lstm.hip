@@ -215,9 +215,9 @@ constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (25
 // lstm_granule_probe_kernel -- a lane publishes its 4 units as two 8-byte {bf16 x 2, tag} granules in one 16-B
 // sc1 store, every wave polls exactly the granules of its next MFMA operand until they carry the step's tag; no
 // counter, no barrier, no vmcnt(0) drain in the step loop.  hx then holds [parity][d][Bp][H / 2] granules.
-// WV (round 5, default for an even MT): 8 waves per workgroup instead of 4 -- two waves per 16-unit tile, each on half of
-// the group's row tiles (tile j * 2 + (w >> 2)), so every SIMD holds two waves of the step and one's gx loads,
-// transcendentals and stores overlap the other's MFMAs; the W slice, the counters and the exchange are unchanged.
+// WV (round 5, default for an even MT): 8 waves per workgroup instead of 4 -- two waves per 16-unit tile, each
+// on half of the group's row tiles (tile j * 2 + (wave >> 2)), so every SIMD holds two waves of the step and one's
+// gx loads, transcendentals and stores overlap the other's MFMAs; W slice, counters and exchange are unchanged.
 template <int MT, bool GR = false, int WV = 4>
 __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
