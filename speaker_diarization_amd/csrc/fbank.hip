@@ -13,6 +13,8 @@
 // contiguous slice of the meeting's frames and window_cmn() only subtracts the
 // per-window mean.  That removes the 6x frame recomputation of overlapping
 // 6 s / 1 s-shift windows.
+#include <algorithm>
+#include <cstdlib>
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -26,6 +28,7 @@ constexpr int kNfft = 512;
 constexpr int kBins = kNfft / 2 + 1;
 constexpr int kFramesPerBlock = 8;
 constexpr int kMaxFbMels = 128;
+constexpr int kMelCap = 2 * kBins + 2 * kMaxFbMels;   // triangular banks: each bin in at most two filters
 
 __device__ __forceinline__ int bitrev9(int x) { return __brev((unsigned)x) >> (32 - 9); }
 __device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses (no workgroup barrier)
@@ -36,8 +39,8 @@ __device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses
 
 // One wave per frame, 8 frames per workgroup.  Built once per workgroup in LDS: the twiddles, the
 // window (the same cospif / powf values the per-sample form computed) and each mel filter's nonzero bin
-// range, so the projection runs over a filter's ~10 bins instead of all 257 (the skipped terms are exact
-// zeros: same sums, same order).  A frame's FFT stages belong to its wave alone: wave barriers only.
+// range and values, so the projection runs over a filter's ~10 bins instead of all 257 (the skipped terms
+// are exact zeros: same sums, same order).  A frame's FFT stages belong to its wave alone: wave barriers only.
 __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                     float in_scale, int n_frames,
                                                     const float* __restrict__ mel_fb, int n_mels,
@@ -50,12 +53,10 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
   __shared__ float pw[kFramesPerBlock][kBins + 3];
   __shared__ float2 tw[kNfft / 2];
   __shared__ float win[kFrameLen];
-  __shared__ int mlo[kMaxFbMels], mhi[kMaxFbMels];
+  __shared__ int mlo[kMaxFbMels], mhi[kMaxFbMels], moff[kMaxFbMels + 1];
+  __shared__ float melv[kMelCap];   // every filter's nonzero run, packed (moff[m] = its start)
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int f = blockIdx.x * kFramesPerBlock + w;
-  const bool active = f < n_frames;
-  const float* x = wav + (int64_t)(active ? f : 0) * kShift;
 
   for (int k = threadIdx.x; k < kNfft / 2; k += blockDim.x) tw[k] = twiddle[k];
   for (int n = threadIdx.x; n < kFrameLen; n += blockDim.x) {
@@ -76,73 +77,107 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
       atomicMax(&mhi[m], k + 1);
     }
   }
+  __syncthreads();   // mel ranges
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int m = 0; m < n_mels; ++m) {
+      moff[m] = o;
+      o += max(mhi[m] - mlo[m], 0);
+    }
+    moff[n_mels] = o;
+  }
+  __syncthreads();
+  // the filters' runs in LDS (the projection read them from global memory, one dependent load per bin: most of
+  // the kernel's time); a mel matrix with more nonzero runs than kMelCap keeps the global reads
+  const bool lds_mel = moff[n_mels] <= kMelCap;
+  if (lds_mel)
+    for (int i = threadIdx.x; i < n_mels * kBins; i += blockDim.x) {
+      const int m = i / kBins, k = i - m * kBins;
+      if (k >= mlo[m] && k < mhi[m]) melv[moff[m] + k - mlo[m]] = mel_fb[i];
+    }
+  __syncthreads();   // window table, twiddles, mel runs
 
-  // Load, DC removal.
-  float v[7];
-  float s = 0.f;
+  // The workgroup walks frame groups blockIdx.x, + gridDim.x, ...: the tables above (a 20 k-entry scan of the
+  // mel matrix) are built once per workgroup instead of once per 8 frames.
+  const int n_groups = (n_frames + kFramesPerBlock - 1) / kFramesPerBlock;
+  for (int fg = blockIdx.x; fg < n_groups; fg += gridDim.x) {
+    const int f = fg * kFramesPerBlock + w;
+    const bool active = f < n_frames;
+    const float* x = wav + (int64_t)(active ? f : 0) * kShift;
+    // Load, DC removal.
+    float v[7];
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    int n = lane + i * 64;
-    int64_t gi = (int64_t)(active ? f : 0) * kShift + n;
-    v[i] = (n < kFrameLen && gi < n_samples) ? x[n] * in_scale : 0.f;
-    s += v[i];
-  }
-  s = warp_sum(s);
-  const float mean = s / (float)kFrameLen;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    int n = lane + i * 64;
-    if (n < kFrameLen) buf[w][pz(n)].x = v[i] - mean;   // scratch (real part)
-  }
-  __syncthreads();   // window table, mel ranges, this frame's scratch
-  // Pre-emphasis + window, written bit-reversed for the DIT FFT.
-  float y[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    int n = lane + i * 64;
-    float val = 0.f;
-    if (n < kFrameLen) {
-      float cur = buf[w][pz(n)].x;
-      float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
-      val = (cur - 0.97f * prev) * win[n];
+    for (int i = 0; i < 7; ++i) {
+      int n = lane + i * 64;
+      int64_t gi = (int64_t)(active ? f : 0) * kShift + n;
+      v[i] = (n < kFrameLen && gi < n_samples) ? x[n] * in_scale : 0.f;
+      s += v[i];
     }
-    y[i] = val;
-  }
-  wave_sync();
+    s = warp_sum(s);
+    const float mean = s / (float)kFrameLen;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    int n = lane + i * 64;
-    buf[w][pz(bitrev9(n))] = make_float2(y[i], 0.f);
-  }
-  // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
-  for (int half = 1; half < kNfft; half <<= 1) {
+    for (int i = 0; i < 7; ++i) {
+      int n = lane + i * 64;
+      if (n < kFrameLen) buf[w][pz(n)].x = v[i] - mean;   // scratch (real part)
+    }
+    wave_sync();   // this frame's scratch
+    // Pre-emphasis + window, written bit-reversed for the DIT FFT.
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int n = lane + i * 64;
+      float val = 0.f;
+      if (n < kFrameLen) {
+        float cur = buf[w][pz(n)].x;
+        float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
+        val = (cur - 0.97f * prev) * win[n];
+      }
+      y[i] = val;
+    }
     wave_sync();
-    const int tstride = kNfft / (2 * half);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int bfly = lane + i * 64;
-      int grp = bfly / half, pos = bfly % half;
-      int i0 = grp * 2 * half + pos, i1 = i0 + half;
-      float2 t0 = tw[pos * tstride];
-      float2 a = buf[w][pz(i0)], b = buf[w][pz(i1)];
-      float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
-      buf[w][pz(i0)] = make_float2(a.x + t.x, a.y + t.y);
-      buf[w][pz(i1)] = make_float2(a.x - t.x, a.y - t.y);
+    for (int i = 0; i < 8; ++i) {
+      int n = lane + i * 64;
+      buf[w][pz(bitrev9(n))] = make_float2(y[i], 0.f);
     }
-  }
-  wave_sync();
-  for (int k = lane; k < kBins; k += 64) {
-    float2 c = buf[w][pz(k)];
-    pw[w][k] = c.x * c.x + c.y * c.y;
-  }
-  wave_sync();
-  if (!active) return;
-  const float eps = 1.1920928955078125e-07f;
-  for (int m = lane; m < n_mels; m += 64) {
-    const float* fr = mel_fb + (int64_t)m * kBins;
-    float acc = 0.f;
-    for (int k = mlo[m]; k < mhi[m]; ++k) acc = fmaf(fr[k], pw[w][k], acc);
-    out[(int64_t)f * n_mels + m] = logf(fmaxf(acc, eps));
+    // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
+    for (int half = 1; half < kNfft; half <<= 1) {
+      wave_sync();
+      const int tstride = kNfft / (2 * half);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int bfly = lane + i * 64;
+        int grp = bfly / half, pos = bfly % half;
+        int i0 = grp * 2 * half + pos, i1 = i0 + half;
+        float2 t0 = tw[pos * tstride];
+        float2 a = buf[w][pz(i0)], b = buf[w][pz(i1)];
+        float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
+        buf[w][pz(i0)] = make_float2(a.x + t.x, a.y + t.y);
+        buf[w][pz(i1)] = make_float2(a.x - t.x, a.y - t.y);
+      }
+    }
+    wave_sync();
+    for (int k = lane; k < kBins; k += 64) {
+      float2 c = buf[w][pz(k)];
+      pw[w][k] = c.x * c.x + c.y * c.y;
+    }
+    wave_sync();
+    if (active) {
+      const float eps = 1.1920928955078125e-07f;
+      for (int m = lane; m < n_mels; m += 64) {
+        float acc = 0.f;
+        if (lds_mel) {
+          const int lo = mlo[m], base = moff[m];
+          for (int k = lo; k < mhi[m]; ++k) acc = fmaf(melv[base + (k - lo)], pw[w][k], acc);
+        } else {
+          const float* fr = mel_fb + (int64_t)m * kBins;
+          for (int k = mlo[m]; k < mhi[m]; ++k) acc = fmaf(fr[k], pw[w][k], acc);
+        }
+        out[(int64_t)f * n_mels + m] = logf(fmaxf(acc, eps));
+      }
+    }
+    wave_sync();   // the next frame group rewrites buf[w] / pw[w]
   }
 }
 
@@ -165,7 +200,19 @@ void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fram
   if (n_frames <= 0) return;
   ProfScope prof("fbank_kaldi", 0.0, 4.0 * ((double)n_frames * kShift + (double)n_frames * n_mels), st);
   SD_CHECK(n_mels > 0 && n_mels <= kMaxFbMels, kErrInvalid, "fbank: n_mels out of range");
-  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(n_frames, kFramesPerBlock)), dim3(512), 0, st, wav,
+  // as many workgroups as are resident at once (each builds its tables once and walks frame groups);
+  // SDIAR_FBANK_PER_GROUP=1 (A/B): one workgroup per 8-frame group, i.e. the tables rebuilt per group
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 0, per_cu = 0;
+    SD_HIP(hipGetDevice(&dev));
+    SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel, 512, 0));
+    slots = std::max(1, cus * std::max(1, per_cu));
+  }
+  static const bool per_group = getenv("SDIAR_FBANK_PER_GROUP") != nullptr;
+  const int groups = cdiv(n_frames, kFramesPerBlock);
+  hipLaunchKernelGGL(fbank_kernel, dim3(per_group ? groups : std::min(groups, slots)), dim3(512), 0, st, wav,
                      n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, window, out);
   SD_LAUNCH_CHECK();
 }
