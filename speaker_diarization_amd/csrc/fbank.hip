@@ -41,6 +41,7 @@ __device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses
 // window (the same cospif / powf values the per-sample form computed) and each mel filter's nonzero bin
 // range and values, so the projection runs over a filter's ~10 bins instead of all 257 (the skipped terms
 // are exact zeros: same sums, same order).  A frame's FFT stages belong to its wave alone: wave barriers only.
+template <bool REG>
 __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                     float in_scale, int n_frames,
                                                     const float* __restrict__ mel_fb, int n_mels,
@@ -100,10 +101,23 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
   // The workgroup walks frame groups blockIdx.x, + gridDim.x, ...: the tables above (a 20 k-entry scan of the
   // mel matrix) are built once per workgroup instead of once per 8 frames.
   const int n_groups = (n_frames + kFramesPerBlock - 1) / kFramesPerBlock;
-  for (int fg = blockIdx.x; fg < n_groups; fg += gridDim.x) {
+  // a frame group's samples are requested one group ahead (in flight during the previous group's FFT)
+  float xr[7];
+  auto load_x = [&](int fg) {
     const int f = fg * kFramesPerBlock + w;
     const bool active = f < n_frames;
     const float* x = wav + (int64_t)(active ? f : 0) * kShift;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      int n = lane + i * 64;
+      int64_t gi = (int64_t)(active ? f : 0) * kShift + n;
+      xr[i] = (fg < n_groups && n < kFrameLen && gi < n_samples) ? x[n] : 0.f;
+    }
+  };
+  load_x(blockIdx.x);
+  for (int fg = blockIdx.x; fg < n_groups; fg += gridDim.x) {
+    const int f = fg * kFramesPerBlock + w;
+    const bool active = f < n_frames;
     // Load, DC removal.
     float v[7];
     float s = 0.f;
@@ -111,9 +125,10 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
     for (int i = 0; i < 7; ++i) {
       int n = lane + i * 64;
       int64_t gi = (int64_t)(active ? f : 0) * kShift + n;
-      v[i] = (n < kFrameLen && gi < n_samples) ? x[n] * in_scale : 0.f;
+      v[i] = (n < kFrameLen && gi < n_samples) ? xr[i] * in_scale : 0.f;
       s += v[i];
     }
+    load_x(fg + gridDim.x);
     s = warp_sum(s);
     const float mean = s / (float)kFrameLen;
 #pragma unroll
@@ -122,45 +137,103 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
       if (n < kFrameLen) buf[w][pz(n)].x = v[i] - mean;   // scratch (real part)
     }
     wave_sync();   // this frame's scratch
-    // Pre-emphasis + window, written bit-reversed for the DIT FFT.
-    float y[8];
+    if constexpr (REG) {
+      // Radix-2 DIT in three register passes of three stages each, the wave's LDS only for the two
+      // transposes between them (the per-stage form below moved every element through LDS nine times).
+      // Same butterflies, same twiddles, same order per element.
+      // pass A: bit-reversed positions 8 lane + k (sample bitrev3(k) * 64 + bitrev6(lane)), stages 1, 2, 4
+      float2 X[8];
+      const int r6 = (int)(__brev((unsigned)lane) >> 26);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int n = lane + i * 64;
-      float val = 0.f;
-      if (n < kFrameLen) {
-        float cur = buf[w][pz(n)].x;
-        float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
-        val = (cur - 0.97f * prev) * win[n];
+      for (int k = 0; k < 8; ++k) {
+        const int n = (int)(__brev((unsigned)k) >> 29) * 64 + r6;
+        float val = 0.f;
+        if (n < kFrameLen) {
+          float cur = buf[w][pz(n)].x;
+          float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
+          val = (cur - 0.97f * prev) * win[n];
+        }
+        X[k] = make_float2(val, 0.f);
       }
-      y[i] = val;
-    }
-    wave_sync();
+      auto bfly = [](float2& a, float2& b, float2 t0) {
+        const float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
+        const float2 a0 = a;
+        a = make_float2(a0.x + t.x, a0.y + t.y);
+        b = make_float2(a0.x - t.x, a0.y - t.y);
+      };
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int n = lane + i * 64;
-      buf[w][pz(bitrev9(n))] = make_float2(y[i], 0.f);
-    }
-    // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
-    for (int half = 1; half < kNfft; half <<= 1) {
+      for (int half = 1; half < 8; half <<= 1)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (!(k & half)) bfly(X[k], X[k + half], tw[(k & (half - 1)) * (kNfft / 2 / half)]);
+      wave_sync();   // every lane's pre-emphasis reads of the scratch are done
+#pragma unroll
+      for (int k = 0; k < 8; ++k) buf[w][pz(8 * lane + k)] = X[k];
       wave_sync();
-      const int tstride = kNfft / (2 * half);
+      // pass B: positions 64 b + r + 8 m (lane = 8 b + r), stages 8, 16, 32
+      const int pb = 64 * (lane >> 3) + (lane & 7);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int bfly = lane + i * 64;
-        int grp = bfly / half, pos = bfly % half;
-        int i0 = grp * 2 * half + pos, i1 = i0 + half;
-        float2 t0 = tw[pos * tstride];
-        float2 a = buf[w][pz(i0)], b = buf[w][pz(i1)];
-        float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
-        buf[w][pz(i0)] = make_float2(a.x + t.x, a.y + t.y);
-        buf[w][pz(i1)] = make_float2(a.x - t.x, a.y - t.y);
+      for (int m = 0; m < 8; ++m) X[m] = buf[w][pz(pb + 8 * m)];
+#pragma unroll
+      for (int h = 1; h < 8; h <<= 1)   // half = 8 h
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          if (!(m & h)) bfly(X[m], X[m + h], tw[((lane & 7) + 8 * m) % (8 * h) * (kNfft / 16 / h)]);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) buf[w][pz(pb + 8 * m)] = X[m];
+      wave_sync();
+      // pass C: positions lane + 64 m, stages 64, 128, 256
+#pragma unroll
+      for (int m = 0; m < 8; ++m) X[m] = buf[w][pz(lane + 64 * m)];
+#pragma unroll
+      for (int h = 1; h < 8; h <<= 1)   // half = 64 h
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          if (!(m & h)) bfly(X[m], X[m + h], tw[(lane + 64 * m) % (64 * h) * (kNfft / 128 / h)]);
+#pragma unroll
+      for (int m = 0; m < 5; ++m)
+        if (lane + 64 * m < kBins) pw[w][lane + 64 * m] = X[m].x * X[m].x + X[m].y * X[m].y;
+    } else {
+      // Pre-emphasis + window, written bit-reversed for the DIT FFT.
+      float y[8];
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        int n = lane + i * 64;
+        float val = 0.f;
+        if (n < kFrameLen) {
+          float cur = buf[w][pz(n)].x;
+          float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
+          val = (cur - 0.97f * prev) * win[n];
+        }
+        y[i] = val;
       }
-    }
-    wave_sync();
-    for (int k = lane; k < kBins; k += 64) {
-      float2 c = buf[w][pz(k)];
-      pw[w][k] = c.x * c.x + c.y * c.y;
+      wave_sync();
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        int n = lane + i * 64;
+        buf[w][pz(bitrev9(n))] = make_float2(y[i], 0.f);
+      }
+      // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
+      for (int half = 1; half < kNfft; half <<= 1) {
+        wave_sync();
+        const int tstride = kNfft / (2 * half);
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int bfly = lane + i * 64;
+          int grp = bfly / half, pos = bfly % half;
+          int i0 = grp * 2 * half + pos, i1 = i0 + half;
+          float2 t0 = tw[pos * tstride];
+          float2 a = buf[w][pz(i0)], b = buf[w][pz(i1)];
+          float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
+          buf[w][pz(i0)] = make_float2(a.x + t.x, a.y + t.y);
+          buf[w][pz(i1)] = make_float2(a.x - t.x, a.y - t.y);
+        }
+      }
+      wave_sync();
+      for (int k = lane; k < kBins; k += 64) {
+        float2 c = buf[w][pz(k)];
+        pw[w][k] = c.x * c.x + c.y * c.y;
+      }
     }
     wave_sync();
     if (active) {
@@ -207,13 +280,19 @@ void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fram
     int dev = 0, cus = 0, per_cu = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel, 512, 0));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel<true>, 512, 0));
     slots = std::max(1, cus * std::max(1, per_cu));
   }
   static const bool per_group = getenv("SDIAR_FBANK_PER_GROUP") != nullptr;
+  static const bool lds_fft = getenv("SDIAR_FBANK_LDS_FFT") != nullptr;   // A/B: the nine-stage LDS FFT
   const int groups = cdiv(n_frames, kFramesPerBlock);
-  hipLaunchKernelGGL(fbank_kernel, dim3(per_group ? groups : std::min(groups, slots)), dim3(512), 0, st, wav,
-                     n_samples, in_scale, n_frames, mel_fb, n_mels, g_twiddle, window, out);
+  const dim3 grid(per_group ? groups : std::min(groups, slots));
+  if (lds_fft)
+    hipLaunchKernelGGL(fbank_kernel<false>, grid, dim3(512), 0, st, wav, n_samples, in_scale, n_frames, mel_fb,
+                       n_mels, g_twiddle, window, out);
+  else
+    hipLaunchKernelGGL(fbank_kernel<true>, grid, dim3(512), 0, st, wav, n_samples, in_scale, n_frames, mel_fb,
+                       n_mels, g_twiddle, window, out);
   SD_LAUNCH_CHECK();
 }
 
