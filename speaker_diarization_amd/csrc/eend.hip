@@ -74,11 +74,17 @@ __global__ __launch_bounds__(FPB * 64) void stft_logmel_kernel(const float* __re
     n_samples = min(n_samples, (int64_t)bound[0]);
   }
   const int64_t base = fg * hop - N / 2 + lpad;
+  // REG (whole-recording 512-point frames): the FFT as three register passes of three radix-2 stages with two LDS
+  // transposes (the per-stage form moves every element through LDS nine times); same butterflies, same twiddles.
+  // The lane then holds samples r6 + 64 u (r6 = bitrev6(lane)): its pass-A positions 8 lane + k are samples
+  // bitrev3(k) * 64 + r6.
+  constexpr bool REG = LOG2N == 9 && !STREAM;
+  const int r6 = (int)(__brev((unsigned)lane) >> 26);
   // the frame's samples, in flight during the table prologue (clamped loads, masked after)
   float raw[N / 64];
 #pragma unroll
   for (int u = 0; u < N / 64; ++u) {
-    const int64_t gi = base + (lane + 64 * u) - lpad;
+    const int64_t gi = base + ((REG ? r6 : lane) + 64 * u) - lpad;
     raw[u] = cap > 0 ? wav[min(max(gi, (int64_t)0), cap - 1)] : 0.f;
   }
   for (int k = threadIdx.x; k < N / 2; k += blockDim.x) {
@@ -116,6 +122,59 @@ __global__ __launch_bounds__(FPB * 64) void stft_logmel_kernel(const float* __re
     }
   }
   __syncthreads();   // window table, filter ranges
+  if constexpr (REG) {
+    auto bfly = [](double2& a, double2& b, double2 t0) {
+      const double2 t = make_double2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
+      const double2 a0 = a;
+      a = make_double2(a0.x + t.x, a0.y + t.y);
+      b = make_double2(a0.x - t.x, a0.y - t.y);
+    };
+    double2 X[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // pass A positions 8 lane + k
+      const int u = (int)(__brev((unsigned)k) >> 29);
+      const int n = r6 + 64 * u;
+      double v = 0.0;
+      const int j = n - lpad;
+      if (active && j >= 0 && j < win_len) {
+        const int64_t gi = base + j;
+        if (gi >= 0 && gi < n_samples) v = (double)raw[u] * win[j];
+      }
+      X[k] = make_double2(v, 0.0);
+    }
+#pragma unroll
+    for (int half = 1; half < 8; half <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!(k & half)) bfly(X[k], X[k + half], tw[(k & (half - 1)) * (N / 2 / half)]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) buf[w][pz(8 * lane + k)] = X[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int pb = 64 * (lane >> 3) + (lane & 7);   // pass B: positions 64 b + r + 8 m (lane = 8 b + r)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) X[m] = buf[w][pz(pb + 8 * m)];
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)   // half = 8 h
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        if (!(m & h)) bfly(X[m], X[m + h], tw[((lane & 7) + 8 * m) % (8 * h) * (N / 16 / h)]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) buf[w][pz(pb + 8 * m)] = X[m];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int m = 0; m < 8; ++m) X[m] = buf[w][pz(lane + 64 * m)];   // pass C: positions lane + 64 m
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)   // half = 64 h
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        if (!(m & h)) bfly(X[m], X[m + h], tw[(lane + 64 * m) % (64 * h) * (N / 128 / h)]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) buf[w][pz(lane + 64 * m)] = X[m];
+  } else {
 #pragma unroll
   for (int u = 0; u < N / 64; ++u) {
     const int n = lane + 64 * u;
@@ -143,6 +202,7 @@ __global__ __launch_bounds__(FPB * 64) void stft_logmel_kernel(const float* __re
       buf[w][pz(i1)] = make_double2(a.x - t.x, a.y - t.y);
     }
   }
+  }   // REG
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
