@@ -452,8 +452,8 @@ def cpu_baseline(cfg, sd_np, meeting, ts, budget_s):
                 **info), post["p"], n
 
 
-def spread_posteriors(job, a, dev, sd_np, precision):
-    """The job's meeting through a second model holding the spread weight variant (numpy posteriors)."""
+def variant_posteriors(job, a, dev, sd_np, precision):
+    """The job's meeting through a second model holding a weight variant (numpy posteriors)."""
     import torch
     from speaker_diarization_amd.ts_vad.model import TSVADModel
     from speaker_diarization_amd.ts_vad.pipeline import TSVADPipeline
@@ -468,27 +468,29 @@ def spread_posteriors(job, a, dev, sd_np, precision):
     return out
 
 
-def spread_der(job, a, dev, meeting, n_win):
-    """DER parity that can fail (round-4 verdict item 4): the same span on the 'spread' weight variant
-    (weights.py spread_fc: only fc rescaled per track, so the posteriors cross every recipe threshold), GPU fp32
-    and GPU in the line's precision against the fp32 CPU oracle.  The rescale multiplies the bf16 logit error by
-    k = 8 / std ~ 120-240 along with the logits: the bf16 figures there measure that sensitivity."""
+def variant_der(job, a, dev, meeting, n_win):
+    """DER parity that can fail (round-5 verdict item 1): the same span on the 'dynamic' weight variant
+    (weights.py dynamic_weights: gsp_fc and the BiLSTM input centred and scaled upstream, fc x4, so the
+    activations move with the frame and 99 % of the posteriors sit in [0.2, 0.8]), GPU fp32 and GPU in the
+    line's precision against the fp32 CPU oracle.  fp32 is the gate; on this variant bf16 as a number format
+    moves the DER by more than 0.1 whichever stage computes in it (tests/bf16_der_emulation.py),
+    so the bf16 figures measure that, not a kernel difference."""
     import torch
     from oracle.pipeline_ref import meeting_posteriors
     from speaker_diarization_amd.weights import to_torch, tsvad_state_dict
-    sd = tsvad_state_dict(job["cfg"], seed=777, spread=True)
+    sd = tsvad_state_dict(job["cfg"], seed=777, dynamic=True)
     torch.set_num_threads(host_threads())
     cpu_post = meeting_posteriors(to_torch(sd), job["cfg"], meeting.wav, job["ts_np"], job["n_lab"], shift=1,
                                   batch_size=min(64, n_win), max_windows=n_win)
     out = {}
     for prec in ("fp32", a.precision):
-        g = spread_posteriors(job, a, dev, sd, prec)
+        g = variant_posteriors(job, a, dev, sd, prec)
         d = der_parity(meeting, g, cpu_post, float(n_win))
         d.pop("note", None)
         d["posterior_parity"] = posterior_parity(g, cpu_post, n_win * 25)
         out[prec] = d
     out["note"] = ("fp32 is the gate (|dDER| <= 0.1 at every threshold on a non-degenerate table); bf16 on this "
-                   "variant is the rescaled sensitivity, not parity")
+                   "variant measures the number format's effect (tests/bf16_der_emulation.py), not parity")
     return out
 
 
@@ -619,7 +621,7 @@ def main(a, wl):
         cpu, cpu_post, n_cpu = cpu_baseline(job["cfg"], job["sd_np"], meeting, job["ts_np"], a.cpu_seconds)
         der = der_parity(meeting, post, cpu_post, float(n_cpu))
         parity = posterior_parity(post.cpu().numpy(), cpu_post, n_cpu * 25)
-        der["spread"] = spread_der(job, a, dev, meeting, n_cpu)
+        der["dynamic"] = variant_der(job, a, dev, meeting, n_cpu)
     c4 = None
     if world == 1 and a.workload == "c2" and not a.no_c4_ref:
         c4 = c4_reference(a, dev)

@@ -264,16 +264,72 @@ def synthetic_state_dict(layout: list, seed: int = 777, extras: Dict[str, np.nda
     return sd
 
 
-def tsvad_state_dict(cfg: TSVADConfig, seed: int = 777, spread: bool = False):
-    """Seeded weights of the reference layout.  spread: the 'spread' variant (tools/calibrate_spread.py) whose
+def tsvad_state_dict(cfg: TSVADConfig, seed: int = 777, spread: bool = False, dynamic: bool = False):
+    """Seeded weights of the reference layout.  spread: the 'spread' variant (tests/golden/calibrate_spread.py) whose
     final Linear is rescaled per track so the posteriors of the bench meeting cover the recipe thresholds
-    (a DER comparison that can fail) instead of sitting on a near-constant plateau."""
+    (a DER comparison that can fail) instead of sitting on a near-constant plateau.  dynamic: the 'dynamic'
+    variant (tests/golden/calibrate_dynamic.py): two upstream layers centred and scaled so the activations vary with
+    the frame, fc at a gain of DYN_FC_GAIN."""
     sd = synthetic_state_dict(tsvad_layout(cfg), seed)
+    if spread and dynamic:
+        raise ValueError("spread and dynamic are two different variants")
+    if dynamic:
+        if seed != 777:
+            raise ValueError("the dynamic variant is calibrated for seed 777")
+        return dynamic_weights(sd, cfg, dynamic_calibration())
     return spread_fc(sd, cfg, seed) if spread else sd
 
 
+# 'dynamic' variant gains (tests/golden/calibrate_dynamic.py): the GSP statistic enters the conformer at unit variance
+# (G_GSP), the BiLSTM gates swing G_IH times further around their operating point, fc is scaled by <= 4.
+DYN_G_GSP = 1.0
+DYN_G_IH = 8.0
+DYN_FC_GAIN = 4.0
+_DYN_CACHE: dict = {}
+
+
+def dynamic_calibration() -> Dict[str, np.ndarray]:
+    """The oracle statistics tests/golden/calibrate_dynamic.py measured on the bench meeting (seed 777, first 48
+    windows): weights_dynamic.npz next to this file (data, no code)."""
+    if not _DYN_CACHE:
+        import os
+        with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "weights_dynamic.npz")) as z:
+            _DYN_CACHE.update({k: np.asarray(z[k], np.float64) for k in z.files})
+    return _DYN_CACHE
+
+
+def dynamic_weights(sd, cfg: TSVADConfig, c: Dict[str, np.ndarray], stage: int = 3):
+    """Apply the dynamic variant's gains (stage < 3: the partial variants the calibration measures on)."""
+    out = OrderedDict(sd)
+    f64 = lambda k: np.asarray(sd[k], np.float64)   # noqa: E731
+    if cfg.variant == 1:
+        if cfg.rs_len != 6:
+            raise ValueError("the dynamic variant is calibrated for ots_vad v1 at rs_len 6")
+        mu, sg = c["v1_stat_mean"], c["v1_stat_std"]
+        w = f64("gsp_fc.weight")
+        out["gsp_fc.weight"] = (w * (DYN_G_GSP / sg)[None, :]).astype(np.float32)
+        out["gsp_fc.bias"] = (f64("gsp_fc.bias") - w @ (DYN_G_GSP * mu / sg)).astype(np.float32)
+        if stage >= 2:
+            xbar = c["v1_conformer_mean"]
+            for sfx in ("", "_reverse"):
+                wih = f64(f"multi_backend.weight_ih_l0{sfx}")
+                out[f"multi_backend.weight_ih_l0{sfx}"] = (wih * DYN_G_IH).astype(np.float32)
+                out[f"multi_backend.bias_ih_l0{sfx}"] = (f64(f"multi_backend.bias_ih_l0{sfx}")
+                                                        - (DYN_G_IH - 1.0) * (wih @ xbar)).astype(np.float32)
+        if stage < 3:
+            return out
+        mean = c["v1_logit_mean"]
+    else:
+        if cfg.rs_len != 4:
+            raise ValueError("the dynamic variant is calibrated for the CAM++/transformer model at rs_len 4")
+        mean = c["v0_logit_mean"]
+    out["fc.weight"] = (f64("fc.weight") * DYN_FC_GAIN).astype(np.float32)
+    out["fc.bias"] = (DYN_FC_GAIN * (f64("fc.bias") - mean)).astype(np.float32)
+    return out
+
+
 # Per-track logit mean / std of the seed-777 weights on the first 48 windows of the bench meeting (synth.py seed
-# 777), measured by tools/calibrate_spread.py with the fp32 CPU oracle.
+# 777), measured by tests/golden/calibrate_spread.py with the fp32 CPU oracle.
 SPREAD_FC = {
     (1, 6): {"mean": [0.258351, 0.142728, -0.231329, 0.047318], "std": [0.033554, 0.035482, 0.052413, 0.064769]},
     (0, 4): {"mean": [0.779544, -0.063408, 0.516351, -0.875209], "std": [0.287668, 0.215942, 0.231649, 0.308424]},

@@ -1,6 +1,6 @@
 """Calibrate the 'spread' TS-VAD weight variant (round-4 verdict item 4: a DER check that can fail).
 
-    PYTHONPATH=. python tools/calibrate_spread.py [--windows 48]
+    PYTHONPATH=. python tests/golden/calibrate_spread.py [--windows 48]
 
 Seeded random weights put every track's logits on a near-constant plateau (C2: per-track std 0.03-0.06
 around offsets -0.23..0.26), so every recipe threshold either splits nothing or everything and the DER
@@ -14,12 +14,13 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle.pipeline_ref import plan, window_batches  # noqa: E402
 from oracle.tsvad_ref import tsvad_forward  # noqa: E402
 from speaker_diarization_amd.synth import make_meeting, speaker_embeddings  # noqa: E402

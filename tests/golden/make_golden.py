@@ -68,6 +68,65 @@ TSVAD_NAN_CASES = {
 }
 
 
+# round 6: the 'dynamic' weight variant (weights.py dynamic_weights, tests/golden/calibrate_dynamic.py) on real windows
+# of the bench meeting (synth.make_meeting(600, seed 777), the restated kaldi fbank + per-window CMN of
+# oracle/pipeline_ref.py), so the reference run pins the variant's arithmetic in the regime it was calibrated
+# for.  The window fbanks are stored in the fixture (data).  name: (variant, rs_len, first window, n windows)
+TSVAD_DYN_CASES = {
+    "tsvad_v1_rs6_dyn": (1, 6, 20, 3),
+    "tsvad_v0_rs4_dyn": (0, 4, 30, 3),
+}
+
+
+def tsvad_dyn_inputs(name):
+    """(ref_speech (B, T_fb, 80), ts (B, 4, 192), n_label) of a TSVAD_DYN_CASES entry, built from the meeting."""
+    from oracle.pipeline_ref import plan, window_batches
+    from speaker_diarization_amd.synth import make_meeting, speaker_embeddings
+    v, rs, w0, n = TSVAD_DYN_CASES[name]
+    m = make_meeting(600.0, n_spk=4, seed=777)
+    ws = plan(m.labels.shape[1], rs, 1)[w0:w0 + n]
+    (_, _, ref, tsb, L), = list(window_batches(m.wav, speaker_embeddings(4, seed=777), ws, n))
+    return ref.numpy(), tsb.numpy(), int(L)
+
+
+def make_tsvad_dyn(name):
+    import torch
+    from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
+    from oracle.torchaudio_conformer import Conformer
+
+    variant, rs_len = TSVAD_DYN_CASES[name][:2]
+    ref_speech, ts, n_lab = tsvad_dyn_inputs(name)
+    install_stubs(Conformer)
+    sys.path.insert(0, os.path.join(REF, "egs/alimeeting/ts_vad2"))
+    import model as ref_model  # reference TSVADModel
+    ref_model.TSVADModel.load_speaker_encoder = lambda self, *a, **k: None
+    mcfg = ref_model.TSVADConfig()
+    dcfg = ref_model.TSVADDataConfig()
+    dcfg.rs_len = rs_len
+    cfg = TSVADConfig(rs_len=rs_len)
+    if variant == 1:
+        mcfg.speech_encoder_type = "CAM++_ots_vad"
+        mcfg.single_backend_type = "conformer_ots_vad"
+        mcfg.multi_backend_type = "lstm_ots_vad"
+        mcfg.ots_vad_style = "v1"
+        cfg = TSVADConfig.ots_vad_v1(rs_len=rs_len)
+    torch.manual_seed(0)
+    m = ref_model.TSVADModel(cfg=mcfg, task_cfg=dcfg)
+    m.eval()
+    m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=777, dynamic=True)), strict=True)
+    B = ref_speech.shape[0]
+    with torch.no_grad():
+        logits = m(torch.from_numpy(ref_speech), torch.from_numpy(ts), torch.zeros(B, 4, n_lab), num_updates=0)
+    out = dict(logits=logits.numpy().astype(np.float32), ref_speech=ref_speech.astype(np.float32),
+               ts=ts.astype(np.float32), variant=np.int64(variant), rs_len=np.int64(rs_len), n_label=np.int64(n_lab))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, {k: v.shape for k, v in out.items() if hasattr(v, "shape")},
+          "logit std over frames", logits.std(-1).mean().item())
+    sys.path.remove(os.path.join(REF, "egs/alimeeting/ts_vad2"))
+    for mod in ("model", "cam_pplus_wespeaker", "build_datasets", "ts_vad_dataset"):
+        sys.modules.pop(mod, None)
+
+
 def tsvad_case_inputs(name):
     """(case tuple, ref_speech, ts) of a TSVAD_CASES or TSVAD_NAN_CASES name."""
     base, nan_at = (TSVAD_NAN_CASES[name][0], TSVAD_NAN_CASES[name][1:4]) if name in TSVAD_NAN_CASES else (name, None)
@@ -494,6 +553,8 @@ if __name__ == "__main__":
     for n in names:
         if n in TSVAD_CASES or n in TSVAD_NAN_CASES:
             make_tsvad(n)
+        elif n in TSVAD_DYN_CASES:
+            make_tsvad_dyn(n)
         elif n in CAMPP_CASES:
             make_campp(n)
         elif n in TSVAD_STREAM_CASES:

@@ -1,17 +1,18 @@
-"""DER parity that can fail (round-4 verdict item 4): the TS-VAD meeting pipeline on the 'spread' weight
-variant (weights.py spread_fc: the seeded reference-architecture weights with only the final Linear rescaled
-per track, so the posteriors of the bench meeting cross every recipe threshold instead of sitting on a
-plateau), scored by the md-eval restatement (speaker_diarization_amd/der.py, collar 0.25,
-ts_vad2/infer.py:134-163) for the GPU path and for the fp32 CPU oracle (oracle/pipeline_ref.py) on the same
-span of the same meeting.
+"""DER parity that can fail: the TS-VAD meeting pipeline on two weight variants whose posteriors cross the recipe
+thresholds, scored by the md-eval restatement (speaker_diarization_amd/der.py, collar 0.25, ts_vad2/infer.py:134-163)
+for the GPU path and for the fp32 CPU oracle (oracle/pipeline_ref.py) on the same span of the same meeting.
+- 'dynamic' (round 6, weights.py dynamic_weights): gsp_fc and the BiLSTM input centred and scaled upstream with the
+  fp32 oracle, fc x4; the activations move with the frame, 99 % of the posteriors sit in [0.2, 0.8]; pinned by the
+  reference run (tests/golden/tsvad_v*_dyn.npz).
+- 'spread' (round 4, weights.py spread_fc): only fc rescaled per track (x120-240).
 
-fp32 mode: |DER(GPU) - DER(oracle)| <= 0.1 at every recipe threshold (north_star's +-0.1), on a table with
-no threshold at DER 100 on both sides.  bf16 mode is reported beside it (printed: DER table, raw and
-medfilt(21) decision flips).  On the seeded weights the bf16 path's logit error (~4e-3) is ~10 % of the
-logits' own variation across frames (std 0.03-0.06 per track), and the rescale multiplies both by k ~ 120-240;
-an iid 0.01 logit perturbation alone moves this DER by 0.5-3.5 points.  bf16 on this variant
-therefore measures that sensitivity and is recorded, not bounded; bf16 parity is held on the plain weights
-(test_gpu_tsvad.py)."""
+fp32 mode: |DER(GPU) - DER(oracle)| <= 0.1 at every recipe threshold (north_star's +-0.1), on a table that splits
+the frames at >= 6 thresholds.  bf16 mode is reported beside it (printed: DER table, raw decision flips), not
+bounded: on these variants bf16 as a number format moves the DER by more than 0.1 whichever single stage computes in
+it -- the fp32 oracle with only one stage's operands / outputs rounded to bf16 (tests/bf16_der_emulation.py) moves
+the C2 dynamic DER by 0.28 (CAM++ trunk), 2.9 (gsp_fc), 12.2 (conformer), 0.74 (BiLSTM + fc) and the C4 one by
+2.7 (trunk alone, posterior error 7e-4) -- so a bf16 gate at 0.1 on them would fail for the reference model
+itself run in bf16.  bf16 parity is held on the plain weights (test_gpu_tsvad.py)."""
 import numpy as np
 import pytest
 import torch
@@ -29,9 +30,9 @@ pytestmark = pytest.mark.gpu
 N_WIN = 90          # windows (= seconds of meeting) scored
 
 
-def _case(variant):
+def _case(variant, weights):
     cfg = TSVADConfig.ots_vad_v1(rs_len=6) if variant == 1 else TSVADConfig(rs_len=4)
-    sd = to_torch(tsvad_state_dict(cfg, seed=777, spread=True))
+    sd = to_torch(tsvad_state_dict(cfg, seed=777, spread=weights == "spread", dynamic=weights == "dynamic"))
     m = make_meeting(600.0, n_spk=4, seed=777)        # the bench meeting (the calibration's)
     keep = (N_WIN + cfg.rs_len) * 16000               # windows starting before N_WIN s are whole in it
     ts = speaker_embeddings(4, seed=777)
@@ -49,14 +50,15 @@ def _der_table(m, post):
     return {t: der_mod.md_eval(ref, der_mod.read_rttm(rt[t]), collar=0.25).der for t in THRESHOLDS}
 
 
-@pytest.fixture(scope="module", params=[1, 0], ids=["c2_v1", "c4_v0"])
+@pytest.fixture(scope="module", params=[(1, "dynamic"), (0, "dynamic"), (1, "spread"), (0, "spread")],
+                ids=["c2_v1_dynamic", "c4_v0_dynamic", "c2_v1_spread", "c4_v0_spread"])
 def spread_case(request):
-    variant = request.param
+    variant, weights = request.param
     torch.set_num_threads(16)
-    cfg, sd, m, wav, ts = _case(variant)
+    cfg, sd, m, wav, ts = _case(variant, weights)
     T = N_WIN * 25
     cpu = meeting_posteriors(sd, cfg, m.wav, ts, m.labels.shape[1], batch_size=64, max_windows=N_WIN)[:, :T]
-    return variant, cfg, sd, m, wav, ts, cpu, _der_table(m, np.ascontiguousarray(cpu))
+    return (variant, weights), cfg, sd, m, wav, ts, cpu, _der_table(m, np.ascontiguousarray(cpu))
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -71,17 +73,18 @@ def test_der_spread_variant(gpu, spread_case, precision):
     der_gpu = _der_table(m, post)
     g = post.cpu().numpy()
     flips = {t: int(((g > t) != (cpu > t)).sum()) for t in THRESHOLDS}
-    print(f"variant {variant} {precision}: max|post diff| {np.abs(g - cpu).max():.3e}")
+    print(f"variant {variant} {precision}: max|post diff| {np.abs(g - cpu).max():.3e} mean {np.abs(g - cpu).mean():.3e}"
+          f" in[.2,.8] {float(((cpu > .2) & (cpu < .8)).mean()):.2f}")
     print("  DER gpu / oracle:", {t: (round(der_gpu[t], 2), round(der_cpu[t], 2)) for t in THRESHOLDS})
     print("  raw flips:", flips)
-    # the table is not degenerate: every threshold has a DER below 100 on the reference side or ours
-    assert all(min(der_gpu[t], der_cpu[t]) < 100.0 for t in THRESHOLDS)
+    # the table is not degenerate: most thresholds split the frames (DER well below 100) and the DER moves with
+    # the threshold
+    assert sum(der_cpu[t] < 95.0 for t in THRESHOLDS) >= 6, der_cpu
     assert len({round(v, 1) for v in der_cpu.values()}) >= 5, der_cpu
     if precision == "fp32":
         assert np.abs(g - cpu).max() < 1e-3
         assert max(abs(der_gpu[t] - der_cpu[t]) for t in THRESHOLDS) <= 0.1
     else:
-        # recorded, not bounded: the rescale multiplies the bf16 path's logit error (4e-3 on the plain weights,
-        # ~10 % of the seeded weights' logit variation) by k = 8 / std ~ 120-240, so bf16 posteriors on this
-        # variant measure that sensitivity, not parity (round 5, r05b: mean |diff| 0.24, DER 52-86 vs 52-98)
+        # recorded, not bounded (module docstring).  MI355X round 6: dynamic C2 |dDER| <= 13.8 (0.55), C4 0.49
+        # (0.5); spread C2 3.3, C4 6.1
         assert np.isfinite(g).all()

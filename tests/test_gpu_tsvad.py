@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from make_golden import TSVAD_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
+from make_golden import TSVAD_CASES, TSVAD_DYN_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
 from speaker_diarization_amd.ts_vad.model import TSVADModel
 from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
 
@@ -45,6 +45,29 @@ def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
     err = np.abs(out - g["logits"]).max()
     print(f"{name} {precision}: max|logit diff| = {err:.3e} (|logit| max {np.abs(g['logits']).max():.3f})")
     assert err < (FP32_ATOL if precision == "fp32" else BF16_ATOL)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", list(TSVAD_DYN_CASES))
+def test_tsvad_dynamic_variant_vs_reference_golden(gpu, name, precision):
+    """The 'dynamic' weight variant on the bench meeting's windows (reference run, make_golden.py
+    TSVAD_DYN_CASES).  fp32: the north_star bound.  bf16: here the logits move with the frame (std 0.6-1.1) and
+    the bf16 error is quoted against that motion (round 6, DESIGN §3: rms error / frame std of the logits);
+    the bound is a regression guard on that ratio, not a parity claim."""
+    v, rs = TSVAD_DYN_CASES[name][:2]
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    cfg = _cfg(v, rs)
+    m = TSVADModel(cfg, device=gpu, precision=precision, max_batch=8)
+    m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=777, dynamic=True)))
+    nl = int(g["n_label"])
+    out = m.forward(torch.from_numpy(g["ref_speech"]).to(gpu), torch.from_numpy(g["ts"]).to(gpu), nl).cpu().numpy()
+    d = out - g["logits"]
+    ratio = float(np.sqrt((d ** 2).mean()) / g["logits"].std(axis=-1).mean())
+    print(f"{name} {precision}: max|logit diff| {np.abs(d).max():.3e}, rms diff / frame std {ratio:.3e}")
+    if precision == "fp32":
+        assert np.abs(d).max() < FP32_ATOL
+    else:
+        assert ratio < 0.2
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from make_golden import TSVAD_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
+from make_golden import TSVAD_CASES, TSVAD_DYN_CASES, TSVAD_NAN_CASES, tsvad_case_inputs, tsvad_inputs
 from oracle import fbank_ref
 from oracle.tsvad_ref import speech_encoder_out, tsvad_forward
 from speaker_diarization_amd.weights import TSVADConfig, tsvad_state_dict, to_torch
@@ -25,6 +25,20 @@ def test_tsvad_oracle_matches_reference(name):
     np.testing.assert_allclose(out, g["logits"], atol=2e-5, rtol=1e-5)
     enc = speech_encoder_out(sd, torch.from_numpy(x)).numpy()
     np.testing.assert_allclose(enc, g["speech_enc"], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", list(TSVAD_DYN_CASES))
+def test_tsvad_oracle_dynamic_variant_matches_reference(name):
+    """The 'dynamic' weight variant (weights.dynamic_weights: centred / scaled gsp_fc and BiLSTM input, fc x4) on
+    windows of the bench meeting, pinned by the reference run (make_golden.py TSVAD_DYN_CASES); the fixture
+    holds the window fbanks.  The logits move with the frame (std across frames 0.6-1.1, vs 0.03-0.3 plain)."""
+    v, rs = TSVAD_DYN_CASES[name][:2]
+    g = np.load(f"{__file__.rsplit('/', 1)[0]}/golden/{name}.npz")
+    cfg = _cfg(v, rs)
+    sd = to_torch(tsvad_state_dict(cfg, seed=777, dynamic=True))
+    out = tsvad_forward(sd, cfg, torch.from_numpy(g["ref_speech"]), torch.from_numpy(g["ts"]), int(g["n_label"])).numpy()
+    np.testing.assert_allclose(out, g["logits"], atol=5e-5, rtol=1e-5)
+    assert g["logits"].std(axis=-1).mean() > 0.5
 
 
 @pytest.mark.parametrize("name", list(TSVAD_NAN_CASES))
