@@ -854,8 +854,7 @@ __global__ __launch_bounds__(256) void attn_tiny_kernel(AttnArgs a) {
 
 template <int HD>
 bool launch_tiny(const AttnArgs& a, bool bf16, hipStream_t st) {
-  static const bool off = getenv("SDIAR_NO_ATTN_TINY") != nullptr;   // A/B switch: attn_short
-  if (off || !bf16 || !a.io_bf16 || a.chunk || a.mask_dump || a.T > 16 || HD % 8 || HD > 128 ||
+  if (!bf16 || !a.io_bf16 || a.chunk || a.mask_dump || a.T > 16 || HD % 8 || HD > 128 ||
       (a.ld_qkv % 8) || (a.D % 8) || (a.ldo % 8) || (a.tok_stride * a.ld_qkv) % 8)
     return false;
   const int64_t n = (int64_t)a.S * a.nh * a.T;
@@ -882,9 +881,8 @@ bool launch_long(const AttnArgs& a, bool bf16, hipStream_t st) {
     // (a split of each query block's key pairs over two workgroups measured 60 -> 54 us here, but the split
     // depends on the grid, so sharded runs — EDA chunk shards, bit-identical for any world size — would
     // differ by world size; not kept)
-    static const bool no_group = getenv("SDIAR_ATTN_NO_GROUP_REMAP") != nullptr;   // A/B switch
     AttnArgs b = a;
-    b.xcd_small = !no_group;
+    b.xcd_small = 1;
     hipLaunchKernelGGL((attn_long_kernel<HD, 2>), grid, dim3(512), 0, st, b);
   } else {
     // large grids: K and the first V half hoisted (126 VGPRs, still 4 waves per SIMD): 187 -> 178 us on the
@@ -910,23 +908,15 @@ bool launch_short(const AttnArgs& a, bool bf16, hipStream_t st) {
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  static const int env_hpw = getenv("SDIAR_ATTN_HPW") ? atoi(getenv("SDIAR_ATTN_HPW")) : 0;
-  static const bool env_xr = getenv("SDIAR_ATTN_NO_XREMAP") == nullptr;
-  int hpw = 1;
-  if (env_hpw > 0) hpw = std::min(env_hpw, a.nh);
+  const int hpw = 1;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_short_kernel<HD, false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(attn_short_kernel<HD, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const dim3 grid(a.S * ((a.nh + hpw - 1) / hpw));
-  if (env_xr)
-    hipLaunchKernelGGL((attn_short_kernel<HD, true>), grid, dim3(256), smem, st, a, TP, hpw);
-  else
-    hipLaunchKernelGGL((attn_short_kernel<HD, false>), grid, dim3(256), smem, st, a, TP, hpw);
+  hipLaunchKernelGGL((attn_short_kernel<HD, true>), grid, dim3(256), smem, st, a, TP, hpw);
   return true;
 }
 

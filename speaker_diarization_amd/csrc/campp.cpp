@@ -64,7 +64,6 @@ ConvL load_conv_bn(ParamStore& ps, DeviceArena& arena, bool bf16, const std::str
 // ------------------------------------------------------------------------------ CamTrunk
 void CamTrunk::load(ParamStore& ps, DeviceArena& arena, const std::string& pre, bool bf16) {
   bf16_ = bf16;
-  no_fused_ = getenv("SDIAR_NO_CAM_FUSED") != nullptr;
   auto conv_bn = [&](const std::string& w, const std::string& bn, const std::string& bias = "") {
     return load_conv_bn(ps, arena, bf16, w, bn, bias);
   };
@@ -198,10 +197,8 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
     if (i == 0) {
       fu.fbank = ref; fu.fb_F = F;
       fu.stem_w = fcm_conv1_.pre_s; fu.stem_alpha = fcm_conv1_.alpha; fu.stem_beta = fcm_conv1_.beta;
-      static const bool stem_valu = getenv("SDIAR_FCM_STEM_VALU") != nullptr;   // A/B switch: fp32 fmaf stem
-      fu.stem_mfma = stem_valu ? 0 : 1;
     }
-    const bool fused = bf && !no_fused_ && rb.has_sc && rb.sc.w.N == 32 && rb.sc.w.K == 32 && fcm_fused_supported(p, fu);
+    const bool fused = bf && rb.has_sc && rb.sc.w.N == 32 && rb.sc.w.K == 32 && fcm_fused_supported(p, fu);
     if (i == 0 && !fused) {
       fcm_conv1(ref, B, Tf, F, fcm_conv1_.pre_s, fcm_conv1_.alpha, fcm_conv1_.beta, fcmA, bf, st);
       stem_done = true;
@@ -250,7 +247,7 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
     const int ld = ctot[b];
     for (const DenseL& L : dense_[b]) {
       SD_CHECK(L.bottleneck.w.Cin == cin, kErrParam, "dense layer input width");
-      if (!no_fused_ && cam_dense_supported(T2, cin, ld, L.bottleneck.w.N, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil,
+      if (cam_dense_supported(T2, cin, ld, L.bottleneck.w.N, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil,
                                             100, bf)) {
         // the whole layer per item in one launch, the 128-channel bottleneck kept in LDS (cam_dense.hip)
         cam_dense(D.p, B, T2, ld, cin, L.dil, L.bottleneck.pre_s, L.bottleneck.pre_h, L.bottleneck.w.w,
@@ -262,7 +259,7 @@ Tens CamTrunk::forward(const float* fbank, int B, int Tf, hipStream_t st, int b0
       ConvGemmArgs p = cam_conv1d(D, B, T2, ld, L.bottleneck, 1, 0, 1, Tens{tmp, bf}, 128);
       p.act = kActRelu;
       conv_gemm(p, bf, st);
-      if (!no_fused_ && cam_local_fused_supported(128, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil, 100, ld, bf)) {
+      if (cam_local_fused_supported(128, L.c1, L.c2, L.local.w.N, L.local.w.kw, L.dil, 100, ld, bf)) {
         // Small batches (the embedding extractor's 96 chunks): one launch per layer that also
         // computes the gate.  Large batches: the context kernel, then the conv kernel reading
         // only each segment's window rows (fewer bytes per workgroup, higher occupancy).

@@ -52,7 +52,6 @@ class CamTrunk {
  private:
   float* ws(DeviceArena& a, size_t n) { return static_cast<float*>(a.alloc(n * sizeof(float))); }
   bool bf16_ = false;
-  bool no_fused_ = false;   // SDIAR_NO_CAM_FUSED: context + local conv as two launches (A/B checks)
   ConvL fcm_conv1_;  // fp32 3x3 Cin=1 weights (32x9) + folded bn
   struct ResBlock { ConvL c1, c2, sc; bool has_sc; int stride; };
   std::vector<ResBlock> fcm_blocks_;

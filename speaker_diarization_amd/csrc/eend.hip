@@ -383,8 +383,7 @@ void stream_frontend(const float* wav, int64_t cap_samples, int rows, int n_fft,
   const int n_frames = (rows - 1) * sub + 2 * context + 1;   // logmel frames the chunk's splice reads
   ProfScope prof("stream_frontend", 5.0 * n_fft * std::log2((double)n_fft) * n_frames,
                  4.0 * (double)n_frames * hop + 4.0 * rows * ld_out, st);
-  static const bool two = getenv("SDIAR_FRONTEND_TWO_LAUNCH") != nullptr;   // A/B switch
-  if (n_fft == 256 && n_frames <= 16 && !two) {   // the chunk in one workgroup, splice included
+  if (n_fft == 256 && n_frames <= 16) {   // the chunk in one workgroup, splice included
     hipLaunchKernelGGL((stft_logmel_kernel<8, true, 16, true>), dim3(1), dim3(1024), 0, st, wav, cap_samples, n_frames,
                        hop, win_len, mel_fb, n_mels, lm, cursor, bound, sub, context, rows, out, ld_out);
     SD_LAUNCH_CHECK();

@@ -259,14 +259,11 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
   const int rows = S * T;
   const Tens y{w.Y, true}, qkv{w.QKV, true}, ao{w.AO, true}, h{w.H, true};
   // the residual stream between the row programs in their MFMA-tiled layout (kernels.h RowProgArgs::x_tiled);
-  // the caller sees X row-major (or only the speaker-layout output).  SDIAR_RP_ROWMAJOR_X=1: row-major throughout.
-  static const bool rowmajor = getenv("SDIAR_RP_ROWMAJOR_X") != nullptr;
-  const int tiled = !rowmajor && rows % 16 == 0;
-  static const bool rowmajor_a = getenv("SDIAR_RP_ROWMAJOR_A") != nullptr;   // A/B: the attention output row-major
-  const int tiled_a = tiled && !rowmajor_a && mha_block_supported(E, nh, T, true);
-  // the attention LayerNorm's rows (y of the FFN programs) go only to mha_block: tiled as well
-  static const bool rowmajor_y = getenv("SDIAR_RP_ROWMAJOR_Y") != nullptr;   // A/B switch
-  const int tiled_y = tiled_a && !rowmajor_y;
+  // the caller sees X row-major (or only the speaker-layout output); so does mha_block's attention output and
+  // the attention LayerNorm's rows (y of the FFN programs), which go only to mha_block
+  const int tiled = rows % 16 == 0;
+  const int tiled_a = tiled && mha_block_supported(E, nh, T, true);
+  const int tiled_y = tiled_a;
   auto ffn = [](const ConformerL& L, bool second) {
     RowFfnArgs f;
     f.w = second ? L.rp_f2 : L.rp_f1;
@@ -309,12 +306,12 @@ void run_conformer_stack(const std::vector<ConformerL>& Ls, float* X, int S, int
       attention(a, true, st);
     }
     // pw1 (+ GLU) reads the conv-LN rows the out-projection program writes: tiled when the register-A GEMM
-    // takes it (SDIAR_RP_ROWMAJOR_Y: row-major, A/B)
+    // takes it
     ConvGemmArgs p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, E);
     p1.glu = 1;
     const bool glu_epi = gemm_stream_supported(p1);
     if (!glu_epi) p1 = lin(y, rows, E, L.pw1, L.pw1_b, h, 2 * E);
-    p1.a_tiled = tiled && !rowmajor_y && gemm_areg_supported(p1);
+    p1.a_tiled = tiled && gemm_areg_supported(p1);
     {
       RowProgArgs r;
       r.X = X; r.Xo = X; r.M = rows;

@@ -30,7 +30,6 @@ constexpr int kFramesPerBlock = 8;
 constexpr int kMaxFbMels = 128;
 constexpr int kMelCap = 2 * kBins + 2 * kMaxFbMels;   // triangular banks: each bin in at most two filters
 
-__device__ __forceinline__ int bitrev9(int x) { return __brev((unsigned)x) >> (32 - 9); }
 __device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses (no workgroup barrier)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -41,7 +40,6 @@ __device__ __forceinline__ void wave_sync() {   // order one wave's LDS accesses
 // window (the same cospif / powf values the per-sample form computed) and each mel filter's nonzero bin
 // range and values, so the projection runs over a filter's ~10 bins instead of all 257 (the skipped terms
 // are exact zeros: same sums, same order).  A frame's FFT stages belong to its wave alone: wave barriers only.
-template <bool REG>
 __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wav, int64_t n_samples,
                                                     float in_scale, int n_frames,
                                                     const float* __restrict__ mel_fb, int n_mels,
@@ -137,9 +135,10 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
       if (n < kFrameLen) buf[w][pz(n)].x = v[i] - mean;   // scratch (real part)
     }
     wave_sync();   // this frame's scratch
-    if constexpr (REG) {
+    {
       // Radix-2 DIT in three register passes of three stages each, the wave's LDS only for the two
-      // transposes between them (the per-stage form below moved every element through LDS nine times).
+      // transposes between them (round 5; the nine-stage LDS form it replaced moved every element through LDS
+      // nine times).
       // Same butterflies, same twiddles, same order per element.
       // pass A: bit-reversed positions 8 lane + k (sample bitrev3(k) * 64 + bitrev6(lane)), stages 1, 2, 4
       float2 X[8];
@@ -193,47 +192,6 @@ __global__ __launch_bounds__(512) void fbank_kernel(const float* __restrict__ wa
 #pragma unroll
       for (int m = 0; m < 5; ++m)
         if (lane + 64 * m < kBins) pw[w][lane + 64 * m] = X[m].x * X[m].x + X[m].y * X[m].y;
-    } else {
-      // Pre-emphasis + window, written bit-reversed for the DIT FFT.
-      float y[8];
-  #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        int n = lane + i * 64;
-        float val = 0.f;
-        if (n < kFrameLen) {
-          float cur = buf[w][pz(n)].x;
-          float prev = n > 0 ? buf[w][pz(n - 1)].x : cur;
-          val = (cur - 0.97f * prev) * win[n];
-        }
-        y[i] = val;
-      }
-      wave_sync();
-  #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        int n = lane + i * 64;
-        buf[w][pz(bitrev9(n))] = make_float2(y[i], 0.f);
-      }
-      // Radix-2 DIT, 9 stages, 256 butterflies per stage -> 4 per lane.
-      for (int half = 1; half < kNfft; half <<= 1) {
-        wave_sync();
-        const int tstride = kNfft / (2 * half);
-  #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int bfly = lane + i * 64;
-          int grp = bfly / half, pos = bfly % half;
-          int i0 = grp * 2 * half + pos, i1 = i0 + half;
-          float2 t0 = tw[pos * tstride];
-          float2 a = buf[w][pz(i0)], b = buf[w][pz(i1)];
-          float2 t = make_float2(b.x * t0.x - b.y * t0.y, b.x * t0.y + b.y * t0.x);
-          buf[w][pz(i0)] = make_float2(a.x + t.x, a.y + t.y);
-          buf[w][pz(i1)] = make_float2(a.x - t.x, a.y - t.y);
-        }
-      }
-      wave_sync();
-      for (int k = lane; k < kBins; k += 64) {
-        float2 c = buf[w][pz(k)];
-        pw[w][k] = c.x * c.x + c.y * c.y;
-      }
     }
     wave_sync();
     if (active) {
@@ -273,26 +231,19 @@ void fbank_kaldi(const float* wav, int64_t n_samples, float in_scale, int n_fram
   if (n_frames <= 0) return;
   ProfScope prof("fbank_kaldi", 0.0, 4.0 * ((double)n_frames * kShift + (double)n_frames * n_mels), st);
   SD_CHECK(n_mels > 0 && n_mels <= kMaxFbMels, kErrInvalid, "fbank: n_mels out of range");
-  // as many workgroups as are resident at once (each builds its tables once and walks frame groups);
-  // SDIAR_FBANK_PER_GROUP=1 (A/B): one workgroup per 8-frame group, i.e. the tables rebuilt per group
+  // as many workgroups as are resident at once (each builds its tables once and walks frame groups)
   static int slots = 0;
   if (!slots) {
     int dev = 0, cus = 0, per_cu = 0;
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel<true>, 512, 0));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel, 512, 0));
     slots = std::max(1, cus * std::max(1, per_cu));
   }
-  static const bool per_group = getenv("SDIAR_FBANK_PER_GROUP") != nullptr;
-  static const bool lds_fft = getenv("SDIAR_FBANK_LDS_FFT") != nullptr;   // A/B: the nine-stage LDS FFT
   const int groups = cdiv(n_frames, kFramesPerBlock);
-  const dim3 grid(per_group ? groups : std::min(groups, slots));
-  if (lds_fft)
-    hipLaunchKernelGGL(fbank_kernel<false>, grid, dim3(512), 0, st, wav, n_samples, in_scale, n_frames, mel_fb,
-                       n_mels, g_twiddle, window, out);
-  else
-    hipLaunchKernelGGL(fbank_kernel<true>, grid, dim3(512), 0, st, wav, n_samples, in_scale, n_frames, mel_fb,
-                       n_mels, g_twiddle, window, out);
+  const dim3 grid(std::min(groups, slots));
+  hipLaunchKernelGGL(fbank_kernel, grid, dim3(512), 0, st, wav, n_samples, in_scale, n_frames, mel_fb, n_mels,
+                     g_twiddle, window, out);
   SD_LAUNCH_CHECK();
 }
 

@@ -206,6 +206,7 @@ template <int R, int SH, bool STEM = false, bool SC = false, bool TOUT = false, 
 __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemmArgs p, FcmFuse f, int n_bands,
                                                                        int n_blk) {
   // A band: (image b, R output rows from ho0, time tile tt of n_blk 16-frame blocks).
+  static_assert(!STEM || SMF, "the stem runs on the MFMA with LDS-only band barriers (the fp32 VALU stem: round 5)");
   constexpr int NR = (R - 1) * SH + 3;
   // staged 16-B vectors per thread: NR rows x (at most 19 x 16 + 2 = 306 frames) x 4 (band_fits checks it)
   constexpr int kVP = (NR * (TOUT ? kToutBlk * 16 + 2 : 306) * 4 + kBandThreads - 1) / kBandThreads;
@@ -293,15 +294,14 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
   float* fbs = reinterpret_cast<float*>(xs + NR * Wp * kPS);
   const int fb_n = (NR + 2) * (Wp + 2);
   constexpr int kFbPer = 5;   // fbank tile floats per thread (<= 2560)
-  float s_al[8], s_be[8];
-  // MFMA stem (f.stem_mfma): v_mfma_f32_32x32x16_bf16 with the 32 channels as rows and 32 staged pixels as
+  // MFMA stem: v_mfma_f32_32x32x16_bf16 with the 32 channels as rows and 32 staged pixels as
   // columns; k = the 9 taps (dh, dw) in order, then beta's bf16 hi and lo parts against a constant 1 (BN
   // folded: A = bf16(alpha_c * w_c), so a pixel is relu(sum + beta) with no epilogue FMAs).  A row m is
   // channel 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3), so accumulator i of lane half h is channel 16 h + i
   // and a lane stores its pixel's 16 contiguous channels as two 16-B LDS writes.
   bf16x8 stem_a;
   if constexpr (STEM) {
-    if constexpr (SMF) {
+    {
       const int m = lane & 31, h = lane >> 5;
       const int c = 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3);
       const float al = f.stem_alpha[c], be = f.stem_beta[c];
@@ -318,13 +318,6 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       const uint32_t w4[4] = {pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]), pack_bf16x2(e[4], e[5]),
                               pack_bf16x2(e[6], e[7])};
       stem_a = *reinterpret_cast<const bf16x8*>(w4);
-    } else {
-      const int c0 = (tid & 3) * 8;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s_al[u] = f.stem_alpha[c0 + u];
-        s_be[u] = f.stem_beta[c0 + u];
-      }
     }
   }
   // fbank value (bin hb - 1 + j, frame w0 - 1 + x) of a band, j < NR + 2, x < Wp + 2; zero outside the map
@@ -365,7 +358,7 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
       // stem: staged pixel (rr, px) = conv1 row hb + rr, frame w0 + px; zero outside (next conv's padding)
       const int tt = band % n_tt, bh = band / n_tt;
       const int hb = (bh % n_rb) * R * SH - 1, w0 = tt * n_blk * 16 - 1;
-      if constexpr (SMF) {
+      {
         const int n = lane & 31, h = lane >> 5;
         const int ngr = (Wp + 31) >> 5;   // 32-pixel groups per staged row (reads past Wp hit the tile's pad)
         for (int g = wv; g < NR * ngr; g += kBandThreads / 64) {
@@ -396,66 +389,6 @@ __global__ __launch_bounds__(kBandThreads) void fcm_conv3x3_band_kernel(ConvGemm
             *reinterpret_cast<uint4*>(dst + 8) = make_uint4(o[4], o[5], o[6], o[7]);
           }
         }
-      } else {
-      const float* swb = f.stem_w;
-      asm volatile("" : "+s"(swb));
-      const float* swp = swb + (tid & 3) * 72;
-      // channel pairs as packed f32 (v_pk_fma_f32: the same fmaf chain per channel, two per instruction)
-      typedef float f32x2 __attribute__((ext_vector_type(2)));
-      f32x2 sw2[4][9];
-#pragma unroll
-      for (int k = 0; k < 72; ++k) sw2[k / 18][k % 9][(k / 9) & 1] = swp[k];
-      // Items: (staged row rr, 4 consecutive frames px0.., this thread's channel group).  The 4 pixels share
-      // their 3 x 6 fbank taps (one 16-B + one 8-B LDS read per tap row instead of 9 reads per pixel), and
-      // (rr, quad) advance incrementally: the per-pixel pix / Wp of the one-pixel loop was a division per item.
-      // The fmaf chain per (pixel, channel) is unchanged (taps in (dh, dw) order): bit-identical output.
-      const int nq = (Wp + 3) >> 2;
-      const int n_items = NR * nq;                 // per channel group
-      int qx = (tid >> 2) % nq, qr = (tid >> 2) / nq;
-      for (int it = tid >> 2; it < n_items; it += kBandThreads / 4) {
-        const int px0 = qx * 4;
-        float xw[3][6];
-#pragma unroll
-        for (int dh = 0; dh < 3; ++dh) {
-          const float* r0 = fbs + (qr + dh) * (Wp + 2) + px0;
-          const float4 a4 = *reinterpret_cast<const float4*>(r0);
-          const float2 b2 = *reinterpret_cast<const float2*>(r0 + 4);
-          xw[dh][0] = a4.x; xw[dh][1] = a4.y; xw[dh][2] = a4.z; xw[dh][3] = a4.w; xw[dh][4] = b2.x; xw[dh][5] = b2.y;
-        }
-        const bool row_ok = (unsigned)(hb + qr) < (unsigned)p.H;
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-          const int px = px0 + pp;
-          if (px >= Wp) break;
-          const bool ok = row_ok && (unsigned)(w0 + px) < (unsigned)W;
-          float v[8];
-#pragma unroll
-          for (int u2 = 0; u2 < 4; ++u2) {
-            f32x2 acc = {0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-              const float xv = xw[k / 3][pp + k % 3];
-              acc = __builtin_elementwise_fma(sw2[u2][k], f32x2{xv, xv}, acc);
-            }
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int u = 2 * u2 + e;
-              v[u] = ok ? fmaxf(acc[e] * s_al[u] + s_be[u], 0.f) : 0.f;
-            }
-          }
-          *reinterpret_cast<uint4*>(xs + (qr * Wp + px) * kPS + (tid & 3) * 8) =
-              make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                         pack_bf16x2(v[6], v[7]));
-        }
-        qx += kBandThreads / 4;
-        while (qx >= nq) {
-          qx -= nq;
-          ++qr;
-        }
-      }
-      const uint16_t* wtp = reinterpret_cast<const uint16_t*>(p.Wt);
-      asm volatile("" : "+s"(wtp));
-      load_wf(wtp);
       }
       // SMF: LDS-only barriers (a __syncthreads() fence would also drain the next band's fbank prefetch
       // and this band's output stores)
@@ -834,27 +767,24 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
     SD_HIP(hipGetDevice(&dev));
     SD_HIP(hipDeviceGetAttribute(&g_fcm_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  static const bool no_band = getenv("SDIAR_NO_FCM_BAND") != nullptr;
-  static const bool no_ring = getenv("SDIAR_NO_FCM_RING") != nullptr;   // A/B switch: the band kernel
-  if (!no_band && !no_ring && ring_ok(p)) {
+  if (ring_ok(p)) {
     const bool relu = p.act == kActRelu;
     if (p.res) relu ? launch_ring<true, true>(p, st) : launch_ring<true, false>(p, st);
     else relu ? launch_ring<false, true>(p, st) : launch_ring<false, false>(p, st);
     SD_LAUNCH_CHECK();
     return;
   }
-  if (!no_band && p.sh == 1 && band_fits<4, 1>(p)) {
+  if (p.sh == 1 && band_fits<4, 1>(p)) {
     launch_band<4, 1>(p, st);
     SD_LAUNCH_CHECK();
     return;
   }
-  static const bool no_tout = getenv("SDIAR_NO_FCM_TOUT") != nullptr;   // A/B switch: per-element stores
-  if (!no_band && !no_tout && tout_ok(p)) {
+  if (tout_ok(p)) {
     launch_tout(p, st);
     SD_LAUNCH_CHECK();
     return;
   }
-  if (!no_band && p.sh == 2 && band_fits<2, 2>(p)) {
+  if (p.sh == 2 && band_fits<2, 2>(p)) {
     launch_band<2, 2>(p, st);
     SD_LAUNCH_CHECK();
     return;
@@ -868,8 +798,7 @@ void conv_fcm3x3(const ConvGemmArgs& p, hipStream_t st) {
 }
 
 bool fcm_fused_supported(const ConvGemmArgs& p, const FcmFuse& f) {
-  static const bool off = getenv("SDIAR_NO_FCM_FUSE") != nullptr;   // A/B switch
-  if (off || p.sh != 2 || !p.out_bf16 || p.res || p.o_sn != 1 || p.o_sw != 32) return false;
+  if (p.sh != 2 || !p.out_bf16 || p.res || p.o_sn != 1 || p.o_sw != 32) return false;
   if (f.sc_w && !(f.sc_alpha && f.sc_beta && f.sc_out)) return false;
   if (f.fbank) {
     if (!(f.stem_w && f.stem_alpha && f.stem_beta && f.fb_F == p.H)) return false;
@@ -894,8 +823,8 @@ void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st) 
   if (f.fbank) flops += 2.0 * (double)p.B * p.H * p.W * 32 * 9;
   const double bytes = in_px * 64 + (f.fbank ? 4.0 * p.B * p.W * f.fb_F : 0.0) + px * 64 * (f.sc_w ? 2 : 1);
   ProfScope prof(f.fbank ? "fcm_stem" : "fcm_conv3x3_band", flops, bytes, st);
-  if (f.fbank && f.sc_w) f.stem_mfma ? launch_band<2, 2, true, true, true>(p, st, f) : launch_band<2, 2, true, true>(p, st, f);
-  else if (f.fbank) f.stem_mfma ? launch_band<2, 2, true, false, true>(p, st, f) : launch_band<2, 2, true, false>(p, st, f);
+  if (f.fbank && f.sc_w) launch_band<2, 2, true, true, true>(p, st, f);
+  else if (f.fbank) launch_band<2, 2, true, false, true>(p, st, f);
   else if (f.sc_w) launch_band<2, 2, false, true, true>(p, st, f);
   else launch_band<2, 2>(p, st);
   SD_LAUNCH_CHECK();

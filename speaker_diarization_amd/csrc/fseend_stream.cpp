@@ -126,7 +126,7 @@ void gemm_fused(ConvGemmArgs p, const PendingLn* ln, const KvEpi* kv, int D, boo
 }  // namespace
 
 // linear1 -> relu -> linear2 of a transformer layer on n rows with the pending post-LN folded in: one stream_ffn_pair
-// launch when it applies (SDIAR_NO_FFN_PAIR=1: the two skinny GEMMs, for A/B), the result in T_ either way
+// launch when it applies (else the two skinny GEMMs), the result in T_ either way
 void FsEendStream::ffn(const PackedW& l1, const float* b1, const PackedW& l2, const float* b2, const float* ln_x,
                        const void* ln_t, const float* ln_g, const float* ln_b, float* ln_out, int n, hipStream_t st) {
   const int D = m_.cfg_.n_units;
@@ -191,8 +191,7 @@ void FsEendStream::dec_chunk(hipStream_t st) {
   const float scale = 1.f / std::sqrt((float)(D / nh));
   // The window gather, the embedding's L2 norm and the slot init run as the A prologues of the GEMMs that
   // consume them (gemm_skinny pro_mode 3 / 1 / 2: same values, three launches fewer) when the skinny path
-  // takes the chunk; SDIAR_NO_STREAM_PRO=1 keeps them as their own kernels.
-  static const bool no_pro = getenv("SDIAR_NO_STREAM_PRO") != nullptr;
+  // takes the chunk (else they run as their own kernels).
   {
     ConvGemmArgs p;
     p.A = W_; p.a_bf16 = false; p.B = 1; p.H = 1; p.W = c + 18; p.Cin = D; p.lda = D; p.a_coff = 0;
@@ -204,7 +203,7 @@ void FsEendStream::dec_chunk(hipStream_t st) {
     p.o_sb = (int64_t)c * D; p.o_sh = 0; p.o_sw = D; p.o_sn = 1;
     ConvGemmArgs q = p;
     q.pro_mode = 3; q.ln_x = hist_; q.pro_cursor = state_ + 2; q.pro_nvalid = state_ + 1; q.pro_pad = 9;
-    if (!no_pro && gemm_skinny_supported(q)) {
+    if (gemm_skinny_supported(q)) {
       conv_gemm_skinny(q, bf_, st);
     } else {
       gather_window(hist_, D, state_ + 2, state_ + 1, 9, c + 18, W_, st);
@@ -215,7 +214,7 @@ void FsEendStream::dec_chunk(hipStream_t st) {
     ConvGemmArgs p = lin(Tens{E_, false}, c, D, m.conv_emb_, nullptr, Tens{G_, false}, D);
     ConvGemmArgs q = p;
     q.pro_mode = 1; q.ln_x = Yc_; q.ln_out = E_;
-    if (!no_pro && gemm_skinny_supported(q)) {
+    if (gemm_skinny_supported(q)) {
       conv_gemm_skinny(q, bf_, st);
     } else {
       row_l2norm(Yc_, c, D, E_, st);
@@ -233,7 +232,7 @@ void FsEendStream::dec_chunk(hipStream_t st) {
       ConvGemmArgs q = lin(Tens{ab[ai], false}, n, D, f.in1, f.in1_b, qkv, 3 * D);
       q.pro_mode = 2; q.ln_x = G_; q.pro_p = m.slot_bias_; q.pro_C = C; q.ln_out = ab[0];
       q.kv_out = kv.dst; q.kv_cursor = kv.cursor; q.kv_mult = kv.mult; q.kv_col0 = D; q.kv_ld = kv.ld;
-      if (!no_pro && gemm_skinny_supported(q)) {
+      if (gemm_skinny_supported(q)) {
         conv_gemm_skinny(q, bf_, st);
       } else {
         slot_init(G_, c, C, D, m.slot_bias_, ab[0], st);
@@ -385,10 +384,8 @@ int FsEendStream::push_audio(const float* samples, int64_t n, float* preds, int 
   while (n_model - n_enc_ >= c_) {
     SD_CHECK(n_enc_ + c_ <= cap_, kErrInvalid, "stream exceeds max_frames");
     // steady state: this encoder chunk makes exactly one decoder chunk ready -> both in one graph launch
-    // (SDIAR_NO_COMBINED_GRAPH=1: two launches, for A/B)
-    static const bool no_comb = getenv("SDIAR_NO_COMBINED_GRAPH") != nullptr;
     const int nv = n_enc_ + c_;
-    if (!no_comb && n_dec_ + c_ + 9 <= nv && n_dec_ + 2 * c_ + 9 > nv) {
+    if (n_dec_ + c_ + 9 <= nv && n_dec_ + 2 * c_ + 9 > nv) {
       run(2, st);
       n_enc_ = nv;
       n_valid_ = nv;

@@ -439,9 +439,8 @@ void conv_gemm_dma(const ConvGemmArgs& p, hipStream_t st) {
 // Split-K for the short-M, long-K GEMMs (the post-LN FFN down-projections: M 6000, K 2048, N 256 is 188
 // 64x128 tiles, one per CU, each walking 32 k-tiles at one DMA latency apiece): ksplit workgroups per tile.
 int gemm_splitk_count(const ConvGemmArgs& p) {
-  static const bool off = getenv("SDIAR_NO_SPLITK") != nullptr;   // A/B switch
   const int M = p.B * p.Ho * p.Wo;
-  if (off || !gemm_dma_supported(p) || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
+  if (!gemm_dma_supported(p) || p.pre_scale || p.alpha || p.res || p.gate || p.glu ||
       p.act != kActNone || p.o_sn != 1 || p.K < 1024 || p.N % 4)
     return 1;
   // enough 256x128 tiles for one per CU: the ring GEMM (3-stage DMA ring) beats the split (FS-EEND decoder

@@ -479,8 +479,7 @@ void launch_ring_persist(const ConvGemmArgs& p, hipStream_t st) {
 
 template <bool PRE, int ACT>
 void launch_ring(const ConvGemmArgs& p, hipStream_t st) {
-  static const bool no_persist = getenv("SDIAR_NO_RING_PERSIST") != nullptr;   // A/B switch
-  if (p.N <= RBN && !no_persist) {
+  if (p.N <= RBN) {
     launch_ring_persist<PRE, ACT>(p, st);
     return;
   }

@@ -98,7 +98,6 @@ struct FcmFuse {
   const float* fbank = nullptr;               // (B, W, fb_F) fp32
   int fb_F = 0;
   const float *stem_w = nullptr, *stem_alpha = nullptr, *stem_beta = nullptr;   // 32x9 raw, folded BN
-  int stem_mfma = 0;   // 1: the stem as one bf16 32x32x16 MFMA per 32 pixels (BN folded); 0: the fp32 fmaf chain
 };
 bool fcm_fused_supported(const ConvGemmArgs& p, const FcmFuse& f);
 void conv_fcm3x3_fused(const ConvGemmArgs& p, const FcmFuse& f, hipStream_t st);
@@ -273,10 +272,9 @@ struct RowProgArgs {
   // -> (b, t) columns spk*384 .. (speakers_to_channels); with Xo == nullptr the fp32 rows are not written
   void* yt = nullptr;
   int yt_NS = 0;
-  // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog(); SDIAR_RP_STAGGER scales it):
+  // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog()):
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
-  int prio = 0;      // 1: waves 4-7 run at s_setprio 1 (A/B: SDIAR_RP_PRIO)
   // X / Xo in the MFMA-tiled layout (M % 16 == 0): 16-row group g, feature f = 16 ft + 4 q + r of row 16 g + l at
   // float ((g * 24 + ft) * 64 + l + 16 q) * 4 + r -- each wave's 16 x 384 fp32 residual block is 24 contiguous
   // 1-KiB runs, one per load / store instruction (row-major it is 16 scattered 64-B pieces per instruction).  The
@@ -576,7 +574,7 @@ struct FfnPairArgs {
   int n = 1, D = 256, F = 2048;
 };
 bool stream_ffn_pair(const FfnPairArgs& a, hipStream_t st);
-// returns true when it also ran the out-projection (wo set, the fused merge taken; SDIAR_NO_ATTN_OUTPROJ=1: never)
+// returns true when it also ran the out-projection (wo set, the fused merge taken)
 bool attn_decode(const DecodeAttnArgs& a, hipStream_t st);
 // dst row (cursor*mult + r) = src row r, r < rows (16-B aligned rows of width_bytes).
 void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes, void* dst, int64_t ld_dst_bytes,

@@ -211,14 +211,12 @@ constexpr int LS_WS = LS_H + 16;     // bf16 LDS row stride of the W slice (conf
 constexpr int LS_MAXMT = 6;
 constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (256 B: own L2 line)
 
-// GR (round 5, opt-in SDIAR_LSTM_GRANULE=1): the h exchange on the data-tagged transport of
-// lstm_granule_probe_kernel -- a lane publishes its 4 units as two 8-byte {bf16 x 2, tag} granules in one 16-B
-// sc1 store, every wave polls exactly the granules of its next MFMA operand until they carry the step's tag; no
-// counter, no barrier, no vmcnt(0) drain in the step loop.  hx then holds [parity][d][Bp][H / 2] granules.
+// (Round 5 also ran this exchange on the data-tagged granule transport of lstm_granule_probe_kernel: slower,
+// C1 10.8 vs 7.1 ms, deleted in round 6; the probe kernel stays as the transport's price.)
 // WV (round 5, default for an even MT): 8 waves per workgroup instead of 4 -- two waves per 16-unit tile, each
 // on half of the group's row tiles (tile j * 2 + (wave >> 2)), so every SIMD holds two waves of the step and one's
 // gx loads, transcendentals and stores overlap the other's MFMAs; W slice, counters and exchange are unchanged.
-template <int MT, bool GR = false, int WV = 4>
+template <int MT, int WV = 4>
 __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
@@ -228,7 +226,6 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   constexpr int H = LS_H, BB = 16 * MT, NT = 64 * WV, WPU = WV / 4, MTW = MT / WPU;
   static_assert(WV == 4 || WV == 8, "4 or 8 waves");
   static_assert(MT % WPU == 0, "the row tiles split evenly over the waves of a unit tile");
-  static_assert(!GR || WV == 4, "granule transport: 4 waves");
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, wt = tid >> 8;
   const int l15 = lane & 15, g = lane >> 4;
@@ -274,22 +271,8 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   int max_len = 0;
   for (int b = b0; b < min(B, b0 + BB); ++b) max_len = max(max_len, lengths ? lengths[b] : T);
 
-  // granule form: h_t carries tag t + 2 (h_{-1}: 1; the buffer is zeroed per launch) in parity tag & 1
-  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * 4), 0x00020000);
-  auto g_off = [&](int parity, int b, int granule) {   // byte offset of an 8-byte granule
-    return (uint32_t)(((int64_t)parity * plane / 2 + ((int64_t)d * Bp + b) * (H / 2) + granule) * 8);
-  };
   // Publish this workgroup's slice of h (rows b0.., units ub..ub+3 per lane), then count.
   auto publish = [&](int parity) {
-    if constexpr (GR) {
-      const uint32_t tag = (uint32_t)parity;   // GR: the argument is the tag
-#pragma unroll
-      for (int mt = 0; mt < MTW; ++mt) {
-        const u32x4_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), tag, pack_bf16x2(hr[mt][2], hr[mt][3]), tag};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rg, g_off(tag & 1, rb(mt), ub / 2), 0, 16);   // sc1
-      }
-      return;
-    }
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt) {
       const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
@@ -319,7 +302,7 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below the poll
   };
 
-  publish(GR ? 1 : 0);   // h_{-1}
+  publish(0);   // h_{-1}
   for (int step = 0; step < max_len; ++step) {
     // gx of this step for the lane's rows: 4 gates x 4 units (float4), issued before the wait.
     float4 gxv[MTW][4];
@@ -340,34 +323,6 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
     bf16x8 hfa[MTW][H / 32];
-    if constexpr (GR) {
-      // poll exactly this lane's operand granules (units kc * 32 + 8 g .. + 7 of its rows) for h_{step-1}'s tag
-      const uint32_t want = (uint32_t)step + 1u;
-      unsigned spins = 0;
-      for (;;) {
-        asm volatile("" ::: "memory");   // re-read on every poll
-        bool ok = true;
-#pragma unroll
-        for (int kc = 0; kc < H / 32; ++kc)
-#pragma unroll
-          for (int mt = 0; mt < MTW; ++mt) {
-            const u32x4_t lo = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, rb(mt), (kc * 32 + 8 * g) / 2), 0, 16);
-            const u32x4_t hi = __builtin_amdgcn_raw_buffer_load_b128(rg, g_off(want & 1, rb(mt), (kc * 32 + 8 * g) / 2 + 2), 0, 16);
-            ok &= lo[1] == want && lo[3] == want && hi[1] == want && hi[3] == want;
-            const u32x4_t v = {lo[0], lo[2], hi[0], hi[2]};
-            hfa[mt][kc] = __builtin_bit_cast(bf16x8, v);
-          }
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-        // a peer that never publishes (broken co-residency) must not hang the GPU: bounded, and once any wave
-        // gave up every later poll returns at once
-        if (++spins >= spin_limit ||
-            ((spins & 1023) == 1023 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    } else {
     wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
     // every h fragment of the step requested at once (one L2 round trip, not one per k-step;
     // s_memtime stamps: 5.1 k of a 10 k-cycle C1 step went to eight serial load -> MFMA waits)
@@ -377,7 +332,6 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
       for (int mt = 0; mt < MTW; ++mt)
         hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                      rh, hx_off(pin, rb(mt), kc * 32 + 8 * g), 0, 16));
-    }
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MTW];
@@ -419,7 +373,7 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
         *reinterpret_cast<float4*>(out + ((int64_t)b * T + t) * ldo + d * H + ub) =
             make_float4(hr[mt][0], hr[mt][1], hr[mt][2], hr[mt][3]);
     }
-    publish(GR ? step + 2 : (step + 1) & 1);   // h_step
+    publish((step + 1) & 1);   // h_step
   }
   // A timed-out poll (co-residency lost) means some h was consumed stale: poison every output of
   // this workgroup so the failure is loud (NaN), besides the err word the host reads back.
@@ -562,30 +516,25 @@ unsigned lstm_spin_limit() {
   return launches++ < n_forced ? v : (1u << 22);
 }
 
-template <int MT, bool GR, int WV = 4>
+template <int MT, int WV = 4>
 void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                          const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
                          uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, GR, WV>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, GR, WV>), dim3(4 * groups), dim3(64 * WV), smem, st, gx, B, T, ndir,
+  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, WV>), dim3(4 * groups), dim3(64 * WV), smem, st, gx, B, T, ndir,
                      reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
                      counters, err, lstm_spin_limit(), host_err);
   SD_LAUNCH_CHECK();
 }
 
-bool lstm_granule_mode() {
-  static const bool v = getenv("SDIAR_LSTM_GRANULE") != nullptr && atoi(getenv("SDIAR_LSTM_GRANULE")) != 0;
-  return v;
-}
-
-// Workgroups of lstm_group_bf16_kernel<MT, false, WV> the occupancy query admits per CU (0 if none fit).
+// Workgroups of lstm_group_bf16_kernel<MT, WV> the occupancy query admits per CU (0 if none fit).
 // This is the check hipLaunchCooperativeKernel would make (MI355X guide, "Residency and
 // cooperative launch": a plain launch of the same grid has the same residency); a cooperative
 // launch itself is avoided because its queue's teardown crashes rocprofv3's exit path here.
@@ -594,25 +543,23 @@ int lstm_group_blocks_per_cu() {
   static int nb = -1;
   if (nb < 0) {
     const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, false, WV>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int v = 0;
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, false, WV>, 64 * WV, smem));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, WV>, 64 * WV, smem));
     nb = v;
   }
   return nb;
 }
 
-// 8 waves per workgroup (the default; SDIAR_LSTM_WV=4 keeps 4): only for an even row-tile count and the counter
-// exchange, and only when the occupancy query admits the 512-thread workgroup.  C2 (600 windows x 2 directions,
-// 2 row tiles per group): recurrence 929 -> 777 us per launch (tools/gpu_r05y.sh).
+// 8 waves per workgroup for an even row-tile count, when the occupancy query admits the 512-thread workgroup
+// (else 4).  C2 (600 windows x 2 directions, 2 row tiles per group): recurrence 929 -> 777 us per launch (round 5).
 template <int MT>
 bool lstm_group_wv8() {
   if constexpr (MT % 2 != 0) {
     return false;
   } else {
-    static const int wv = getenv("SDIAR_LSTM_WV") ? atoi(getenv("SDIAR_LSTM_WV")) : 8;
-    return wv == 8 && !lstm_granule_mode() && lstm_group_blocks_per_cu<MT, 8>() >= 1;
+    return lstm_group_blocks_per_cu<MT, 8>() >= 1;
   }
 }
 
@@ -622,17 +569,13 @@ void launch_lstm_group(const float* gx, int B, int T, int ndir, const void* whh_
                        uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
   if constexpr (MT % 2 == 0) {
     if (lstm_group_wv8<MT>()) {
-      launch_lstm_group_t<MT, false, 8>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters,
+      launch_lstm_group_t<MT, 8>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters,
                                         err, host_err, st);
       return;
     }
   }
-  if (lstm_granule_mode())
-    launch_lstm_group_t<MT, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err,
-                                  host_err, st);
-  else
-    launch_lstm_group_t<MT, false>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err,
-                                   host_err, st);
+  launch_lstm_group_t<MT>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err,
+                          host_err, st);
 }
 
 int lstm_group_capacity(int mt) {
@@ -656,17 +599,14 @@ int lstm_group_mt(int B, int ndir) {
   // Smallest row block (16 * MT) whose 4 x groups fit one workgroup per CU, provided the occupancy
   // query admits the kernel at all (co-residency of every workgroup of the grid); else 0 and the
   // caller takes the per-step launches.
-  // SDIAR_LSTM_MT=<m> (diagnostic A/B): at least m row tiles per group
-  static const int mt_min = getenv("SDIAR_LSTM_MT") ? std::max(1, std::min(LS_MAXMT, atoi(getenv("SDIAR_LSTM_MT")))) : 1;
-  for (int m = mt_min; m <= LS_MAXMT; ++m)
+  for (int m = 1; m <= LS_MAXMT; ++m)
     if (4 * ndir * cdiv(B, 16 * m) <= n_cu) return lstm_group_capacity(m) >= 1 ? m : 0;
   return 0;
 }
 
 // Layout of the persistent kernel's scratch inside the caller's `work`: the double-buffered bf16
 // h exchange, then (16-B aligned) one counter per group and the err word.
-// (sized for the granule form: 4 bytes per exchanged value instead of 2)
-size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 4 + 15) / 16 * 16; }
+size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
 
 }  // namespace
 
@@ -754,7 +694,6 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       uint16_t* hx = reinterpret_cast<uint16_t*>(work);
       unsigned* ctl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(work) + hx_bytes);
       zero_fill(ctl, ctl_bytes, st);
-      if (lstm_granule_mode()) zero_fill(hx, hx_bytes, st);   // no stale tag of an earlier launch may match
       ProfScope prof("lstm_recurrence", 2.0 * ndir * B * T * 4.0 * H * H,
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       prof.set_steps(T);   // sequential steps (an upper bound with packed lengths: the launch runs max(len))

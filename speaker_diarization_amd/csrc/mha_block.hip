@@ -66,7 +66,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// PROBE (timing diagnostics, SDIAR_MHA_VARIANT 8-10, wrong outputs): bit 0 skips the attention phase, bit 1 the
+// PROBE (timing diagnostics, sd_op_mha_block variants 8-10, wrong outputs): bit 0 skips the attention phase, bit 1 the
 // projection MFMAs
 template <int SEQ, int W, int NSLOT, int QS, int PROBE = 0>
 __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
@@ -343,13 +343,12 @@ void mha_block(const MhaBlockArgs& a, hipStream_t st, int variant) {
   const double flops = 2.0 * rows * 3 * kD * kD + 4.0 * a.S * (double)a.T * a.T * kD;
   const double bytes = rows * kD * (2.0 + 2.0) + 2.0 * 3 * kD * kD;
   ProfScope prof("mha_block", flops, bytes, st);
-  // SDIAR_MHA_SEQ2=1: the rounds 2-4 layout (two sequences per 8-wave workgroup, one workgroup per CU);
-  // SDIAR_MHA_VARIANT (diagnostic): 2 <1,4,2,64>, 3 <1,4,2,48>, 4 <1,4,3,48>, 5 <1,8,3,64>, 6 <1,8,2,48>, 7 <2,8,4,48>
+  // variant (sd_op_mha_block, tests / probes only; the product passes -1 = 0): 1 <2,8,3,64> (rounds 2-4),
+  // 2 <1,4,2,64>, 3 <1,4,2,48>, 4 <1,4,3,48>, 5 <1,8,3,64>, 6 <1,8,2,48>, 7 <2,8,4,48>
   // Round 5 sweep on C2 (ms per step, one box, 2-3 rounds): <2,8,3,48> 26.39-26.79 (shipped), <1,4,2,48> 26.53-26.97,
   // <2,8,4,48> 26.55-26.61, <2,8,3,64> 27.15-27.18, <1,8,2,48> 28.35-28.42, <1,8,3,64> 28.83-28.90,
   // <1,4,2,64> / <1,4,3,48> 29.26-29.36 (over 80 KiB: one 4-wave workgroup per CU)
-  static const int var_env = getenv("SDIAR_MHA_SEQ2") ? 1 : getenv("SDIAR_MHA_VARIANT") ? atoi(getenv("SDIAR_MHA_VARIANT")) : 0;
-  const int var = variant >= 0 ? variant : var_env;
+  const int var = variant >= 0 ? variant : 0;
   switch (var) {
     case 1: launch_mha<2, 8, 3, 64>(a, st); break;
     case 2: launch_mha<1, 4, 2, 64>(a, st); break;

@@ -1100,15 +1100,13 @@ void glu_dwconv(const void* x, int S, int T, int C, const float* w, const float*
   dim3 grid(cdiv(C, kDwCB), S);
   const double eb = io_bf16 ? 2.0 : 4.0;
   ProfScope prof(glu_in ? "glu_dwconv" : "dwconv", 2.0 * S * T * C * k, eb * S * T * (glu_in ? 3.0 : 2.0) * C, st);
-  static const bool no_pk = getenv("SDIAR_NO_DWCONV_PK") != nullptr;   // A/B switch: the runtime-k kernel
-  static const bool no_pp = getenv("SDIAR_NO_DWCONV_PP") != nullptr;   // A/B switch: one workgroup per sequence
-  if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk && !no_pp && !glu_in && T <= 8 * 19) {
+  if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !glu_in && T <= 8 * 19) {
     auto xp = reinterpret_cast<const uint16_t*>(x);
     auto yp = reinterpret_cast<uint16_t*>(y);
     const int R = T <= 8 * 9 ? 9 : T <= 8 * 13 ? 13 : 19;
     if (k == 31) launch_dwconv_pp<31>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
     else launch_dwconv_pp<15>(R, S, T, C, st, xp, w, bias, yp, partial, (int)fused_silu);
-  } else if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0 && !no_pk) {
+  } else if (io_bf16 && (k == 15 || k == 31) && C % kDwCB == 0) {
     const int R = dwconv_pk_runlen(T, k);
     auto xp = reinterpret_cast<const uint16_t*>(x);
     auto yp = reinterpret_cast<uint16_t*>(y);

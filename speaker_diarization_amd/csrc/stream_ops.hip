@@ -867,11 +867,7 @@ void kv_append(const void* src, int64_t ld_src_bytes, int rows, int width_bytes,
 }
 
 int attn_decode_blocks(int max_keys) {
-  static const int cap = [] {   // A/B: SDIAR_DECODE_MAXBLK=<1..32> caps the blocks per (sequence, head)
-    const char* e = getenv("SDIAR_DECODE_MAXBLK");
-    return e ? std::max(1, std::min(atoi(e), kMaxBlk)) : kMaxBlk;
-  }();
-  return std::min(cdiv(max_keys, 256), cap);
+  return std::min(cdiv(max_keys, 256), kMaxBlk);
 }
 
 template <bool IOBF, bool FUSED>
@@ -884,14 +880,12 @@ static void launch_decode_q(const DecodeAttnArgs& a, dim3 g1, hipStream_t st) {
 
 template <bool IOBF>
 static bool launch_decode(const DecodeAttnArgs& a, int nblk, hipStream_t st) {
-  static const bool split = getenv("SDIAR_DECODE_SPLIT") != nullptr;   // A/B: the separate combine launch
-  static const bool no_op = getenv("SDIAR_NO_ATTN_OUTPROJ") != nullptr;   // A/B: the out-projection's own GEMM
   const int nsh = a.nseq * a.nh;
   const dim3 g1(nblk, nsh), g2(nsh, cdiv(a.nq, 4));
-  if (a.cnt && !split) {
+  if (a.cnt) {
     // the out-projection merge for one query per sequence (the 1-frame chunks of the latency mode; with more
     // queries its per-query partials push the kernel past the register budget)
-    const bool op = !no_op && a.nq == 1 && a.wo && a.bo && a.o2 && a.ws2 && a.cnt2 && a.nh * kHD <= 256 &&
+    const bool op = a.nq == 1 && a.wo && a.bo && a.o2 && a.ws2 && a.cnt2 && a.nh * kHD <= 256 &&
                     reinterpret_cast<uintptr_t>(a.wo) % 16 == 0;
     if (op) {
       hipLaunchKernelGGL((attn_decode_kernel<IOBF, 1, true, true>), g1, dim3(256), 0, st, a);
@@ -927,9 +921,8 @@ static void launch_slot_block(const SlotBlockArgs& a, hipStream_t st) {
 }
 
 bool stream_slot_block(const SlotBlockArgs& a, hipStream_t st) {
-  static const bool off = getenv("SDIAR_NO_SLOT_BLOCK") != nullptr;   // A/B switch: the three-launch path
   const int n = a.c * a.C;
-  if (off || a.D != kSlotD || a.nh * kHD != a.D || a.nh > 8 || n < 1 || n > kSlotRows || a.C > 8 || !a.ws || !a.cnt)
+  if (a.D != kSlotD || a.nh * kHD != a.D || a.nh > 8 || n < 1 || n > kSlotRows || a.C > 8 || !a.ws || !a.cnt)
     return false;
   ProfScope prof("slot_block", 2.0 * n * a.D * 4.0 * a.D + 4.0 * n * a.C * a.D, (a.w_bf16 ? 2.0 : 4.0) * 4 * a.D * a.D, st);
   if (n <= 2) launch_slot_block<2>(a, st);
@@ -953,8 +946,7 @@ static void launch_ffn_pair(const FfnPairArgs& a, hipStream_t st) {
 }
 
 bool stream_ffn_pair(const FfnPairArgs& a, hipStream_t st) {
-  static const bool off = getenv("SDIAR_NO_FFN_PAIR") != nullptr;   // A/B switch: l1 and l2 as two skinny GEMMs
-  if (off || a.D != kSlotD || a.F != 2048 || a.n < 1 || a.n > 8 || !a.ws || !a.cnt || !a.ln_g || !a.ln_b || !a.ln_out)
+  if (a.D != kSlotD || a.F != 2048 || a.n < 1 || a.n > 8 || !a.ws || !a.cnt || !a.ln_g || !a.ln_b || !a.ln_out)
     return false;
   auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
   if (!al(a.w1) || !al(a.w2) || !al(a.ln_x) || !al(a.ln_out) || !al(a.out) || !al(a.ws) || !al(a.b2)) return false;

@@ -117,7 +117,6 @@ void TsvadModel::alloc_workspace() {
 }
 
 TsvadModel::~TsvadModel() {
-  for (hipEvent_t e : ev_slice_) (void)hipEventDestroy(e);
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
   if (side_) (void)hipStreamDestroy(side_);
@@ -240,35 +239,7 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
                         s, &io);
   };
   if (fused_v1) SD_CHECK(std::abs(T3 - Tl) <= 3, kErrShape, "label and ref_speech(mix speech) diff: " + std::to_string(T3 - Tl));
-  // SDIAR_SLICES=K (K >= 2): the per-window part as K window slices PIPELINED over the two streams: the caller's
-  // stream runs every slice's CAM++ trunk, speech_down conv and gsp_fc back to back; side_ runs slice i's conformer
-  // stack once slice i's trunk is done (an event per slice), so slice i's MFMA-bound conformer overlaps slice
-  // i + 1's HBM-bound trunk and only the first trunk and the last conformer run alone.
-  static const int n_slices = getenv("SDIAR_SLICES") ? std::max(0, atoi(getenv("SDIAR_SLICES"))) : 0;
-  if (fused_v1 && two && n_slices >= 2) {
-    const int K = std::min(n_slices, 8);
-    while ((int)ev_slice_.size() < K) {
-      hipEvent_t e = nullptr;
-      SD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ev_slice_.push_back(e);
-    }
-    SD_HIP(hipEventRecord(ev_fork_, st));
-    SD_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-    for (int i = 0; i < K; ++i) {
-      const int b0 = (int)((int64_t)B * i / K), Bh = (int)((int64_t)B * (i + 1) / K) - b0;
-      const Tens x4s = cam_.forward(ref, Bh, Tf, st, b0);
-      float* mx = mix_ + (int64_t)b0 * T3 * SE;
-      conv_gemm(cam_conv1d(x4s, Bh, T2, CamTrunk::kChannels, down_, 2, 2, 1, Tens{mx, false}, SE), bf, st);
-      BnRelu sb = sd_bn;
-      sb.win0 = b0;
-      gsp_fc(mx, Bh * T3, SE, SE, gsp_w_, gsp_b_, SE, mixg_ + (int64_t)b0 * T3 * SE, SE, st, sb, T3);
-      SD_HIP(hipEventRecord(ev_slice_[i], st));
-      SD_HIP(hipStreamWaitEvent(side_, ev_slice_[i], 0));
-      conformer_slice(b0, Bh, side_);
-    }
-    SD_HIP(hipEventRecord(ev_join_, side_));
-    SD_HIP(hipStreamWaitEvent(st, ev_join_, 0));
-  } else if (fused_v1 && two) {
+  if (fused_v1 && two) {
     // Two window slices, each through the whole per-window part of the model on its own stream: CAM++ trunk,
     // speech_down conv, gsp_fc, conformer stack.  Nothing joins between the trunk and the conformer, so one
     // slice's HBM-bound CAM++ kernels overlap the other's MFMA-bound conformer programs (bit-identical per

@@ -87,7 +87,6 @@ class TsvadModel {
   // workgroups leaves idle (cam_dense: 600 items on 256 CUs = 2.34 rounds of 3).
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
-  std::vector<hipEvent_t> ev_slice_;   // pipelined slices (SDIAR_SLICES): slice i's trunk done
 
   // Workspace.
   float *mix_ = nullptr, *mixg_ = nullptr;

@@ -273,227 +273,3 @@ def test_audio_stream_reset_modes_and_errors(gpu):
     s.set_audio()
     with pytest.raises(SdiarError, match="audio"):
         s._push_rows(f[:3])
-
-
-SPLIT = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-import tests.test_gpu_fseend_stream as t
-from tests.golden.make_golden import eda_inputs
-m = t._model(806, {prec!r}, max_frames=1100)
-x = torch.from_numpy(eda_inputs([1100], seed=86)[0]).cuda()
-out, _ = t._stream_all(m, x, 1)
-torch.save(out.cpu(), {path!r})
-"""
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_decode_attention_fused_combine_bit_identical(gpu, precision, tmp_path):
-    """attn_decode's last block merges the partials in the same launch (write-through partials + a
-    per-(sequence, head) counter) with the separate combine launch's arithmetic: the 1-frame-chunk stream
-    over 1100 frames (5 key blocks) is bit-identical with SDIAR_DECODE_SPLIT=1 (child processes: the switch is
-    read once) and, on the way, every counter stays a multiple of the block count across 2 x 1100 x 6 launches."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    outs = []
-    for split in (None, "1"):
-        env = dict(os.environ)
-        env.pop("SDIAR_DECODE_SPLIT", None)
-        env["SDIAR_NO_ATTN_OUTPROJ"] = "1"   # the out-projection's own GEMM in both (its fused merge: test below)
-        if split:
-            env["SDIAR_DECODE_SPLIT"] = split
-        path = str(tmp_path / f"o_{split}.pt")
-        r = subprocess.run([sys.executable, "-c", SPLIT.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        outs.append(torch.load(path, weights_only=True))
-    assert torch.equal(outs[0], outs[1])
-
-
-SLOT = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-import tests.test_gpu_fseend_stream as t
-from tests.golden.make_golden import eda_inputs
-m = t._model(807, {prec!r}, max_frames=400)
-x = torch.from_numpy(eda_inputs([400], seed=87)[0]).cuda()
-out, _ = t._stream_all(m, x, 1)
-ref, _, _ = m.test([x], [400], max_nspks=6)
-torch.save((out.cpu(), ref[0].cpu()), {path!r})
-"""
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_slot_block_matches_three_launches(gpu, precision, tmp_path):
-    """stream_slot_block (in2 + slot attention + out2 in one launch, the per-head out-projection partials merged
-    by the last workgroup) against the three launches (SDIAR_NO_SLOT_BLOCK=1, child processes: the switch is read
-    once): both streams match test() within the stream tolerances, and each other within 1e-5 (fp32: the same
-    fp32 arithmetic in another summation order) / 1e-2 (bf16: the fused block keeps q, k, v and the attention
-    output in fp32)."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = []
-    for off in (None, "1"):
-        env = dict(os.environ)
-        env.pop("SDIAR_NO_SLOT_BLOCK", None)
-        if off:
-            env["SDIAR_NO_SLOT_BLOCK"] = off
-        path = str(tmp_path / f"s_{off}.pt")
-        r = subprocess.run([sys.executable, "-c", SLOT.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res.append(torch.load(path, weights_only=True))
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
-    for out, ref in res:
-        np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=tol)
-    d = float((res[0][0] - res[1][0]).abs().max())
-    assert d <= (1e-5 if precision == "fp32" else 1e-2), d
-
-
-PRO = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-import tests.test_gpu_fseend_stream as t
-from tests.golden.make_golden import eda_inputs
-m = t._model(808, {prec!r}, max_frames=300)
-x = torch.from_numpy(eda_inputs([300], seed=88)[0]).cuda()
-outs = [t._stream_all(m, x, c)[0].cpu() for c in (1, 2)]
-torch.save(outs, {path!r})
-"""
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_gemm_prologues_bit_identical(gpu, precision, tmp_path):
-    """The decoder's window gather, embedding L2 norm and slot init run as A prologues of the skinny GEMMs
-    that consume them (gemm_skinny pro_mode 3 / 1 / 2) with the same arithmetic as gather_window, row_l2norm
-    and slot_init: the streams (chunks of 1 and 2 frames) are bit-identical with SDIAR_NO_STREAM_PRO=1."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = []
-    for off in (None, "1"):
-        env = dict(os.environ)
-        env.pop("SDIAR_NO_STREAM_PRO", None)
-        if off:
-            env["SDIAR_NO_STREAM_PRO"] = off
-        path = str(tmp_path / f"p_{off}.pt")
-        r = subprocess.run([sys.executable, "-c", PRO.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res.append(torch.load(path, weights_only=True))
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
-
-
-AUD = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-import tests.test_gpu_fseend_stream as t
-m = t._model(809, {prec!r}, max_frames=400)
-wav = t._wav8k(20.0, 96, 11)
-outs = [t._audio_stream(m, wav, c, [640])[0].cpu() for c in (1, 2)]
-torch.save(outs, {path!r})
-"""
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_audio_fusions_bit_identical(gpu, precision, tmp_path):
-    """The c = 1 audio chunk's STFT / logmel / splice in one workgroup (stft_logmel_kernel SPLICE) and the
-    encoder + decoder chunks in one captured graph per steady-state push: 80-ms audio streams (chunks 1 and
-    2) are bit-identical with SDIAR_FRONTEND_TWO_LAUNCH=1 SDIAR_NO_COMBINED_GRAPH=1 (the two-launch frontend,
-    one graph per chunk)."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = []
-    for off in (None, "1"):
-        env = dict(os.environ)
-        for k in ("SDIAR_FRONTEND_TWO_LAUNCH", "SDIAR_NO_COMBINED_GRAPH"):
-            env.pop(k, None)
-            if off:
-                env[k] = off
-        path = str(tmp_path / f"a_{off}.pt")
-        r = subprocess.run([sys.executable, "-c", AUD.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res.append(torch.load(path, weights_only=True))
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
-
-
-FFN = r"""
-import sys, torch
-sys.path.insert(0, {repo!r})
-import tests.test_gpu_fseend_stream as t
-from tests.golden.make_golden import eda_inputs
-m = t._model(810, {prec!r}, max_frames=400)
-x = torch.from_numpy(eda_inputs([400], seed=89)[0]).cuda()
-outs = [t._stream_all(m, x, c)[0].cpu() for c in (1, 2)]
-ref, _, _ = m.test([x], [400], max_nspks=6)
-torch.save((outs, ref[0].cpu()), {path!r})
-"""
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_ffn_pair_matches_two_launches(gpu, precision, tmp_path):
-    """stream_ffn_pair (LN + linear1 + relu + linear2 in one launch, the down-projection's split-K partials merged
-    by the last workgroup in workgroup order) against the two skinny GEMMs (SDIAR_NO_FFN_PAIR=1, child processes):
-    chunk 1 runs it for the encoder (1 row, 128 workgroups) and the decoder (6 rows, 64 workgroups), chunk 2 for the
-    encoder's 2 rows (the decoder's 12 rows take the two-launch path); every stream matches test() within the stream
-    tolerances and the two paths agree within 1e-5 (fp32: another summation order) / 2e-2 (bf16: the fused hidden
-    layer stays fp32, the two-launch path stores it as bf16)."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = []
-    for off in (None, "1"):
-        env = dict(os.environ)
-        env.pop("SDIAR_NO_FFN_PAIR", None)
-        if off:
-            env["SDIAR_NO_FFN_PAIR"] = off
-        path = str(tmp_path / f"f_{off}.pt")
-        r = subprocess.run([sys.executable, "-c", FFN.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res.append(torch.load(path, weights_only=True))
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
-    for outs, ref in res:
-        for o in outs:
-            np.testing.assert_allclose(o.numpy(), ref.numpy(), atol=tol)
-    for a, b in zip(res[0][0], res[1][0]):
-        d = float((a - b).abs().max())
-        assert d <= (1e-5 if precision == "fp32" else 2e-2), d
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_attn_outproj_matches_gemm(gpu, precision, tmp_path):
-    """attn_decode with the out-projection in its merge (1-query chunks: each (sequence, head)'s merging block
-    publishes its head's out-projection partial, the last head of the sequence sums them in head order + bias)
-    against the attention followed by the skinny out-projection GEMM (SDIAR_NO_ATTN_OUTPROJ=1, child processes):
-    chunk 1 takes it in all 4 encoder layers and both decoder applications, chunk 2 never; every stream matches
-    test() within the stream tolerances and the two paths agree within 1e-5 (fp32) / 2e-2 (bf16: the fused
-    path projects the fp32 attention output, the GEMM path its bf16 copy)."""
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = []
-    for off in (None, "1"):
-        env = dict(os.environ)
-        env.pop("SDIAR_NO_ATTN_OUTPROJ", None)
-        if off:
-            env["SDIAR_NO_ATTN_OUTPROJ"] = off
-        path = str(tmp_path / f"o_{off}.pt")
-        r = subprocess.run([sys.executable, "-c", FFN.format(repo=repo, prec=precision, path=path)], env=env,
-                           capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res.append(torch.load(path, weights_only=True))
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
-    for outs, ref in res:
-        for o in outs:
-            np.testing.assert_allclose(o.numpy(), ref.numpy(), atol=tol)
-    for a, b in zip(res[0][0], res[1][0]):
-        d = float((a - b).abs().max())
-        assert d <= (1e-5 if precision == "fp32" else 2e-2), d
-    assert torch.equal(res[0][0][1], res[1][0][1])   # chunk 2: the same launches in both runs

@@ -1,9 +1,9 @@
 """mha_block (the C2 conformer's in-projection + multi-head attention in one launch, mha_block.hip) through
 sd_op_mha_block against a plain torch fp32 restatement of torchaudio's MHA core (ts_vad2/model.py:259-267 ->
 torch.nn.MultiheadAttention: q/k/v = y W^T + b, softmax(q k^T / sqrt(48)) v per head, key_padding_mask from
-the lengths), on bf16 inputs.  Both kernel layouts (0: one sequence per 4-wave workgroup, two workgroups per
-CU; 1: two sequences per 8-wave workgroup) must agree with the reference within bf16 rounding and with each
-other bit for bit."""
+the lengths), on bf16 inputs.  Every kernel layout sd_op_mha_block can launch (0: the shipped <SEQ 2, 8 waves,
+3-slot ring, 48-wide Q / K rows>; 1-7: the round-5 sweep's other layouts, mha_block.hip) must agree with the
+reference within bf16 rounding and with each other bit for bit."""
 import numpy as np
 import pytest
 import torch
