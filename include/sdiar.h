@@ -431,6 +431,11 @@ int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const
 /* Diagnostics: while `stamps` (device, >= 16 u64 per workgroup of a launch) is non-NULL, every cam_dense
  * launch records its workgroups' phase-boundary s_memrealtime stamps there (tools/cam_dense_probe.py). */
 int sd_debug_cam_dense_probe(void* stamps);
+/* Diagnostics: while `stamps` (device, >= 64 u64 per workgroup, zeroed) is non-NULL, every conformer pw2 + FFN
+ * row-program launch (rowprog.hip, program 5) runs its stamping instantiation: lane 0 of every wave adds the
+ * s_memtime cycles of its phases to stamps[(workgroup * 8 + wave) * 8 + k], k = 0 whole launch, 1 piece waits,
+ * 2 slot-free waits (refills), 3 epilogue, 4 tile loads (tools/rowprog_probe.py). */
+int sd_debug_rowprog_probe(void* stamps);
 /* Diagnostics: a captured graph [memsetAsync(X, 0) -> kernel: Y = X, then X = 7] (fork != 0: the kernel behind
  * an event fork / join of a second captured stream) replayed `replays` times; bad_per_replay (host, replays
  * ints) = Y values that were not 0 after each replay. */

@@ -730,6 +730,10 @@ int sd_debug_cam_dense_probe(void* stamps) {
   return guard([&] { sd::cam_dense_set_probe(stamps); });
 }
 
+int sd_debug_rowprog_probe(void* stamps) {
+  return guard([&] { sd::rowprog_set_probe(stamps); });
+}
+
 int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const float* s1, const float* h1,
                     const float* wb, const float* a2, const float* b2, const float* wl, const float* bl,
                     const float* w1, const float* c1, const float* w2, const float* c2, void* out, int repeats,

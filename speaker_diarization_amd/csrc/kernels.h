@@ -145,6 +145,7 @@ bool cam_dense_supported(int T, int cin, int ld, int bn, int C1, int C2, int N, 
                          bool bf16);
 size_t cam_dense_record_bytes(int B);
 void cam_dense_set_probe(void* stamps);
+void rowprog_set_probe(void* stamps);
 // Graph-replay diagnostic (diag.hip): [memset(X, 0) -> kernel Y = X; X = 7] replayed `replays` times;
 // bad_per_replay[r] = non-zero Y values after replay r (host array).
 void graph_memset_probe(int n, int replays, bool fork, int* bad_per_replay, hipStream_t st);   // test-only phase stamps ([grid][16] u64), null = off
@@ -275,6 +276,9 @@ struct RowProgArgs {
   // start offset of the odd workgroups, in s_sleep(64) units (set by rowprog()):
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
+  // diagnostics (sd_debug_rowprog_probe): per wave, lane 0 accumulates s_memtime cycles of the tile's phases
+  // into probe[(block * 8 + wave) * 8 + k] (k: 0 whole, 1 piece waits, 2 slot-free waits, 3 epilogue, 4 loads)
+  unsigned long long* probe = nullptr;
   // X / Xo in the MFMA-tiled layout (M % 16 == 0): 16-row group g, feature f = 16 ft + 4 q + r of row 16 g + l at
   // float ((g * 24 + ft) * 64 + l + 16 q) * 4 + r -- each wave's 16 x 384 fp32 residual block is 24 contiguous
   // 1-KiB runs, one per load / store instruction (row-major it is 16 scattered 64-B pieces per instruction).  The

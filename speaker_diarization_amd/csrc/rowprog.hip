@@ -24,8 +24,13 @@
 //
 // Weights stream from L2 as 24-KiB pieces of 24 pre-packed 1-KiB MFMA fragments (lane-linear, so every
 // ds_read_b128 is conflict-free) through a 5-slot LDS ring (global_load_lds, 4 pieces in flight, counted
-// vmcnt waits, one barrier per piece).  The workgroups are persistent over tiles; the ring runs across tile
-// boundaries, so the next tile's first weights are in flight during the current tile's epilogue.
+// vmcnt waits).  The workgroups are persistent over tiles; the ring runs across tile boundaries, so the next
+// tile's first weights are in flight during the current tile's epilogue.  Slot hand-off (kFlagRing, round 6):
+// per-slot FULL / FREE words in LDS instead of one workgroup barrier per piece -- a wave publishes FULL for
+// piece g + 1 once its own share of g + 1 has landed (counted vmcnt) as it starts piece g, and FREE for piece
+// g - 1 as it starts piece g (every read of g - 1 was consumed by an MFMA of g - 1); it waits for FULL(g) from
+// all 8 waves before reading piece g, and for FREE(g - 1) from all 8 before refilling that slot.  So the 8 waves
+// may drift by about a piece instead of meeting at every piece (kFlagRing = false: the barrier form).
 // MFMA accumulators in the VGPR form (the 2-tile layout spilled to scratch with the default AGPR form)
 // sdiar-build: -mllvm -amdgpu-mfma-vgpr-form=1
 #include <cstring>
@@ -52,9 +57,13 @@ constexpr int kRefillAt = 3;          // the DMA refill is issued after this man
 constexpr int kPrmFfn = 3 * kD + kMaxHidden;
 constexpr int kPrmB0 = 0, kPrmFfn0 = kD, kPrmY = kD + 2 * kPrmFfn;
 constexpr int kPrmGn = kPrmY + 2 * kD;   // GroupNorm gamma | beta of the pre-GEMM's A transform
+constexpr int kPrmFlags = kPrmGn + 2 * kD;   // FULL[kNSlot] | FREE[kNSlot] counters (uint32, in the padding)
 constexpr int kPrmFloats = (kPrmGn + 2 * kD + 255) / 256 * 256;   // padded to whole KiB
+constexpr bool kFlagRing = true;
+constexpr unsigned kFlagSpin = 1u << 16;   // poll bound: a wave that never publishes must not hang the GPU
 constexpr size_t kSmemBytes = sizeof(uint16_t) * (size_t)kNSlot * kPiece + sizeof(float) * kPrmFloats;
 static_assert((kPrmFloats * 4) % 1024 == 0, "ring slots stay 1-KiB aligned");
+static_assert(kPrmFlags + 2 * kNSlot <= kPrmFloats, "the slot counters fit the parameter block's padding");
 static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -75,6 +84,19 @@ __device__ __forceinline__ void wait_piece(int younger) {
 
 __device__ __forceinline__ float silu(float v) { return v * sigmoid_rcp(v); }
 
+// LDS slot counters (inline asm: the compiler neither reorders them with the ring's fragment reads nor puts
+// vmcnt drains in front of them).  One lane adds; every lane polls the same word (uniform value).
+__device__ __forceinline__ void lds_count(uint32_t addr, int lane) {
+  if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
+}
+__device__ __forceinline__ void lds_wait_ge(uint32_t addr, uint32_t target) {
+  for (unsigned spins = 0; spins < kFlagSpin; ++spins) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+  }
+}
+
 // TT 16-token MFMA column tiles per wave; 8 / TT waves per 128-token tile.
 template <int TT>
 struct Ring {
@@ -88,6 +110,7 @@ struct Ring {
   int total;    // pieces this workgroup consumes
   int w, lane;
   bool dma;     // probe: false skips the weight stream
+  uint32_t full, free_;   // LDS byte addresses of FULL[0] / FREE[0]
 
   __device__ __forceinline__ const uint16_t* src(int q) const {
     if (q < n_pre) return w0 + (size_t)q * kPiece;
@@ -97,6 +120,8 @@ struct Ring {
   }
   __device__ __forceinline__ void issue(int g) const {
     if (g >= total || !dma) return;
+    // flag ring: the slot's previous piece (g - kNSlot) must be consumed by every wave
+    if (kFlagRing && g >= kNSlot) lds_wait_ge(free_ + 4 * (g % kNSlot), (uint32_t)(kWaves * (g / kNSlot)));
     const uint16_t* s = src(g % P);
     uint16_t* slot = ring + (g % kNSlot) * kPiece;
 #pragma unroll
@@ -105,9 +130,24 @@ struct Ring {
       dma_lds16(s + f * kFrag + lane * 8, (lds_ptr_t)(slot + f * kFrag));
     }
   }
+  // First piece (flag ring): this wave's share of piece 0 landed -> FULL(0).
+  __device__ __forceinline__ void start() const {
+    if (!kFlagRing || total <= 0) return;
+    if (dma) wait_piece<kDpw>(min(kNSlot - 2, total - 1));
+    lds_count(full, lane);
+  }
   // Wait for piece g and make every wave's part visible; returns g's slot.  The slot of piece g - 1 is
   // free from here on: refill(g) (called a few MFMAs into the piece) streams piece g + kNSlot - 1 into it.
   __device__ __forceinline__ const uint16_t* wait(int g) const {
+    if constexpr (kFlagRing) {
+      if (g + 1 < total) {   // this wave's share of piece g + 1 (issued up to g + 3 so far) landed -> FULL(g + 1)
+        if (dma) wait_piece<kDpw>(min(kNSlot - 3, total - 2 - g));
+        lds_count(full + 4 * ((g + 1) % kNSlot), lane);
+      }
+      if (g >= 1) lds_count(free_ + 4 * ((g - 1) % kNSlot), lane);   // piece g - 1's reads are consumed
+      lds_wait_ge(full + 4 * (g % kNSlot), (uint32_t)(kWaves * (g / kNSlot + 1)));
+      return ring + (g % kNSlot) * kPiece;
+    }
     wait_piece<kDpw>(min(kNSlot - 2, total - 1 - g));
     // plain s_barrier: __syncthreads()' workgroup fence waits for vmcnt(0) and would drain the ring
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -201,6 +241,7 @@ void rowprog_kernel(RowProgArgs a) {
   cp(kPrmY + kD, a.y_b, kD);
   cp(kPrmGn, a.gn_g, kD);
   cp(kPrmGn + kD, a.gn_b, kD);
+  if (tid < 2 * kNSlot) reinterpret_cast<uint32_t*>(prm)[kPrmFlags + tid] = 0u;
   __syncthreads();
 
   const int ntiles = (a.M + kRows - 1) / kRows;
@@ -217,8 +258,35 @@ void rowprog_kernel(RowProgArgs a) {
   R.w = w;
   R.lane = lane;
   R.dma = !(PROBE & 2);
+  R.full = (uint32_t)reinterpret_cast<uintptr_t>(prm + kPrmFlags);
+  R.free_ = R.full + 4 * kNSlot;
+  // PROBE & 8: phase cycles per wave (RowProgArgs::probe)
+  constexpr bool kStamp = (PROBE & 8) != 0;
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+  const unsigned long long st_t0 = kStamp ? __builtin_amdgcn_s_memtime() : 0;
+  auto now = [&]() -> unsigned long long { return kStamp ? __builtin_amdgcn_s_memtime() : 0ull; };
   for (int g = 0; g < kNSlot - 1; ++g) R.issue(g);
+  R.start();
   int g = 0;
+  auto pwait = [&](int q) {
+    if constexpr (kStamp) {
+      const unsigned long long t = now();
+      const uint16_t* r = R.wait(q);
+      st_acc[1] += now() - t;
+      return r;
+    } else {
+      return R.wait(q);
+    }
+  };
+  auto prefill = [&](int q) {
+    if constexpr (kStamp) {
+      const unsigned long long t = now();
+      R.refill(q);
+      st_acc[2] += now() - t;
+    } else {
+      R.refill(q);
+    }
+  };
   // probe 4: fragments from registers instead of LDS
   const bf16x8 wconst = __builtin_bit_cast(bf16x8, make_uint4(0x3c003c00u, 0u, 0u, 0u));
   auto rd = [&](const uint16_t* slot, int f) {
@@ -228,6 +296,7 @@ void rowprog_kernel(RowProgArgs a) {
 
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
+    unsigned long long t_ld = now();
     int64_t row[TT];
     bool live[TT];
 #pragma unroll
@@ -269,6 +338,7 @@ void rowprog_kernel(RowProgArgs a) {
       }
     }
 
+    if constexpr (kStamp) st_acc[4] += now() - t_ld;
     // ---- pre-GEMM: acc += A · W0ᵀ + b0 (A rows in natural k order, 16 B per lane and k-step)
     if (has_pre) {
       bf16x8 af[TT][kKK];
@@ -327,7 +397,7 @@ void rowprog_kernel(RowProgArgs a) {
       }
 #pragma unroll
       for (int kk = 0; kk < kKK; ++kk) {
-        const uint16_t* slot = R.wait(g);
+        const uint16_t* slot = pwait(g);
         bf16x8 wq[kPD];
 #pragma unroll
         for (int q = 0; q < kPD; ++q) wq[q] = rd(slot, q);
@@ -337,7 +407,7 @@ void rowprog_kernel(RowProgArgs a) {
           if (ft + kPD < kFT) wq[ft % kPD] = rd(slot, ft + kPD);
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) acc[ft][tt] = mfma<do_mfma>(wc, af[tt][kk], acc[ft][tt]);
-          if (ft == kRefillAt) R.refill(g);
+          if (ft == kRefillAt) prefill(g);
           asm volatile("" ::: "memory");   // kPD fragment reads ahead, not the whole piece
         }
         ++g;
@@ -374,7 +444,7 @@ void rowprog_kernel(RowProgArgs a) {
 #pragma unroll 1
       for (int c = 0; c < nch; ++c) {
         // up projection: hidden features 32c + 16f + 4g + r
-        const uint16_t* up = R.wait(g);
+        const uint16_t* up = pwait(g);
         floatx4 u[2][TT];
 #pragma unroll
         for (int f = 0; f < 2; ++f)
@@ -390,7 +460,7 @@ void rowprog_kernel(RowProgArgs a) {
           if (j + kPD < 2 * kKK) wq[j % kPD] = rd(up, ((j + kPD) & 1) * kKK + ((j + kPD) >> 1));
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) u[j & 1][tt] = mfma<do_mfma>(wc, af[tt][j >> 1], u[j & 1][tt]);
-          if (j == kRefillAt) R.refill(g);
+          if (j == kRefillAt) prefill(g);
           asm volatile("" ::: "memory");
         }
         ++g;
@@ -405,7 +475,7 @@ void rowprog_kernel(RowProgArgs a) {
                                  pack_bf16x2(silu(u[1][tt][0] + c1.x), silu(u[1][tt][1] + c1.y)),
                                  pack_bf16x2(silu(u[1][tt][2] + c1.z), silu(u[1][tt][3] + c1.w))));
         // down projection: k-step c of W2 for all 24 output tiles
-        const uint16_t* dn = R.wait(g);
+        const uint16_t* dn = pwait(g);
 #pragma unroll
         for (int q = 0; q < kPD; ++q) wq[q] = rd(dn, q);
 #pragma unroll
@@ -414,7 +484,7 @@ void rowprog_kernel(RowProgArgs a) {
           if (ft + kPD < kFT) wq[ft % kPD] = rd(dn, ft + kPD);
 #pragma unroll
           for (int tt = 0; tt < TT; ++tt) acc[ft][tt] = mfma<do_mfma>(wc, hf[tt], acc[ft][tt]);
-          if (ft == kRefillAt) R.refill(g);
+          if (ft == kRefillAt) prefill(g);
           asm volatile("" ::: "memory");
         }
         ++g;
@@ -440,6 +510,7 @@ void rowprog_kernel(RowProgArgs a) {
     }
 
     // ---- epilogue: Xo = acc; y = LN_y(acc)
+    const unsigned long long t_ep = now();
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) {
       if (a.yt && live[tt]) {
@@ -483,8 +554,17 @@ void rowprog_kernel(RowProgArgs a) {
         }
       }
     }
+    if constexpr (kStamp) st_acc[3] += now() - t_ep;
   }
   wait_vm<0>();   // no DMA into this workgroup's LDS outlives it (every issued piece was consumed)
+  if constexpr (kStamp) {
+    st_acc[0] = now() - st_t0;
+    if (lane == 0 && a.probe) {   // launches on one stream add up (the tool runs the forward one-stream)
+      a.probe[((size_t)blockIdx.x * kWaves + w) * 8 + 5] += (unsigned long long)my_tiles;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) a.probe[((size_t)blockIdx.x * kWaves + w) * 8 + k] += st_acc[k];
+    }
+  }
 }
 
 // Host: k index of slot j (0..7) of lane group g in k-step kk.
@@ -551,6 +631,9 @@ std::vector<uint16_t> rowprog_pack_ffn(const std::vector<float>& W1in, const std
   return out;
 }
 
+static unsigned long long* g_rp_probe = nullptr;
+void rowprog_set_probe(void* stamps) { g_rp_probe = static_cast<unsigned long long*>(stamps); }
+
 void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
   SD_CHECK(a.n_ffn >= 0 && a.n_ffn <= 2, kErrInvalid, "rowprog: n_ffn");
   for (int i = 0; i < a.n_ffn; ++i)
@@ -573,7 +656,7 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
     SD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const void* ks[] = {reinterpret_cast<const void*>(rowprog_kernel<1, 0, 1>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 2>),
                         reinterpret_cast<const void*>(rowprog_kernel<1, 0, 3>), reinterpret_cast<const void*>(rowprog_kernel<1, 0, 5>),
-                        reinterpret_cast<const void*>(rowprog_kernel<1, 0>)};
+                        reinterpret_cast<const void*>(rowprog_kernel<1, 0>), reinterpret_cast<const void*>(rowprog_kernel<1, 8, 5>)};
     for (const void* k : ks)
       SD_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmemBytes));
     grid_max = cus > 0 ? cus : 256;
@@ -600,7 +683,10 @@ void rowprog(const RowProgArgs& a, const char* name, hipStream_t st) {
     RowProgArgs b = a;
     const int base = prog == 5 ? 20 : prog == 3 ? 12 : 8;
     b.stagger = ntiles > grid ? base : 0;
-    if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, b);
+    if (prog == 5 && g_rp_probe) {   // diagnostics: the pw2 + FFN program with phase stamps
+      b.probe = g_rp_probe;
+      hipLaunchKernelGGL((rowprog_kernel<1, 8, 5>), g3, dim3(512), kSmemBytes, st, b);
+    } else if (prog == 1) hipLaunchKernelGGL((rowprog_kernel<1, 0, 1>), g3, dim3(512), kSmemBytes, st, b);
     else if (prog == 2) hipLaunchKernelGGL((rowprog_kernel<1, 0, 2>), g3, dim3(512), kSmemBytes, st, b);
     else if (prog == 3) hipLaunchKernelGGL((rowprog_kernel<1, 0, 3>), g3, dim3(512), kSmemBytes, st, b);
     else if (prog == 5) hipLaunchKernelGGL((rowprog_kernel<1, 0, 5>), g3, dim3(512), kSmemBytes, st, b);
