@@ -434,7 +434,7 @@ int sd_debug_cam_dense_probe(void* stamps);
 /* Diagnostics: while `stamps` (device, >= 64 u64 per workgroup, zeroed) is non-NULL, every conformer pw2 + FFN
  * row-program launch (rowprog.hip, program 5) runs its stamping instantiation: lane 0 of every wave adds the
  * s_memtime cycles of its phases to stamps[(workgroup * 8 + wave) * 8 + k], k = 0 whole launch, 1 piece waits,
- * 2 slot-free waits (refills), 3 epilogue, 4 tile loads (tools/rowprog_probe.py). */
+ * 2 refill issue, 3 epilogue, 4 tile loads (tools/rowprog_probe.py). */
 int sd_debug_rowprog_probe(void* stamps);
 /* Diagnostics: a captured graph [memsetAsync(X, 0) -> kernel: Y = X, then X = 7] (fork != 0: the kernel behind
  * an event fork / join of a second captured stream) replayed `replays` times; bad_per_replay (host, replays

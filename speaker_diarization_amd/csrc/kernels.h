@@ -277,7 +277,7 @@ struct RowProgArgs {
   // half the CUs run their epilogue store burst while the other half streams MFMAs
   int stagger = 0;
   // diagnostics (sd_debug_rowprog_probe): per wave, lane 0 accumulates s_memtime cycles of the tile's phases
-  // into probe[(block * 8 + wave) * 8 + k] (k: 0 whole, 1 piece waits, 2 slot-free waits, 3 epilogue, 4 loads)
+  // into probe[(block * 8 + wave) * 8 + k] (k: 0 whole, 1 piece waits, 2 refill issue, 3 epilogue, 4 loads)
   unsigned long long* probe = nullptr;
   // X / Xo in the MFMA-tiled layout (M % 16 == 0): 16-row group g, feature f = 16 ft + 4 q + r of row 16 g + l at
   // float ((g * 24 + ft) * 64 + l + 16 q) * 4 + r -- each wave's 16 x 384 fp32 residual block is 24 contiguous

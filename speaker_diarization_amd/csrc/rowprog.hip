@@ -25,12 +25,14 @@
 // Weights stream from L2 as 24-KiB pieces of 24 pre-packed 1-KiB MFMA fragments (lane-linear, so every
 // ds_read_b128 is conflict-free) through a 5-slot LDS ring (global_load_lds, 4 pieces in flight, counted
 // vmcnt waits).  The workgroups are persistent over tiles; the ring runs across tile boundaries, so the next
-// tile's first weights are in flight during the current tile's epilogue.  Slot hand-off (kFlagRing, round 6):
-// per-slot FULL / FREE words in LDS instead of one workgroup barrier per piece -- a wave publishes FULL for
-// piece g + 1 once its own share of g + 1 has landed (counted vmcnt) as it starts piece g, and FREE for piece
-// g - 1 as it starts piece g (every read of g - 1 was consumed by an MFMA of g - 1); it waits for FULL(g) from
-// all 8 waves before reading piece g, and for FREE(g - 1) from all 8 before refilling that slot.  So the 8 waves
-// may drift by about a piece instead of meeting at every piece (kFlagRing = false: the barrier form).
+// tile's first weights are in flight during the current tile's epilogue.  One workgroup barrier per piece hands
+// the slots over.  (Round 6 replaced it by per-slot FULL / FREE words in LDS -- a wave published FULL(g + 1) once
+// its own share of g + 1 had landed and FREE(g - 1) as it started piece g, waited for all 8 FULL(g) before reading
+// and all 8 FREE(g - 1) before refilling, so the waves could drift by about a piece: the pw2 + FFN program went
+// 5.69 -> 6.38 ms per C2 step; the phase stamps, profiles/r06/rowprog_ring/, put the loss in the slot-free polls
+// (36.8k -> 66.5k cycles per tile) while the piece waits did not shrink (46.6k -> 51.6k): the polls take LDS
+// issue slots from the fragment reads that already bound the streaming phase, and a one-piece drift absorbs
+// none of the epilogue-sized skew.  Deleted; git history holds it.)
 // MFMA accumulators in the VGPR form (the 2-tile layout spilled to scratch with the default AGPR form)
 // sdiar-build: -mllvm -amdgpu-mfma-vgpr-form=1
 #include <cstring>
@@ -57,13 +59,9 @@ constexpr int kRefillAt = 3;          // the DMA refill is issued after this man
 constexpr int kPrmFfn = 3 * kD + kMaxHidden;
 constexpr int kPrmB0 = 0, kPrmFfn0 = kD, kPrmY = kD + 2 * kPrmFfn;
 constexpr int kPrmGn = kPrmY + 2 * kD;   // GroupNorm gamma | beta of the pre-GEMM's A transform
-constexpr int kPrmFlags = kPrmGn + 2 * kD;   // FULL[kNSlot] | FREE[kNSlot] counters (uint32, in the padding)
 constexpr int kPrmFloats = (kPrmGn + 2 * kD + 255) / 256 * 256;   // padded to whole KiB
-constexpr bool kFlagRing = true;
-constexpr unsigned kFlagSpin = 1u << 16;   // poll bound: a wave that never publishes must not hang the GPU
 constexpr size_t kSmemBytes = sizeof(uint16_t) * (size_t)kNSlot * kPiece + sizeof(float) * kPrmFloats;
 static_assert((kPrmFloats * 4) % 1024 == 0, "ring slots stay 1-KiB aligned");
-static_assert(kPrmFlags + 2 * kNSlot <= kPrmFloats, "the slot counters fit the parameter block's padding");
 static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -84,19 +82,6 @@ __device__ __forceinline__ void wait_piece(int younger) {
 
 __device__ __forceinline__ float silu(float v) { return v * sigmoid_rcp(v); }
 
-// LDS slot counters (inline asm: the compiler neither reorders them with the ring's fragment reads nor puts
-// vmcnt drains in front of them).  One lane adds; every lane polls the same word (uniform value).
-__device__ __forceinline__ void lds_count(uint32_t addr, int lane) {
-  if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
-}
-__device__ __forceinline__ void lds_wait_ge(uint32_t addr, uint32_t target) {
-  for (unsigned spins = 0; spins < kFlagSpin; ++spins) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-    if (__builtin_amdgcn_readfirstlane(v) >= target) return;
-  }
-}
-
 // TT 16-token MFMA column tiles per wave; 8 / TT waves per 128-token tile.
 template <int TT>
 struct Ring {
@@ -110,7 +95,6 @@ struct Ring {
   int total;    // pieces this workgroup consumes
   int w, lane;
   bool dma;     // probe: false skips the weight stream
-  uint32_t full, free_;   // LDS byte addresses of FULL[0] / FREE[0]
 
   __device__ __forceinline__ const uint16_t* src(int q) const {
     if (q < n_pre) return w0 + (size_t)q * kPiece;
@@ -120,8 +104,6 @@ struct Ring {
   }
   __device__ __forceinline__ void issue(int g) const {
     if (g >= total || !dma) return;
-    // flag ring: the slot's previous piece (g - kNSlot) must be consumed by every wave
-    if (kFlagRing && g >= kNSlot) lds_wait_ge(free_ + 4 * (g % kNSlot), (uint32_t)(kWaves * (g / kNSlot)));
     const uint16_t* s = src(g % P);
     uint16_t* slot = ring + (g % kNSlot) * kPiece;
 #pragma unroll
@@ -130,24 +112,9 @@ struct Ring {
       dma_lds16(s + f * kFrag + lane * 8, (lds_ptr_t)(slot + f * kFrag));
     }
   }
-  // First piece (flag ring): this wave's share of piece 0 landed -> FULL(0).
-  __device__ __forceinline__ void start() const {
-    if (!kFlagRing || total <= 0) return;
-    if (dma) wait_piece<kDpw>(min(kNSlot - 2, total - 1));
-    lds_count(full, lane);
-  }
   // Wait for piece g and make every wave's part visible; returns g's slot.  The slot of piece g - 1 is
   // free from here on: refill(g) (called a few MFMAs into the piece) streams piece g + kNSlot - 1 into it.
   __device__ __forceinline__ const uint16_t* wait(int g) const {
-    if constexpr (kFlagRing) {
-      if (g + 1 < total) {   // this wave's share of piece g + 1 (issued up to g + 3 so far) landed -> FULL(g + 1)
-        if (dma) wait_piece<kDpw>(min(kNSlot - 3, total - 2 - g));
-        lds_count(full + 4 * ((g + 1) % kNSlot), lane);
-      }
-      if (g >= 1) lds_count(free_ + 4 * ((g - 1) % kNSlot), lane);   // piece g - 1's reads are consumed
-      lds_wait_ge(full + 4 * (g % kNSlot), (uint32_t)(kWaves * (g / kNSlot + 1)));
-      return ring + (g % kNSlot) * kPiece;
-    }
     wait_piece<kDpw>(min(kNSlot - 2, total - 1 - g));
     // plain s_barrier: __syncthreads()' workgroup fence waits for vmcnt(0) and would drain the ring
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -241,7 +208,6 @@ void rowprog_kernel(RowProgArgs a) {
   cp(kPrmY + kD, a.y_b, kD);
   cp(kPrmGn, a.gn_g, kD);
   cp(kPrmGn + kD, a.gn_b, kD);
-  if (tid < 2 * kNSlot) reinterpret_cast<uint32_t*>(prm)[kPrmFlags + tid] = 0u;
   __syncthreads();
 
   const int ntiles = (a.M + kRows - 1) / kRows;
@@ -258,15 +224,12 @@ void rowprog_kernel(RowProgArgs a) {
   R.w = w;
   R.lane = lane;
   R.dma = !(PROBE & 2);
-  R.full = (uint32_t)reinterpret_cast<uintptr_t>(prm + kPrmFlags);
-  R.free_ = R.full + 4 * kNSlot;
   // PROBE & 8: phase cycles per wave (RowProgArgs::probe)
   constexpr bool kStamp = (PROBE & 8) != 0;
   unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
   const unsigned long long st_t0 = kStamp ? __builtin_amdgcn_s_memtime() : 0;
   auto now = [&]() -> unsigned long long { return kStamp ? __builtin_amdgcn_s_memtime() : 0ull; };
   for (int g = 0; g < kNSlot - 1; ++g) R.issue(g);
-  R.start();
   int g = 0;
   auto pwait = [&](int q) {
     if constexpr (kStamp) {

@@ -1,7 +1,7 @@
 """Phase split of the conformer pw2 + FFN row program (rowprog.hip program 5, the C2 line's dominant kernel) from
 its stamping instantiation (sd_debug_rowprog_probe; GPU box).  One C2-shaped TS-VAD forward (ots_vad v1, B windows
 of 598 fbank frames, one stream so the 6 launches run one after another); per wave, s_memtime cycles of: piece waits
-(FULL(g) / barrier), slot-free waits before refills, epilogue stores, tile loads; MFMA streaming + LayerNorms = the
+(barrier), refill issue (the DMA instructions of the next piece), epilogue stores, tile loads; MFMA streaming + LayerNorms = the
 rest.  Printed per 128-token tile (mean over waves).
     SDIAR_CAM_ONE_STREAM=1 python3 tools/rowprog_probe.py [B]"""
 import os
@@ -37,7 +37,7 @@ s = s[live]
 tiles = s[:, :, 5]                              # tiles this wave ran over the forward's launches
 per_tile = s[:, :, :5] / tiles[:, :, None]
 mean = per_tile.reshape(-1, 5).mean(0)
-names = ["whole", "piece waits", "slot-free waits", "epilogue", "tile loads"]
+names = ["whole", "piece waits", "refill issue", "epilogue", "tile loads"]
 print(f"B {B}: {int(live.sum())} workgroups, {tiles.mean():.1f} tiles per wave over the forward's launches")
 for n, v in zip(names, mean):
     print(f"  {n:16s} {v:9.0f} cycles per tile ({100 * v / mean[0]:5.1f} %)")
