@@ -443,9 +443,11 @@ int sd_probe_graph_memset(int n, int replays, int fork, int* bad_per_replay, voi
 /* The conformer self-attention block's in-projection + attention (mha_block.hip; torchaudio MHA with
  * batch_first, 8 heads of 48, D 384) on LayerNorm'd bf16 rows y (S, T, 384): w (1152, 384) / bias (1152) the
  * packed in_proj, key_len device int32 (S) or NULL, out bf16 (S, T, 384) = the heads' outputs before out_proj.
- * variant: the kernel layout (0: one sequence per 4-wave workgroup, 1: two per 8-wave workgroup; tests). */
+ * variant: the kernel layout (-1 or 0: the shipped <2 sequences, 8 waves, 3-slot ring, 48-wide Q / K rows>;
+ * 1-7 the round-5 sweep's other layouts, mha_block.hip; tests).  flags (round 6): bit 0 = y given in the row
+ * programs' MFMA-fragment layout (RowProgArgs::a_tiled), bit 1 = out written in it (S * T % 16 == 0). */
 int sd_op_mha_block(const void* y, const float* w, const float* bias, int S, int T, const int* key_len, void* out,
-                    int variant, void* stream);
+                    int variant, int flags, void* stream);
 /* nn.Conv1d on channel-last input x (B, T, Cin) with weight (Cout, Cin, k) -> out (B, To, Cout). */
 int sd_op_conv1d(const float* x, int B, int T, int Cin, const float* w, const float* b, int Cout,
                  int k, int stride, int pad, int dil, int act, float* out, int precision, void* stream);

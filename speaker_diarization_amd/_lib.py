@@ -194,7 +194,7 @@ _SIGS = {
     "sd_debug_cam_dense_probe": (c_int, [c_void_p]),
     "sd_debug_rowprog_probe": (c_int, [c_void_p]),
     "sd_probe_graph_memset": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p]),
-    "sd_op_mha_block": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "sd_op_mha_block": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "sd_op_cam_dense": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_int, c_void_p]),

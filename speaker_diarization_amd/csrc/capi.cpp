@@ -755,15 +755,18 @@ int sd_op_cam_dense(const void* x, int B, int T, int ld, int cin, int dil, const
 }
 
 int sd_op_mha_block(const void* y, const float* w, const float* bias, int nseq, int T, const int* key_len, void* out,
-                    int variant, void* stream) {
+                    int variant, int flags, void* stream) {
   return guard([&] {
     hipStream_t st = S(stream);
     SD_CHECK(nseq >= 1 && sd::mha_block_supported(384, 8, T, true), sd::kErrInvalid, "mha_block: unsupported shape");
+    SD_CHECK(flags >= 0 && flags <= 3, sd::kErrInvalid, "mha_block: flags");
     Scratch wt((size_t)3 * 384 * 384 * 2, st);
     sd::pack_weight(w, 3 * 384, 384, 1, wt.p, true, st);
     sd::MhaBlockArgs m;
     m.y = y; m.W = wt.p; m.bias = bias; m.out = out; m.ldo = 384;
     m.S = nseq; m.T = T; m.D = 384; m.nh = 8; m.scale = 1.f / std::sqrt(48.f); m.key_len = key_len;
+    m.y_tiled = flags & 1;     // y in RowProgArgs::a_tiled's fragment layout (what the FFN programs hand over)
+    m.out_tiled = (flags >> 1) & 1;   // the output in that layout (what the out-projection program reads)
     sd::mha_block(m, st, variant);
   });
 }

@@ -54,7 +54,7 @@ constexpr int kPiece = kPieceFrags * kFrag;   // 12288 bf16 = 24 KiB
 constexpr int kNSlot = 5;
 constexpr int kMaxHidden = 1024;
 constexpr int kPD = 3;                // fragment reads in flight ahead of the MFMA that uses them
-constexpr int kRefillAt = 3;          // the DMA refill is issued after this many MFMAs of a piece
+constexpr int kRefillAt = 8;          // the DMA refill is issued after this many MFMAs of a piece (round 6 sweep 0 / 3 / 8 / 16 / 22: 8)
 // LDS parameter block (floats): b0 | per FFN: post_g post_b b2 (D each) b1 (kMaxHidden) | y_g y_b
 constexpr int kPrmFfn = 3 * kD + kMaxHidden;
 constexpr int kPrmB0 = 0, kPrmFfn0 = kD, kPrmY = kD + 2 * kPrmFfn;

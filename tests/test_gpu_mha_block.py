@@ -27,13 +27,28 @@ def _ref(y, w, b, key_len):
     return (sc.softmax(-1) @ v).transpose(1, 2).reshape(S, T, D)
 
 
-def _run(y, w, b, key_len, variant):
+def _run(y, w, b, key_len, variant, flags=0):
     S, T, D = y.shape
     out = torch.zeros(S, T, D, device=y.device, dtype=torch.bfloat16)
     _lib.call("sd_op_mha_block", _lib.ptr(y), _lib.ptr(w), _lib.ptr(b), S, T,
-              _lib.ptr(key_len) if key_len is not None else None, _lib.ptr(out), variant, _lib.stream_ptr(y.device))
+              _lib.ptr(key_len) if key_len is not None else None, _lib.ptr(out), variant, flags,
+              _lib.stream_ptr(y.device))
     torch.cuda.synchronize()
     return out
+
+
+def _tile(x):
+    """(S, T, 384) rows -> the row programs' MFMA-fragment layout (kernels.h RowProgArgs::a_tiled): 16-row group g,
+    fragment kk (features 32 kk ..), lane l = row % 16 + 16 q holds features 32 kk + 8 q .. + 7 of row 16 g + l % 16."""
+    S, T, D = x.shape
+    r = x.reshape(S * T // 16, 16, D // 32, 4, 8)          # (group, row, kk, q, 8)
+    return r.permute(0, 2, 3, 1, 4).contiguous().reshape(S, T, D)
+
+
+def _untile(x):
+    S, T, D = x.shape
+    r = x.reshape(S * T // 16, D // 32, 4, 16, 8)           # (group, kk, q, row, 8)
+    return r.permute(0, 3, 1, 2, 4).contiguous().reshape(S, T, D)
 
 
 @pytest.mark.parametrize("S,T,lens", [(4, 150, False), (7, 150, True), (3, 100, False), (5, 37, True), (1, 160, False)])
@@ -51,3 +66,50 @@ def test_mha_block_layouts(gpu, S, T, lens):
         assert err.max().item() < 3e-2, v
     for v in range(1, 8):
         assert torch.equal(outs[0], outs[v]), v
+
+
+
+@pytest.mark.parametrize("S,T", [(8, 150), (3, 160), (2, 96)])
+def test_mha_block_tiled_layouts_bit_identical(gpu, S, T):
+    """The production hand-offs: y read in the row programs' fragment layout and the output written in
+    it (encoder.cpp's tiled_y / tiled_a) give the row-major call's bits once de-tiled on the host."""
+    g = torch.Generator().manual_seed(S * 7 + T)
+    y = torch.randn(S, T, 384, generator=g).to(torch.bfloat16).to(gpu)
+    w = (torch.randn(1152, 384, generator=g) * 384 ** -0.5).to(gpu)
+    b = (torch.randn(1152, generator=g) * 0.1).to(gpu)
+    key_len = torch.randint(1, T + 1, (S,), generator=g, dtype=torch.int32).to(gpu)
+    base = _run(y, w, b, key_len, -1)
+    assert torch.equal(_untile(_tile(y)), y)
+    for flags in (1, 2, 3):
+        yin = _tile(y) if flags & 1 else y
+        out = _run(yin, w, b, key_len, -1, flags)
+        out = _untile(out) if flags & 2 else out
+        assert torch.equal(out, base), flags
+
+
+def test_mha_block_nonfinite_masked_rows(gpu):
+    """Rows past key_len holding Inf / NaN (with 48-wide Q / K rows, a key row's features 0..15 meet the
+    zeroed Q lanes of the key before it, and 0 * Inf = NaN).  The kernel never reads a key tile that starts at or past
+    key_len and masks the rest of the boundary tile before the softmax, so the visible queries of every sequence equal
+    the reference computed with those rows replaced by finite values.  (torch's MHA itself would return NaN for the
+    whole sequence -- the masked key's weight 0 times its non-finite value row; on the product path a window with a
+    non-finite input is poisoned to NaN upstream, tsvad.cpp nonfinite_windows / poison_windows, so the window's
+    outputs agree either way.)"""
+    S, T = 4, 150
+    g = torch.Generator().manual_seed(99)
+    y = torch.randn(S, T, 384, generator=g)
+    key_len = torch.tensor([150, 120, 90, 150], dtype=torch.int32)
+    clean = y.clone()
+    y[1, 130:] = float("inf")
+    y[2, 100, 5] = float("nan")
+    y[2, 91, 0] = float("-inf")      # in the boundary tile (keys 64..95), past key_len 90
+    w = (torch.randn(1152, 384, generator=g) * 384 ** -0.5).to(gpu)
+    b = (torch.randn(1152, generator=g) * 0.1).to(gpu)
+    kl = key_len.to(gpu)
+    ref = _ref(clean.to(torch.bfloat16).to(gpu), w.to(torch.bfloat16).float(), b, kl)
+    out = _run(y.to(torch.bfloat16).to(gpu), w, b, kl, -1).float()
+    for s_ in range(S):
+        n = int(key_len[s_])                       # the visible queries (every row past key_len is padding)
+        o, r = out[s_, :n], ref[s_, :n]
+        assert torch.isfinite(o).all(), s_
+        assert (o - r).abs().max().item() < 3e-2, s_

@@ -112,6 +112,65 @@ void run_raw(float* d, float* h, int iters) {
   printf("RAW wait states %2d: last element %8.1f (expect 33), wrong elements %6.0f of %d\n", N, h[0], bad, 64 * 4 * iters);
 }
 
+// RAW for the 16-pass 32x32x16 bf16 shape (the FCM stem's MFMA): the first destination register read N wait
+// states after the MFMA (a stale -5 if too early).  A = B = 1, C = 0: every element 16.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+template <int N, int K>
+__global__ __launch_bounds__(64) void raw32_kernel(float* out, int iters) {
+  bf16x8 one;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) one[i] = (__bf16)1.0f;
+  const float stale = -5.0f;
+  int bad = 0;
+  for (int it = 0; it < iters; ++it) {
+    float r0;
+    asm volatile(
+        "v_accvgpr_write_b32 a16, %[s]\n\ts_nop 7\n\ts_nop 7\n\t"
+        "v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\t"
+        "v_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\t"
+        "v_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\t"
+        "v_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\t"
+        "v_accvgpr_write_b32 a17, %[s]\n\tv_accvgpr_write_b32 a18, %[s]\n\tv_accvgpr_write_b32 a19, %[s]\n\t"
+        "v_accvgpr_write_b32 a20, %[s]\n\tv_accvgpr_write_b32 a21, %[s]\n\tv_accvgpr_write_b32 a22, %[s]\n\t"
+        "v_accvgpr_write_b32 a23, %[s]\n\tv_accvgpr_write_b32 a24, %[s]\n\tv_accvgpr_write_b32 a25, %[s]\n\t"
+        "v_accvgpr_write_b32 a26, %[s]\n\tv_accvgpr_write_b32 a27, %[s]\n\tv_accvgpr_write_b32 a28, %[s]\n\t"
+        "v_accvgpr_write_b32 a29, %[s]\n\tv_accvgpr_write_b32 a30, %[s]\n\tv_accvgpr_write_b32 a31, %[s]\n\t"
+        "s_nop 7\n\ts_nop 7\n\t"
+        "v_mfma_f32_32x32x16_bf16 a[16:31], %[A], %[B], a[0:15]\n\t"
+        "s_nop %[n]\n\t"
+        "v_accvgpr_read_b32 %[r0], a%c[k]\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+        : [r0] "=v"(r0)
+        : [A] "v"(one), [B] "v"(one), [s] "v"(stale), [n] "n"(N - 1), [k] "n"(16 + K)
+        : "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15",
+          "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31");
+    bad += r0 != 16.f;
+    if (it == 0) out[threadIdx.x] = r0;
+  }
+  out[64 + threadIdx.x] = (float)bad;
+}
+
+template <int N, int K>
+double raw32_bad(float* d, float* h, int iters) {
+  hipLaunchKernelGGL((raw32_kernel<N, K>), dim3(1), dim3(64), 0, 0, d, iters);
+  (void)hipMemcpy(h, d, 128 * sizeof(float), hipMemcpyDeviceToHost);
+  double bad = 0;
+  for (int i = 0; i < 64; ++i) bad += h[64 + i];
+  return bad;
+}
+// per destination register (a16 + K) of the 32x32x16 MFMA: wrong reads at N wait states
+template <int N>
+void run_raw32(float* d, float* h, int iters) {
+  printf("RAW32 wait states %2d, wrong reads per destination register:", N);
+  const double b[16] = {raw32_bad<N, 0>(d, h, iters), raw32_bad<N, 1>(d, h, iters), raw32_bad<N, 2>(d, h, iters),
+                        raw32_bad<N, 3>(d, h, iters), raw32_bad<N, 4>(d, h, iters), raw32_bad<N, 5>(d, h, iters),
+                        raw32_bad<N, 6>(d, h, iters), raw32_bad<N, 7>(d, h, iters), raw32_bad<N, 8>(d, h, iters),
+                        raw32_bad<N, 9>(d, h, iters), raw32_bad<N, 10>(d, h, iters), raw32_bad<N, 11>(d, h, iters),
+                        raw32_bad<N, 12>(d, h, iters), raw32_bad<N, 13>(d, h, iters), raw32_bad<N, 14>(d, h, iters),
+                        raw32_bad<N, 15>(d, h, iters)};
+  for (int k = 0; k < 16; ++k) printf(" %.0f", b[k]);
+  printf("\n");
+}
+
 template <int N>
 void run(float* d, float* h, int iters) {
   hipLaunchKernelGGL(war_kernel<N>, dim3(1), dim3(64), 0, 0, d, iters);
@@ -150,6 +209,17 @@ int main() {
   run_raw<10>(d, h, iters);
   run_raw<11>(d, h, iters);
   run_raw<12>(d, h, iters);
+  run_raw32<4>(d, h, iters);
+  run_raw32<6>(d, h, iters);
+  run_raw32<8>(d, h, iters);
+  run_raw32<9>(d, h, iters);
+  run_raw32<10>(d, h, iters);
+  run_raw32<11>(d, h, iters);
+  run_raw32<12>(d, h, iters);
+  run_raw32<13>(d, h, iters);
+  run_raw32<14>(d, h, iters);
+  run_raw32<15>(d, h, iters);
+  run_raw32<16>(d, h, iters);
   (void)hipFree(d);
   return 0;
 }
