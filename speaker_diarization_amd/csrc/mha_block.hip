@@ -212,19 +212,12 @@ __global__ __launch_bounds__(W * 64) void mha_block_kernel(MhaBlockArgs a) {
     const float scl = c == 0 ? a.scale : 1.f;
     const int n0 = ft * 16 + 4 * lk;
     const float4 bv = *reinterpret_cast<const float4*>(s_bias + c * kD + h * kHD + n0);
-    // K / V rows of keys past key_len are stored as zeros: the attention masks those keys (P = 0), and a zero row
-    // keeps a non-finite padded input from turning 0 * Inf into NaN there -- in P·V, and in the QS = 48 layout's
-    // second QK^T k-step, which reads the next key row's features 0..15 against zeroed Q lanes (identical bits
-    // for finite inputs)
 #pragma unroll
     for (int rt = 0; rt < kMaxTiles; ++rt)
-      if (rt < ntile) {
-        const bool zero = c != 0 && rowj[rt] >= klenj[sqj[rt]];
+      if (rt < ntile)
         *reinterpret_cast<uint2*>(qimg(sqj[rt]) + coff + rowj[rt] * ld + n0) =
-            zero ? make_uint2(0u, 0u)
-                 : make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
-                              pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
-      }
+            make_uint2(pack_bf16x2((acc[rt][0] + bv.x) * scl, (acc[rt][1] + bv.y) * scl),
+                       pack_bf16x2((acc[rt][2] + bv.z) * scl, (acc[rt][3] + bv.w) * scl));
     if (c != 2 || ft != 2 || (PROBE & 1)) continue;
     __syncthreads();   // head h's Q, K, V images complete (every sequence of the workgroup)
 
