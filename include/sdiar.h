@@ -47,6 +47,9 @@ int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream);
 /* The same 4-workgroup exchange on data-tagged 8-byte granules (no counter, no barrier; MI355X guide
  * handoff-1to1): the hardware's hand-off price for the recurrence, us per step. */
 int sd_probe_lstm_granule(int steps, float* us_per_step, void* stream);
+/* Round 6: the granule exchange between TWO workgroups (each lane polls only the other one's half of its operand,
+ * 1-to-1): the exchange floor of a recurrence that holds half of W_hh per CU. */
+int sd_probe_lstm_granule2(int steps, float* us_per_step, void* stream);
 
 /* ------------------------------------------------------------------ TS-VAD
  * Replaces TSVADModel (egs/alimeeting/ts_vad2/model.py:179-1142):

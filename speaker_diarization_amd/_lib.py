@@ -114,6 +114,7 @@ _SIGS = {
     "sd_prof_query": (c_int, [c_int, c_char_p, c_int, POINTER(c_int64), POINTER(ctypes.c_double),
                               POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
     "sd_prof_query_steps": (ctypes.c_double, [c_int]),
+    "sd_probe_lstm_granule2": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_probe_lstm_granule": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_probe_lstm_handoff": (c_int, [c_int, c_void_p, c_void_p]),
     "sd_tsvad_create": (c_int, [POINTER(TsvadConfig), POINTER(c_void_p)]),

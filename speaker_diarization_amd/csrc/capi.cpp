@@ -116,6 +116,13 @@ int sd_probe_lstm_granule(int steps, float* us_per_step, void* stream) {
   });
 }
 
+int sd_probe_lstm_granule2(int steps, float* us_per_step, void* stream) {
+  return guard([&] {
+    SD_CHECK(steps >= 1 && us_per_step, sd::kErrInvalid, "probe_lstm_granule2: bad argument");
+    *us_per_step = sd::lstm_granule_probe(steps, S(stream), 2);
+  });
+}
+
 int sd_probe_lstm_handoff(int steps, float* us_per_step, void* stream) {
   return guard([&] {
     SD_CHECK(steps >= 1 && us_per_step, sd::kErrInvalid, "probe_lstm_handoff: bad argument");

@@ -402,7 +402,8 @@ int64_t lstm_work_floats(int B, int H, int ndir);
 // Exchange floor of the persistent recurrence (sd_probe_lstm_handoff): us per step of its hand-off alone.
 float lstm_handoff_probe(int steps, hipStream_t st);
 // The same exchange on 8-byte {data, tag} granules (sd_probe_lstm_granule; lstm.hip): us per step.
-float lstm_granule_probe(int steps, hipStream_t st);
+// nwg 2: the two-workgroup 1-to-1 form (each lane polls only the other workgroup's half of its operand).
+float lstm_granule_probe(int steps, hipStream_t st, int nwg = 4);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr,

@@ -503,6 +503,63 @@ __global__ __launch_bounds__(256) void lstm_granule_probe_kernel(int steps, uint
   if (tid == 0) sink[blockIdx.x] = hr;
 }
 
+// Round 6 (verdict item 6): the same granule exchange between TWO workgroups per direction -- the shape a recurrence
+// holding half of W_hh per CU (160 KiB LDS + 96 KiB of VGPR fragments) would need: workgroup q owns units
+// 128 q .. + 127 (a lane 8 units of its batch row: two 16-B sc1 stores of two granules each), and every lane polls only
+// the other workgroup's half of its MFMA operand (4 k-steps x 2 16-B sc1 loads, 1-to-1 instead of all-to-all).
+// sd_probe_lstm_granule2: us per step of this hand-off alone.
+__global__ __launch_bounds__(256) void lstm_granule_probe2_kernel(int steps, uint64_t* __restrict__ gx,
+                                                                  int* __restrict__ err, unsigned spin_limit,
+                                                                  float* __restrict__ sink) {
+  constexpr int H = LS_H, NG = H / 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int q = blockIdx.x & 1;
+  const int ub = 128 * q + 32 * w + 8 * g;                   // the lane's 8 units
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(gx, (short)0, 2 * 16 * NG * 8, 0x00020000);
+  auto goff = [&](int parity, int b, int granule) { return (uint32_t)(((parity * 16 + b) * NG + granule) * 8); };
+  float hr = (float)ub;
+  auto publish = [&](int step_tag) {
+    const uint32_t d = pack_bf16x2(hr, hr);
+    const u32x4_t v = {d, (uint32_t)step_tag, d, (uint32_t)step_tag};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rg, goff(step_tag & 1, l15, ub / 2), 0, 16);       // sc1
+    __builtin_amdgcn_raw_buffer_store_b128(v, rg, goff(step_tag & 1, l15, ub / 2 + 2), 0, 16);   // sc1
+  };
+  publish(1);
+  int bad = 0;
+  const int kr0 = 4 * (1 - q);                                // the other workgroup's k-steps: kr0 .. kr0 + 3
+  for (int step = 1; step <= steps && !bad; ++step) {
+    u32x4_t f[4][2];
+    unsigned spins = 0;
+    for (;;) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          f[kc][r] = __builtin_amdgcn_raw_buffer_load_b128(rg, goff(step & 1, l15, ((kr0 + kc) * 32 + 8 * g) / 2 + 2 * r), 0, 16);
+      bool ok = true;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) ok &= f[kc][r][1] == (uint32_t)step && f[kc][r][3] == (uint32_t)step;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (++spins > spin_limit) {
+        bad = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) x ^= f[kc][0][0] ^ f[kc][1][2];
+    hr = __uint_as_float((x & 0x007fffffu) | 0x3f800000u);
+    publish(step + 1);
+  }
+  if (bad && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) sink[blockIdx.x] = hr;
+}
+
 // Poll bound of the persistent kernel's waits: 2^22 polls (~0.1 s).  Tests only: SDIAR_LSTM_SPIN_LIMIT
 // shrinks it so a test can force the co-residency-lost path and check that it is reported;
 // SDIAR_LSTM_SPIN_LIMIT_LAUNCHES=n applies that limit to the first n persistent launches of the process
@@ -638,7 +695,7 @@ float lstm_handoff_probe(int steps, hipStream_t st) {
   return ms * 1000.f / (float)steps;
 }
 
-float lstm_granule_probe(int steps, hipStream_t st) {
+float lstm_granule_probe(int steps, hipStream_t st, int nwg) {
   const size_t gx_bytes = (size_t)2 * 16 * (LS_H / 2) * 8;
   void* buf = nullptr;
   SD_HIP(hipMalloc(&buf, gx_bytes + 256));
@@ -650,7 +707,10 @@ float lstm_granule_probe(int steps, hipStream_t st) {
   SD_HIP(hipEventCreate(&a));
   SD_HIP(hipEventCreate(&b));
   SD_HIP(hipEventRecord(a, st));
-  hipLaunchKernelGGL(lstm_granule_probe_kernel, dim3(4), dim3(256), 0, st, steps, gx, err, lstm_spin_limit(), sink);
+  if (nwg == 2)
+    hipLaunchKernelGGL(lstm_granule_probe2_kernel, dim3(2), dim3(256), 0, st, steps, gx, err, lstm_spin_limit(), sink);
+  else
+    hipLaunchKernelGGL(lstm_granule_probe_kernel, dim3(4), dim3(256), 0, st, steps, gx, err, lstm_spin_limit(), sink);
   SD_LAUNCH_CHECK();
   SD_HIP(hipEventRecord(b, st));
   SD_HIP(hipEventSynchronize(b));
