@@ -66,7 +66,8 @@ WORKLOADS = {
                      "replicas only"),
 }
 
-PEAKS = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (MI355X_MICROARCH.md)
+# dense TFLOP/s (MI355X_MICROARCH.md); bf16x3 = the bf16 peak over its 3 MFMAs per fp32-equivalent product
+PEAKS = {"bf16": 2500.0, "f32": 157.3, "bf16x3": 2500.0 / 3}
 HBM_PEAK = 8000.0                        # GB/s
 ATTN_KERNELS = ("mha_block", "attention_bf16", "attention_f32")   # fused block first (C2 conformer)
 
@@ -86,7 +87,7 @@ def parse(argv=None):
                     help="weak scaling: meeting minutes per GPU; strong scaling: total meeting minutes")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="default: strong (fixed 60-min meeting) when WORLD_SIZE > 1, else one 10-min meeting")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "bf16x3"])
     ap.add_argument("--batch", type=int, default=64, help="reference batch (windows, zero-pad unit)")
     ap.add_argument("--device-batch", type=int, default=640, help="windows per device launch (a 10-min meeting in one launch)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU-baseline budget (3 timed runs)")
@@ -254,7 +255,7 @@ def kernel_report(kernels, workload, ms_per_step, precision):
     flops = sum(v["flops"] for v in kernels.values())
     byts = sum(v["bytes"] for v in kernels.values())
     kms = sum(v["ms"] for v in kernels.values())
-    dt = "f32" if precision == "fp32" else "bf16"
+    dt = {"fp32": "f32", "bf16x3": "bf16x3"}.get(precision, "bf16")
     s = ms_per_step * 1e-3
     out["step_work"] = {"algorithmic_gflop_per_step": round(flops / 1e9, 2),
                         "algorithmic_gb_per_step": round(byts / 1e9, 3),

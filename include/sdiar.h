@@ -66,7 +66,7 @@ typedef struct {
   int rs_len;                     /* seconds; PositionalEncoding max_len = rs_len * 25       */
   int max_batch;                  /* workspace sizing                                        */
   int max_fbank_frames;           /* workspace sizing: 1 + (rs_len*16000 - 400) / 160        */
-  int precision;                  /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate */
+  int precision;                  /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate, 2: bf16x3 (fp32 tensors; the GEMMs as bf16 hi+lo splits: hi·hi + hi·lo + lo·hi) */
   int num_transformer_layer;      /* TSVADConfig defaults: 2, 4, 384, 1536, 192              */
   int num_attention_head;
   int transformer_embed_dim;
@@ -237,7 +237,7 @@ typedef struct {
   int max_seqs;         /* workspace: sequences (chunks) per forward                          */
   int max_frames;       /* workspace: frames per sequence (chunk_size, 2000)                  */
   int max_n_speakers;   /* attractors decoded (15)                                            */
-  int precision;        /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate            */
+  int precision;        /* 0: fp32 (exact-f32 MFMA), 1: bf16 MFMA, fp32 accumulate, 2: bf16x3 GEMMs */
   int n_speakers;       /* variant 3 only: decoder outputs                                    */
 } sd_eda_config;
 /* variant 3 is the plain EEND TransformerModel (speaker_diarization/eend/models.py:17-101,
@@ -285,7 +285,7 @@ typedef struct {
   int max_seqs;             /* workspace: sequences per call                              */
   int max_frames;           /* workspace: frames per sequence (chunk_size 10000)          */
   int max_nspks;            /* workspace: attractor slots (max_speakers + 2 = 6)         */
-  int precision;            /* 0 fp32, 1 bf16 MFMA                                         */
+  int precision;            /* 0 fp32, 1 bf16 MFMA, 2 bf16x3 GEMMs (fp32 tensors) */
 } sd_fseend_config;
 
 int sd_fseend_create(const sd_fseend_config* cfg, sd_fseend** out);

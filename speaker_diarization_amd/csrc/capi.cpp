@@ -25,10 +25,12 @@ const char* last_error() { return g_err.c_str(); }
 }  // namespace sd
 
 struct sd_tsvad {
+  bool x3 = false;   // precision 2: conv_gemm's exact path in bf16x3 (GemmX3Scope around compute)
   std::unique_ptr<sd::TsvadModel> model;
 };
 
 struct sd_eda {
+  bool x3 = false;   // precision 2: conv_gemm's exact path in bf16x3 (GemmX3Scope around compute)
   std::unique_ptr<sd::EdaModel> model;
 };
 
@@ -45,6 +47,7 @@ struct sd_tsvad_stream {
 };
 
 struct sd_fseend {
+  bool x3 = false;   // precision 2: conv_gemm's exact path in bf16x3 (GemmX3Scope around compute)
   std::unique_ptr<sd::FsEendModel> model;
 };
 
@@ -134,7 +137,7 @@ int sd_tsvad_create(const sd_tsvad_config* c, sd_tsvad** out) {
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
     SD_CHECK(c->variant == 0 || c->variant == 1, sd::kErrInvalid, "unknown TS-VAD variant");
-    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->precision >= 0 && c->precision <= 2, sd::kErrInvalid, "precision must be 0, 1 or 2");
     SD_CHECK(c->max_batch > 0 && c->max_fbank_frames > 0, sd::kErrInvalid, "bad workspace sizes");
     SD_CHECK(c->max_num_speaker > 0 && c->num_transformer_layer >= 1 && c->transformer_ffn_embed_dim > 0 &&
                  c->speaker_embed_dim > 0, sd::kErrInvalid, "bad model dimensions");
@@ -153,6 +156,7 @@ int sd_tsvad_create(const sd_tsvad_config* c, sd_tsvad** out) {
     t.ffn_dim = c->transformer_ffn_embed_dim;
     t.speaker_embed_dim = c->speaker_embed_dim;
     auto* h = new sd_tsvad;
+    h->x3 = c->precision == 2;
     h->model.reset(new sd::TsvadModel(t));
     *out = h;
   });
@@ -177,6 +181,7 @@ int sd_tsvad_finalize(sd_tsvad* h) {
 int sd_tsvad_forward(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl,
                      float* logits, void* stream) {
   return guard([&] {
+    const sd::GemmX3Scope x3(h && h->x3);
     SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
     h->model->forward(ref, ts, B, Tf, Tl, logits, S(stream));
   });
@@ -185,6 +190,7 @@ int sd_tsvad_forward(sd_tsvad* h, const float* ref, const float* ts, int B, int 
 int sd_tsvad_forward_graph(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl, float* logits,
                            int replays, const char* dot_path, void* stream) {
   return guard([&] {
+    const sd::GemmX3Scope x3(h && h->x3);
     SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
     h->model->forward_graph(ref, ts, B, Tf, Tl, logits, replays, dot_path, S(stream));
   });
@@ -207,6 +213,7 @@ int sd_tsvad_status(sd_tsvad* h, void* stream) {
 int sd_tsvad_forward_batched(sd_tsvad* h, const float* ref, const float* ts, int B, int Tf, int Tl,
                              int forward_batch, int force, float* logits, void* stream) {
   return guard([&] {
+    const sd::GemmX3Scope x3(h && h->x3);
     SD_CHECK(h && ref && ts && logits, sd::kErrInvalid, "null argument");
     h->model->forward(ref, ts, B, Tf, Tl, logits, S(stream), forward_batch, force);
   });
@@ -223,7 +230,7 @@ int sd_eda_create(const sd_eda_config* c, sd_eda** out) {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
     SD_CHECK(c->variant >= 0 && c->variant <= 3, sd::kErrInvalid, "Unknown model type.");
     SD_CHECK(c->variant != 3 || c->n_speakers > 0, sd::kErrInvalid, "n_speakers must be positive");
-    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->precision >= 0 && c->precision <= 2, sd::kErrInvalid, "precision must be 0, 1 or 2");
     SD_CHECK(c->max_seqs > 0 && c->max_frames > 0 && c->max_n_speakers >= 2, sd::kErrInvalid,
              "bad workspace sizes");
     SD_CHECK(c->n_units > 0 && c->n_heads > 0 && c->n_units % c->n_heads == 0, sd::kErrInvalid,
@@ -241,6 +248,7 @@ int sd_eda_create(const sd_eda_config* c, sd_eda** out) {
     t.n_speakers = c->n_speakers;
     t.bf16 = c->precision == 1;
     auto* h = new sd_eda;
+    h->x3 = c->precision == 2;
     h->model.reset(new sd::EdaModel(t));
     *out = h;
   });
@@ -266,6 +274,7 @@ int sd_eda_input_stride(const sd_eda* h) { return h && h->model->finalized() ? h
 int sd_eda_forward(sd_eda* h, const float* feats, int ld_feats, int S_, int T, const int* lengths,
                    const int* key_len, const int* perm, float* probs, float* act, void* stream) {
   return guard([&] {
+    const sd::GemmX3Scope x3(h && h->x3);
     SD_CHECK(h && feats && act, sd::kErrInvalid, "null argument");
     h->model->forward(feats, ld_feats, S_, T, lengths, key_len, perm, probs, act, S(stream));
   });
@@ -287,7 +296,7 @@ int sd_eda_destroy(sd_eda* h) {
 int sd_fseend_create(const sd_fseend_config* c, sd_fseend** out) {
   return guard([&] {
     SD_CHECK(c && out, sd::kErrInvalid, "null argument");
-    SD_CHECK(c->precision == 0 || c->precision == 1, sd::kErrInvalid, "precision must be 0 or 1");
+    SD_CHECK(c->precision >= 0 && c->precision <= 2, sd::kErrInvalid, "precision must be 0, 1 or 2");
     SD_CHECK(c->max_seqs > 0 && c->max_frames > 0 && c->max_nspks > 0, sd::kErrInvalid, "bad workspace sizes");
     SD_CHECK(c->n_units > 0 && c->n_heads > 0 && c->n_units % c->n_heads == 0, sd::kErrInvalid,
              "n_units must be divisible by n_heads");
@@ -309,6 +318,7 @@ int sd_fseend_create(const sd_fseend_config* c, sd_fseend** out) {
     t.max_nspks = c->max_nspks;
     t.bf16 = c->precision == 1;
     auto* h = new sd_fseend;
+    h->x3 = c->precision == 2;
     h->model.reset(new sd::FsEendModel(t));
     *out = h;
   });
@@ -334,6 +344,7 @@ int sd_fseend_input_stride(const sd_fseend* h) { return h && h->model->finalized
 int sd_fseend_test(sd_fseend* h, const float* feats, int ld_feats, int S_, int T, const int* ilens_host,
                    int max_nspks, float* preds, float* emb, float* attractors, void* stream) {
   return guard([&] {
+    const sd::GemmX3Scope x3(h && h->x3);
     SD_CHECK(h && feats && preds, sd::kErrInvalid, "null argument");
     h->model->forward(feats, ld_feats, S_, T, ilens_host, max_nspks, preds, emb, attractors, S(stream));
   });

@@ -21,7 +21,12 @@
 // Tiles: BM x BN per 256-thread workgroup (2x2 waves), BK = 32, register-staged
 // global->LDS double buffer (one barrier per k-step).  bf16 mode converts the
 // fp32 activations to bf16 while staging and runs v_mfma_f32_16x16x32_bf16;
-// fp32 mode runs the exact-f32 v_mfma_f32_16x16x4_f32.
+// fp32 mode runs the exact-f32 v_mfma_f32_16x16x4_f32; bf16x3 mode (round 6, the
+// fp32-equivalent fast path) stages fp32 like fp32 mode and splits each operand
+// fragment in registers into bf16 hi + lo: acc += hi·hi + hi·lo + lo·hi on
+// v_mfma_f32_16x16x32_bf16 (the lo·lo term and the lo part's own rounding leave
+// ~2^-16 relative error per product; 3 MFMAs of 16 cycles per 32-k step against
+// 8 f32 MFMAs of 32).
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -34,8 +39,35 @@ constexpr int kBK = 32;
 constexpr int kLdsBf = kBK + 8;   // bf16 row stride (80 B: 16-B aligned, conflict-light)
 constexpr int kLdsF = kBK + 2;    // fp32 row stride (34 words: conflict-free 16x16x4 reads)
 
-template <int BM, int BN, bool BF16>
+thread_local bool t_gemm_x3 = false;
+
+// 8 fp32 values -> bf16 hi (round to nearest even) and lo = bf16(v - hi)
+__device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+    const float h0 = __uint_as_float(h[j] << 16), h1 = __uint_as_float(h[j] & 0xffff0000u);
+    l[j] = pack_bf16x2(v[2 * j] - h0, v[2 * j + 1] - h1);
+  }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
+
+// 8 consecutive fp32 of an LDS row (8-B aligned: the fp32 stride of 34 words) as 4 x 8-B reads
+__device__ __forceinline__ void lds_f32x8(const float* p, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float2 t = *reinterpret_cast<const float2*>(p + 2 * j);
+    v[2 * j] = t.x;
+    v[2 * j + 1] = t.y;
+  }
+}
+
+// MODE 0: exact f32 MFMA, 1: bf16 (fp32 activations converted on staging), 2: bf16x3 on fp32 tiles
+template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
+  constexpr bool BF16 = MODE == 1;
   constexpr int TM = BM / 2, TN = BN / 2;
   constexpr int MT = TM / 16, NT = TN / 16;
   constexpr int APASS = BM / 32;
@@ -192,6 +224,30 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+    } else if constexpr (MODE == 2) {
+      // one 16x16x32 k-step per BK = 32: lane (row lrow, k 8 lk .. 8 lk + 7) of every fragment, split hi / lo
+      const float* Af = reinterpret_cast<const float*>(As[buf]);
+      const float* Bf = reinterpret_cast<const float*>(Bs[buf]);
+      bf16x8 bh[NT], bl[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        float v[8];
+        lds_f32x8(Bf + (wn * TN + nt * 16 + lrow) * LDS_STRIDE + lk * 8, v);
+        split_bf16x8(v, bh[nt], bl[nt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float v[8];
+        lds_f32x8(Af + (wm * TM + mt * 16 + lrow) * LDS_STRIDE + lk * 8, v);
+        bf16x8 ah, al;
+        split_bf16x8(v, ah, al);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], acc[mt][nt], 0, 0, 0);
+        }
+      }
     } else {
       const float* Af = reinterpret_cast<const float*>(As[buf]);
       const float* Bf = reinterpret_cast<const float*>(Bs[buf]);
@@ -249,12 +305,18 @@ void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   const int M = p.B * p.Ho * p.Wo;
   dim3 grid(cdiv(p.N, BN), cdiv(M, BM));
   if (bf16)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, true>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1>), grid, dim3(256), 0, st, p);
+  else if (t_gemm_x3)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 2>), grid, dim3(256), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, false>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 0>), grid, dim3(256), 0, st, p);
 }
 
 }  // namespace
+
+bool gemm_x3() { return t_gemm_x3; }
+GemmX3Scope::GemmX3Scope(bool on) : prev(t_gemm_x3) { t_gemm_x3 = on; }
+GemmX3Scope::~GemmX3Scope() { t_gemm_x3 = prev; }
 
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(p.K == p.kh * p.kw * p.Cin, kErrInvalid, "conv_gemm: K != kh*kw*Cin");
@@ -284,7 +346,7 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   const double flops = 2.0 * M * p.N * (double)p.K;
   const double bytes = 4.0 * p.B * p.H * p.W * p.Cin + (bf16 ? 2.0 : 4.0) * p.N * p.K +
                        4.0 * M * p.N * (p.res ? 2.0 : 1.0);
-  ProfScope prof(bf16 ? "conv_gemm_bf16" : "conv_gemm_f32", flops, bytes, st);
+  ProfScope prof(bf16 ? "conv_gemm_bf16" : t_gemm_x3 ? "conv_gemm_bf16x3" : "conv_gemm_f32", flops, bytes, st);
   const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
   const int tiles128 = cdiv(M, 128) * cdiv(p.N, bn);
   const bool big = tiles128 >= 512;

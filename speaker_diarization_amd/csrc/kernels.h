@@ -76,6 +76,16 @@ inline int glu_interleave_row(int r, int C) {   // new row index of original row
   return (c / 16) * 32 + (gate ? 16 : 0) + c % 16;
 }
 void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st);
+// Arithmetic of conv_gemm's exact (non-bf16) path on this host thread: false = the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32); true = "bf16x3": each fp32 operand split into bf16 hi + lo, acc += hi·hi + hi·lo +
+// lo·hi on v_mfma_f32_16x16x32_bf16 (fp32 accumulate; ~2^-16 relative per product, 5.3x the f32 MFMA rate).
+// Handles created with precision 2 set it around their compute calls (capi.cpp, GemmX3Scope).
+bool gemm_x3();
+struct GemmX3Scope {
+  explicit GemmX3Scope(bool on);
+  ~GemmX3Scope();
+  bool prev;
+};
 void conv_gemm_bf16(const ConvGemmArgs& p, hipStream_t st);   // bf16-MFMA production kernel
 bool gemm_dma_supported(const ConvGemmArgs& p);               // bf16 A, no prologue, taps==1 or Cin%64==0
 // Split-K: the split count worth using for p on the gemm_dma path (1 = none), and the launch writing

@@ -21,8 +21,8 @@ class TransformerModel:
                  max_frames: int = 2000):
         if has_pos:
             raise NotImplementedError("has_pos=True is not on the inference path")
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be bf16 or fp32, got {precision}")
+        if precision not in ("bf16", "fp32", "bf16x3"):
+            raise ValueError(f"precision must be bf16, fp32 or bf16x3, got {precision}")
         self.cfg = EDAConfig(n_speakers=n_speakers, in_size=in_size, n_heads=n_heads, n_units=n_units,
                              n_layers=n_layers, dim_feedforward=dim_feedforward)
         self.n_speakers = n_speakers
@@ -40,7 +40,7 @@ class TransformerModel:
         conf = _lib.EdaConfig(variant=3, in_size=c.in_size, n_units=c.n_units, n_heads=c.n_heads,
                               n_layers=c.n_layers, dim_feedforward=c.dim_feedforward, max_seqs=self.max_seqs,
                               max_frames=self.max_frames, max_n_speakers=2,
-                              precision=1 if self.precision == "bf16" else 0, n_speakers=c.n_speakers)
+                              precision={"fp32": 0, "bf16": 1, "bf16x3": 2}[self.precision], n_speakers=c.n_speakers)
         h = _lib.create_handle("eda", conf, _lib.host_state(state_dict))
         self._release()
         self._h = h

@@ -64,8 +64,8 @@ class _EdaBase:
                  max_seqs: int = 8, max_frames: int = 2000):
         import torch
         cfg.variant  # validates model/encoder type like the reference constructor
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be bf16 or fp32, got {precision}")
+        if precision not in ("bf16", "fp32", "bf16x3"):
+            raise ValueError(f"precision must be bf16, fp32 or bf16x3, got {precision}")
         self.cfg = cfg
         self.precision = precision
         self.max_seqs = max_seqs
@@ -84,7 +84,7 @@ class _EdaBase:
         conf = _lib.EdaConfig(variant=c.variant, in_size=c.in_size, n_units=c.n_units, n_heads=c.n_heads,
                               n_layers=c.n_layers, dim_feedforward=c.dim_feedforward, max_seqs=self.max_seqs,
                               max_frames=self.max_frames, max_n_speakers=max_n_speakers,
-                              precision=1 if self.precision == "bf16" else 0)
+                              precision={"fp32": 0, "bf16": 1, "bf16x3": 2}[self.precision])
         h = ctypes.c_void_p()
         _lib.call("sd_eda_create", ctypes.byref(conf), ctypes.byref(h))
         try:

@@ -27,8 +27,8 @@ class OnlineTransformerDADiarization:
                  max_seqlen, dec_dim_feedforward, conv_delay=9, mask_delay=0, decom_kernel_size=64, *,
                  device=None, precision: str = "fp32", max_seqs: int = 1, max_frames: int = None,
                  max_nspks: int = 6):
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be bf16 or fp32, got {precision}")
+        if precision not in ("bf16", "fp32", "bf16x3"):
+            raise ValueError(f"precision must be bf16, fp32 or bf16x3, got {precision}")
         self.cfg = FSEENDConfig(n_speakers=n_speakers, in_size=in_size, n_units=n_units, n_heads=n_heads,
                                 enc_n_layers=enc_n_layers, dec_n_layers=dec_n_layers, dropout=dropout,
                                 has_mask=has_mask, max_seqlen=max_seqlen, dec_dim_feedforward=dec_dim_feedforward,
@@ -54,7 +54,7 @@ class OnlineTransformerDADiarization:
                                  dec_dim_feedforward=c.dec_dim_feedforward, conv_delay=c.conv_delay,
                                  mask_delay=c.mask_delay, has_mask=int(bool(c.has_mask)), max_seqs=self.max_seqs,
                                  max_frames=self.max_frames, max_nspks=self.max_nspks,
-                                 precision=1 if self.precision == "bf16" else 0)
+                                 precision={"fp32": 0, "bf16": 1, "bf16x3": 2}[self.precision])
         h = _lib.create_handle("fseend", conf, _lib.host_state(unwrap_checkpoint(state_dict)))
         self._release()
         self._h = h

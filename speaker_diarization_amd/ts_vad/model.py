@@ -32,8 +32,8 @@ class TSVADModel:
                 if hasattr(task_cfg, k):
                     setattr(self.cfg, k, getattr(task_cfg, k))
         assert self.cfg.label_rate == 25, f"self.label_rate is {self.cfg.label_rate} not support!"
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be bf16 or fp32, got {precision}")
+        if precision not in ("bf16", "fp32", "bf16x3"):
+            raise ValueError(f"precision must be bf16, fp32 or bf16x3, got {precision}")
         self.precision = precision
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
@@ -49,7 +49,7 @@ class TSVADModel:
         c = self.cfg
         conf = _lib.TsvadConfig(
             variant=c.variant, max_num_speaker=c.max_num_speaker, rs_len=c.rs_len, max_batch=self.max_batch,
-            max_fbank_frames=self.max_fbank, precision=1 if self.precision == "bf16" else 0,
+            max_fbank_frames=self.max_fbank, precision={"fp32": 0, "bf16": 1, "bf16x3": 2}[self.precision],
             num_transformer_layer=c.num_transformer_layer, num_attention_head=c.num_attention_head,
             transformer_embed_dim=c.transformer_embed_dim,
             transformer_ffn_embed_dim=c.transformer_ffn_embed_dim, speaker_embed_dim=c.speaker_embed_dim)

@@ -57,13 +57,13 @@ def test_eend_features_real_length_and_bad_transform(gpu):
         eend_features(wav, transform_type="logmel40")
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("name", list(EDA_CASES))
 def test_eda_forward_matches_golden(gpu, name, precision):
     mtype, L, lens, nspk, iseed, wseed = EDA_CASES[name]
     g = _load(name)
     m = _model(mtype, L, wseed, precision)
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    tol = BF16_ATOL if precision == "bf16" else FP32_ATOL   # bf16x3: fp32-equivalent GEMMs
     xs = eda_inputs(lens, seed=iseed)
     offs = np.cumsum([0] + lens)
     for i, x in enumerate(xs):

@@ -33,13 +33,13 @@ def _fseend(delay, wseed, precision="fp32", max_seqs=2, max_frames=512, max_nspk
     return m
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("name", list(FSEEND_CASES))
 def test_fseend_test_matches_golden(gpu, name, precision):
     lens, C, delay, iseed, wseed = FSEEND_CASES[name]
     g = _load(name)
     m = _fseend(delay, wseed, precision)
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    tol = BF16_ATOL if precision == "bf16" else FP32_ATOL   # bf16x3: fp32-equivalent GEMMs
     xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
     out, emb, att = m.test(xs, lens, max_nspks=C)
     np.testing.assert_allclose(torch.cat(out).cpu().numpy(), g["out"], atol=tol)
@@ -73,7 +73,7 @@ def _fseend_empty():
     return OnlineTransformerDADiarization(None, 345, 256, 4, 4, 2, 0.1, True, 10000, 2048, max_frames=64)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("name", list(EEND_CASES))
 def test_eend_matches_golden(gpu, name, precision):
     nspk, L, lens, iseed, wseed = EEND_CASES[name]
@@ -82,7 +82,7 @@ def test_eend_matches_golden(gpu, name, precision):
     m.load_state_dict(to_torch(synthetic_state_dict(eend_layout(EDAConfig(n_speakers=nspk, n_layers=L)), wseed)))
     xs = [torch.from_numpy(x) for x in eda_inputs(lens, seed=iseed)]
     ys = m(xs, activation=torch.sigmoid)
-    tol = FP32_ATOL if precision == "fp32" else BF16_ATOL
+    tol = BF16_ATOL if precision == "bf16" else FP32_ATOL   # bf16x3: fp32-equivalent GEMMs
     np.testing.assert_allclose(torch.cat(ys).cpu().numpy(), g["ys"], atol=tol)
     with pytest.raises(AttributeError):
         m(xs, has_mask=True, activation=torch.sigmoid)

@@ -33,7 +33,7 @@ def _model(v, rs, wseed, precision, gpu):
     return _models[key]
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("name", list(TSVAD_CASES))
 def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
     v, rs, B, T, nl, iseed, wseed = TSVAD_CASES[name]
@@ -44,10 +44,10 @@ def test_tsvad_forward_vs_reference_golden(gpu, name, precision):
     out = m.forward(torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu), labels).cpu().numpy()
     err = np.abs(out - g["logits"]).max()
     print(f"{name} {precision}: max|logit diff| = {err:.3e} (|logit| max {np.abs(g['logits']).max():.3f})")
-    assert err < (FP32_ATOL if precision == "fp32" else BF16_ATOL)
+    assert err < (BF16_ATOL if precision == "bf16" else FP32_ATOL)   # bf16x3: fp32-equivalent, the fp32 bound
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("name", list(TSVAD_DYN_CASES))
 def test_tsvad_dynamic_variant_vs_reference_golden(gpu, name, precision):
     """The 'dynamic' weight variant on the bench meeting's windows (reference run, make_golden.py
@@ -64,7 +64,7 @@ def test_tsvad_dynamic_variant_vs_reference_golden(gpu, name, precision):
     d = out - g["logits"]
     ratio = float(np.sqrt((d ** 2).mean()) / g["logits"].std(axis=-1).mean())
     print(f"{name} {precision}: max|logit diff| {np.abs(d).max():.3e}, rms diff / frame std {ratio:.3e}")
-    if precision == "fp32":
+    if precision != "bf16":     # fp32 and bf16x3 (fp32-equivalent GEMMs): the north_star bound
         assert np.abs(d).max() < FP32_ATOL
     else:
         assert ratio < 0.2
@@ -154,7 +154,7 @@ def test_tsvad_length_assert(gpu):
         m.forward(x, ts, torch.zeros(1, 4, 90))
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("variant", [0, 1])
 def test_pipeline_vs_oracle(gpu, variant, precision):
     """Meeting wav in HBM -> posteriors, vs the CPU restatement of the reference
@@ -179,7 +179,7 @@ def test_pipeline_vs_oracle(gpu, variant, precision):
     # posterior level (the bf16 product path measured 1.2e-3 / 1.4e-3 on MI355X for v1 / v0): 1e-3 fp32
     # (north_star), 3e-3 bf16 (about 2x measured); and the recipe's threshold decisions (ts_vad2/infer.py
     # thresholds) agree on >= 99 % of the frames at every threshold
-    assert err < (1e-3 if precision == "fp32" else 3e-3)
+    assert err < (3e-3 if precision == "bf16" else 1e-3)
     for thr in (0.2, 0.3, 0.35, 0.4, 0.45, 0.5, 0.55, 0.6, 0.7, 0.8):
         flips = int(((post[:3] > thr) != (ref[:3] > thr)).sum())
         assert flips <= 0.01 * post[:3].size, (thr, flips)
