@@ -22,11 +22,13 @@
 // global->LDS double buffer (one barrier per k-step).  bf16 mode converts the
 // fp32 activations to bf16 while staging and runs v_mfma_f32_16x16x32_bf16;
 // fp32 mode runs the exact-f32 v_mfma_f32_16x16x4_f32; bf16x3 mode (round 6, the
-// fp32-equivalent fast path) stages fp32 like fp32 mode and splits each operand
-// fragment in registers into bf16 hi + lo: acc += hi·hi + hi·lo + lo·hi on
+// fp32-equivalent fast path: conv_gemm_x3_kernel) keeps fp32 tensors and splits every
+// staged element into bf16 hi + lo: acc += lo·hi + hi·lo + hi·hi on
 // v_mfma_f32_16x16x32_bf16 (the lo·lo term and the lo part's own rounding leave
 // ~2^-16 relative error per product; 3 MFMAs of 16 cycles per 32-k step against
 // 8 f32 MFMAs of 32).
+#include <string>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -41,30 +43,7 @@ constexpr int kLdsF = kBK + 2;    // fp32 row stride (34 words: conflict-free 16
 
 thread_local bool t_gemm_x3 = false;
 
-// 8 fp32 values -> bf16 hi (round to nearest even) and lo = bf16(v - hi)
-__device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
-  uint32_t h[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    h[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
-    const float h0 = __uint_as_float(h[j] << 16), h1 = __uint_as_float(h[j] & 0xffff0000u);
-    l[j] = pack_bf16x2(v[2 * j] - h0, v[2 * j + 1] - h1);
-  }
-  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-  lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
-}
-
-// 8 consecutive fp32 of an LDS row (8-B aligned: the fp32 stride of 34 words) as 4 x 8-B reads
-__device__ __forceinline__ void lds_f32x8(const float* p, float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float2 t = *reinterpret_cast<const float2*>(p + 2 * j);
-    v[2 * j] = t.x;
-    v[2 * j + 1] = t.y;
-  }
-}
-
-// MODE 0: exact f32 MFMA, 1: bf16 (fp32 activations converted on staging), 2: bf16x3 on fp32 tiles
+// MODE 0: exact f32 MFMA, 1: bf16 (fp32 activations converted on staging); bf16x3: conv_gemm_x3_kernel
 template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
   constexpr bool BF16 = MODE == 1;
@@ -106,7 +85,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
   }
 
   const int KT = (p.K + kBK - 1) / kBK;
-  float4 areg[APASS];
+  // raw loads only: the BN-ReLU prologue is applied in store_tile, after the k-step's MFMAs, so no wait for a
+  // load sits between a k-step's loads and its MFMAs (applied at load time, the compiler waited for each load)
+  float4 areg[APASS], s4, h4;
+  uint32_t avalid = 0;
   // B staging registers.
   constexpr int BCHUNK = BF16 ? (BN * 4) : (BN * 8);   // 16-B chunks per tile
   constexpr int BPASS = (BCHUNK + 255) / 256;
@@ -119,11 +101,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
     const int ti = tap / p.kw;
     const int tj = tap - ti * p.kw;
     const int c = c0 + kq;
-    float4 s4, h4;
     if (p.pre_scale && k0 + kq < p.K) {
       s4 = *reinterpret_cast<const float4*>(p.pre_scale + c);
       h4 = *reinterpret_cast<const float4*>(p.pre_shift + c);
     }
+    avalid = 0;
 #pragma unroll
     for (int i = 0; i < APASS; ++i) {
       int hi = rh[i] + ti * p.dh;
@@ -132,12 +114,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
       if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && k0 + kq < p.K) {
         const float* src = reinterpret_cast<const float*>(p.A) + ((int64_t)(rbh[i] + hi) * p.W + wi) * p.lda + p.a_coff + c;
         v = *reinterpret_cast<const float4*>(src);
-        if (p.pre_scale) {
-          v.x = fmaxf(v.x * s4.x + h4.x, 0.f);
-          v.y = fmaxf(v.y * s4.y + h4.y, 0.f);
-          v.z = fmaxf(v.z * s4.z + h4.z, 0.f);
-          v.w = fmaxf(v.w * s4.w + h4.w, 0.f);
-        }
+        avalid |= 1u << i;
       }
       areg[i] = v;
     }
@@ -166,6 +143,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
 #pragma unroll
     for (int i = 0; i < APASS; ++i) {
       int row = i * 32 + (tid >> 3);
+      if (p.pre_scale && (avalid >> i & 1u)) {   // padded taps stay exact zeros
+        areg[i].x = fmaxf(areg[i].x * s4.x + h4.x, 0.f);
+        areg[i].y = fmaxf(areg[i].y * s4.y + h4.y, 0.f);
+        areg[i].z = fmaxf(areg[i].z * s4.z + h4.z, 0.f);
+        areg[i].w = fmaxf(areg[i].w * s4.w + h4.w, 0.f);
+      }
       if (BF16) {
         uint2 pk;
         pk.x = (uint32_t)f2bf_bits(areg[i].x) | ((uint32_t)f2bf_bits(areg[i].y) << 16);
@@ -224,30 +207,6 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
-    } else if constexpr (MODE == 2) {
-      // one 16x16x32 k-step per BK = 32: lane (row lrow, k 8 lk .. 8 lk + 7) of every fragment, split hi / lo
-      const float* Af = reinterpret_cast<const float*>(As[buf]);
-      const float* Bf = reinterpret_cast<const float*>(Bs[buf]);
-      bf16x8 bh[NT], bl[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        float v[8];
-        lds_f32x8(Bf + (wn * TN + nt * 16 + lrow) * LDS_STRIDE + lk * 8, v);
-        split_bf16x8(v, bh[nt], bl[nt]);
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        float v[8];
-        lds_f32x8(Af + (wm * TM + mt * 16 + lrow) * LDS_STRIDE + lk * 8, v);
-        bf16x8 ah, al;
-        split_bf16x8(v, ah, al);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], acc[mt][nt], 0, 0, 0);
-        }
-      }
     } else {
       const float* Af = reinterpret_cast<const float*>(As[buf]);
       const float* Bf = reinterpret_cast<const float*>(Bs[buf]);
@@ -299,6 +258,238 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
   }
 }
 
+// 4 fp32 -> bf16 hi (round to nearest even) and lo = bf16(v - hi) (v - hi is exact in fp32), 2 words each
+__device__ __forceinline__ void split_bf16x4(const float4& v, uint2& hi, uint2& lo) {
+  hi.x = pack_bf16x2(v.x, v.y);
+  hi.y = pack_bf16x2(v.z, v.w);
+  lo.x = pack_bf16x2(v.x - __uint_as_float(hi.x << 16), v.y - __uint_as_float(hi.x & 0xffff0000u));
+  lo.y = pack_bf16x2(v.z - __uint_as_float(hi.y << 16), v.w - __uint_as_float(hi.y & 0xffff0000u));
+}
+
+// LDS offset (bf16 elements) of 16-B chunk c (k 8c .. 8c + 7) of tile row r in the bf16x3 tiles: 64-B rows,
+// chunk XOR (r >> 1) & 3.  Conflict-free for both accesses (MI355X_MICROARCH.md LDS table): the stores
+// (ds_write_b64, 16 contiguous lanes = 2 rows x 64 B, banks mod 32) and the fragment reads (ds_read_b128 in
+// its 4 x 16-lane groups, banks mod 64), where the 80-B padded rows left a 2-way conflict on both.
+__device__ __forceinline__ int x3_chunk(int r, int c) { return r * kBK + ((c ^ ((r >> 1) & 3)) << 3); }
+
+// bf16x3 GEMM (round 6).  Every fp32 element is split ONCE, by the thread that stages it, into bf16 hi (RNE)
+// and lo = bf16(x - hi), written to hi / lo LDS tiles (64-B rows, x3_chunk swizzle); the waves read ready bf16
+// fragments with ds_read_b128.  Per 32-deep k-step a wave issues, per 16x16 output tile, lo_A·hi_B, hi_A·lo_B,
+// hi_A·hi_B (fp32 accumulate, that order for every accumulator).  The loads are unconditional (out-of-range
+// rows / taps read chunk 0 and are zeroed when staged) and the BN-ReLU prologue is applied at staging, so the
+// k-step's MFMAs never wait for its own loads.  LDS: hi + lo tiles of A and B, double-buffered =
+// 2 * 2 * (BM + BN) * 64 B (64 KiB at 128 x 128: two workgroups per CU).
+// Measured on C2 (bf16x3 line): the first form, each wave re-splitting the fp32
+// fragments it read from fp32 tiles, 153 ms; this form 126 ms.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_gemm_x3_kernel(ConvGemmArgs p) {
+  constexpr int TM = BM / 2, TN = BN / 2;
+  constexpr int MT = TM / 16, NT = TN / 16;
+  constexpr int APASS = BM / 32;
+  constexpr int S = kBK;   // 64-B rows, 16-B chunks XOR-swizzled by x3_chunk (no padding)
+  constexpr int ABUF = 2 * BM * S, BBUF = 2 * BN * S;   // hi tile then lo tile
+  extern __shared__ __attribute__((aligned(16))) uint16_t smx[];
+  uint16_t* const As = smx;                 // [2][ABUF]
+  uint16_t* const Bs = smx + 2 * ABUF;      // [2][BBUF]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int M = p.B * p.Ho * p.Wo;
+  const int m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+
+  int rbh[APASS], rh[APASS], rw[APASS];
+  const int kq = (tid & 7) * 4;
+#pragma unroll
+  for (int i = 0; i < APASS; ++i) {
+    int m = m0 + i * 32 + (tid >> 3);
+    if (m < M) {
+      int wo = m % p.Wo;
+      int t = m / p.Wo;
+      int ho = t % p.Ho;
+      int b = t / p.Ho;
+      rbh[i] = b * p.H;
+      rh[i] = ho * p.sh - p.ph;
+      rw[i] = wo * p.sw - p.pw;
+    } else {
+      rbh[i] = 0;
+      rh[i] = -(1 << 28);
+      rw[i] = 0;
+    }
+  }
+
+  const int KT = (p.K + kBK - 1) / kBK;
+  constexpr int BPASS = (BN * 8 + 255) / 256;   // 16-B fp32 chunks of the B tile
+  // raw loads only: the BN-ReLU prologue is applied in store_tile, after the MFMAs, so no wait for a load
+  // sits between a k-step's loads and its MFMAs (applied at load time, the compiler waited for each load).
+  // (two register stages, each k-step's loads issued two compute phases ahead, measured 127 -> 186 ms on C2:
+  // the second stage's registers cost the second workgroup per CU)
+  struct Stage {
+    float4 a[APASS], b[BPASS], s4, h4;
+    uint32_t av, bv;
+  };
+  Stage st;
+
+  auto load_tile = [&](int kt, Stage& sg) {
+    const int k0 = kt * kBK;
+    const int tap = k0 / p.Cin;
+    const int c0 = k0 - tap * p.Cin;
+    const int ti = tap / p.kw;
+    const int tj = tap - ti * p.kw;
+    const int c = c0 + kq;
+    if (p.pre_scale && k0 + kq < p.K) {
+      sg.s4 = *reinterpret_cast<const float4*>(p.pre_scale + c);
+      sg.h4 = *reinterpret_cast<const float4*>(p.pre_shift + c);
+    }
+    sg.av = 0;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      int hi = rh[i] + ti * p.dh;
+      int wi = rw[i] + tj * p.dw;
+      // unconditional load (an out-of-range tap reads the tensor's first chunk, zeroed in store_tile): with
+      // exec-masked loads the compiler copied every loaded register at the top of the MFMA phase, i.e.
+      // waited for the loads there
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W && k0 + kq < p.K;
+      const int64_t off = ok ? ((int64_t)(rbh[i] + hi) * p.W + wi) * p.lda + p.a_coff + c : 0;
+      sg.a[i] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.A) + off);
+      sg.av |= (ok ? 1u : 0u) << i;
+    }
+    sg.bv = 0;
+#pragma unroll
+    for (int i = 0; i < BPASS; ++i) {
+      const int ch = tid + i * 256;
+      const int n = ch >> 3, kc = (ch & 7) * 4;
+      const bool ok = ch < BN * 8 && n0 + n < p.N && k0 + kc < p.K;
+      sg.b[i] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.Wt) +
+                                                 (ok ? (int64_t)(n0 + n) * p.K + k0 + kc : 0));
+      sg.bv |= (ok ? 1u : 0u) << i;
+    }
+  };
+
+  auto store_tile = [&](int buf, const Stage& sg) {
+    uint16_t* a = As + buf * ABUF;
+    uint16_t* b = Bs + buf * BBUF;
+#pragma unroll
+    for (int i = 0; i < APASS; ++i) {
+      const int row = i * 32 + (tid >> 3);
+      float4 v = sg.a[i];
+      if (!(sg.av >> i & 1u)) {
+        v = make_float4(0.f, 0.f, 0.f, 0.f);    // padded taps are exact zeros
+      } else if (p.pre_scale) {
+        v.x = fmaxf(v.x * sg.s4.x + sg.h4.x, 0.f);
+        v.y = fmaxf(v.y * sg.s4.y + sg.h4.y, 0.f);
+        v.z = fmaxf(v.z * sg.s4.z + sg.h4.z, 0.f);
+        v.w = fmaxf(v.w * sg.s4.w + sg.h4.w, 0.f);
+      }
+      uint2 h, l;
+      split_bf16x4(v, h, l);
+      const int o = x3_chunk(row, kq >> 3) + (kq & 4);
+      *reinterpret_cast<uint2*>(a + o) = h;
+      *reinterpret_cast<uint2*>(a + BM * S + o) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BPASS; ++i) {
+      const int ch = tid + i * 256;
+      if (ch < BN * 8) {
+        const int n = ch >> 3, kc = (ch & 7) * 4;
+        uint2 h, l;
+        split_bf16x4((sg.bv >> i & 1u) ? sg.b[i] : make_float4(0.f, 0.f, 0.f, 0.f), h, l);
+        const int o = x3_chunk(n, kc >> 3) + (kc & 4);
+        *reinterpret_cast<uint2*>(b + o) = h;
+        *reinterpret_cast<uint2*>(b + BN * S + o) = l;
+      }
+    }
+  };
+
+  floatx4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int lrow = lane & 15;
+  const int lk = lane >> 4;
+  auto compute = [&](int buf) {
+    const uint16_t* a = As + buf * ABUF;
+    const uint16_t* b = Bs + buf * BBUF;
+    bf16x8 bh[NT], bl[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int o = x3_chunk(wn * TN + nt * 16 + lrow, lk);
+      bh[nt] = *reinterpret_cast<const bf16x8*>(b + o);
+      bl[nt] = *reinterpret_cast<const bf16x8*>(b + BN * S + o);
+    }
+    // per row tile, term-major over the NT column tiles: NT - 1 independent MFMAs between two on the same
+    // accumulator, which sums al·bh, ah·bl, ah·bh in that order
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int o = x3_chunk(wm * TM + mt * 16 + lrow, lk);
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a + o);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + BM * S + o);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+
+  load_tile(0, st);
+  store_tile(0, st);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tile(kt + 1, st);
+    compute(buf);
+    if (kt + 1 < KT) store_tile(buf ^ 1, st);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * TM + mt * 16 + lk * 4 + r;
+      if (m >= M) continue;
+      const int wo = m % p.Wo;
+      const int t = m / p.Wo;
+      const int ho = t % p.Ho;
+      const int b = t / p.Ho;
+      const int64_t obase = (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = n0 + wn * TN + nt * 16 + lrow;
+        if (n >= p.N) continue;
+        float v = acc[mt][nt][r];
+        if (p.alpha) v *= p.alpha[n];
+        if (p.beta) v += p.beta[n];
+        if (p.res) v += reinterpret_cast<const float*>(p.res)[(int64_t)m * p.res_ld + n];
+        v = apply_act(v, p.act);
+        if (p.gate) v *= p.gate[((int64_t)b * p.gate_nseg + wo / p.gate_seg) * p.N + n];
+        reinterpret_cast<float*>(p.out)[obase + (int64_t)n * p.o_sn] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+void launch_x3(const ConvGemmArgs& p, dim3 grid, hipStream_t st) {
+  constexpr int kBytes = 2 * (2 * BM + 2 * BN) * kBK * (int)sizeof(uint16_t);   // 2 buffers x (hi+lo of A, B)
+  static bool attr = [] {
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<BM, BN>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kBytes));
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((conv_gemm_x3_kernel<BM, BN>), grid, dim3(256), kBytes, st, p);
+}
+
 template <int BM, int BN>
 void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(!p.a_bf16 && !p.out_bf16 && !p.res_bf16, kErrInvalid, "fp32 conv_gemm takes fp32 tensors");
@@ -307,7 +498,7 @@ void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   if (bf16)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1>), grid, dim3(256), 0, st, p);
   else if (t_gemm_x3)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 2>), grid, dim3(256), 0, st, p);
+    launch_x3<BM, BN>(p, grid, st);
   else
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 0>), grid, dim3(256), 0, st, p);
 }
@@ -346,7 +537,12 @@ void conv_gemm(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   const double flops = 2.0 * M * p.N * (double)p.K;
   const double bytes = 4.0 * p.B * p.H * p.W * p.Cin + (bf16 ? 2.0 : 4.0) * p.N * p.K +
                        4.0 * M * p.N * (p.res ? 2.0 : 1.0);
-  ProfScope prof(bf16 ? "conv_gemm_bf16" : t_gemm_x3 ? "conv_gemm_bf16x3" : "conv_gemm_f32", flops, bytes, st);
+  static const bool detail = getenv("SDIAR_PROF_DETAIL") != nullptr;
+  std::string key = bf16 ? "conv_gemm_bf16" : t_gemm_x3 ? "conv_gemm_bf16x3" : "conv_gemm_f32";
+  if (detail && prof_enabled())
+    key += " M=" + std::to_string(M) + " N=" + std::to_string(p.N) + " K=" + std::to_string(p.K) +
+           " taps=" + std::to_string(p.kh * p.kw) + (p.pre_scale ? " pre" : "");
+  ProfScope prof(key.c_str(), flops, bytes, st);
   const int bn = p.N >= 128 ? 128 : (p.N >= 64 ? 64 : 32);
   const int tiles128 = cdiv(M, 128) * cdiv(p.N, bn);
   const bool big = tiles128 >= 512;

@@ -1,4 +1,5 @@
-"""Print per-kernel (and per-GEMM-shape with SDIAR_PROF_DETAIL=1) timing of one pipeline step."""
+"""Print per-kernel (and per-GEMM-shape with SDIAR_PROF_DETAIL=1) timing of one pipeline step.
+    python tools/kernel_table.py [variant 0|1] [minutes] [precision bf16|fp32|bf16x3]"""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))   # the repo root
 import torch
@@ -10,9 +11,10 @@ from speaker_diarization_amd.weights import TSVADConfig, to_torch, tsvad_state_d
 
 variant = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 minutes = float(sys.argv[2]) if len(sys.argv) > 2 else 10.0
+precision = sys.argv[3] if len(sys.argv) > 3 else "bf16"
 cfg = TSVADConfig(rs_len=4) if variant == 0 else TSVADConfig.ots_vad_v1(rs_len=6)
 dev = torch.device("cuda", 0)
-m = TSVADModel(cfg, device=dev, precision="bf16", max_batch=int(os.environ.get("SDIAR_MAX_BATCH", "256")))
+m = TSVADModel(cfg, device=dev, precision=precision, max_batch=int(os.environ.get("SDIAR_MAX_BATCH", "640")))
 m.load_state_dict(to_torch(tsvad_state_dict(cfg, seed=777)))
 pipe = TSVADPipeline(m, 1, 64)
 mt = make_meeting(minutes * 60, 4, seed=777)
