@@ -472,10 +472,10 @@ def variant_posteriors(job, a, dev, sd_np, precision):
 def variant_der(job, a, dev, meeting, n_win):
     """DER parity that can fail (round-5 verdict item 1): the same span on the 'dynamic' weight variant
     (weights.py dynamic_weights: gsp_fc and the BiLSTM input centred and scaled upstream, fc x4, so the
-    activations move with the frame and 99 % of the posteriors sit in [0.2, 0.8]), GPU fp32 and GPU in the
-    line's precision against the fp32 CPU oracle.  fp32 is the gate; on this variant bf16 as a number format
-    moves the DER by more than 0.1 whichever stage computes in it (tests/bf16_der_emulation.py),
-    so the bf16 figures measure that, not a kernel difference."""
+    activations move with the frame and 99 % of the posteriors sit in [0.2, 0.8]), GPU fp32, GPU bf16x3 and GPU
+    in the line's precision against the fp32 CPU oracle.  fp32 and bf16x3 are the gate; on this variant bf16 as
+    a number format moves the DER by more than 0.1 whichever stage computes in it (tests/bf16_der_emulation.py,
+    DESIGN.md §6 round-6 item 1), so the bf16 figures measure that, not a kernel difference."""
     import torch
     from oracle.pipeline_ref import meeting_posteriors
     from speaker_diarization_amd.weights import to_torch, tsvad_state_dict
@@ -484,14 +484,15 @@ def variant_der(job, a, dev, meeting, n_win):
     cpu_post = meeting_posteriors(to_torch(sd), job["cfg"], meeting.wav, job["ts_np"], job["n_lab"], shift=1,
                                   batch_size=min(64, n_win), max_windows=n_win)
     out = {}
-    for prec in ("fp32", a.precision):
+    for prec in dict.fromkeys(("fp32", "bf16x3", a.precision)):
         g = variant_posteriors(job, a, dev, sd, prec)
         d = der_parity(meeting, g, cpu_post, float(n_win))
         d.pop("note", None)
         d["posterior_parity"] = posterior_parity(g, cpu_post, n_win * 25)
         out[prec] = d
-    out["note"] = ("fp32 is the gate (|dDER| <= 0.1 at every threshold on a non-degenerate table); bf16 on this "
-                   "variant measures the number format's effect (tests/bf16_der_emulation.py), not parity")
+    out["note"] = ("fp32 and bf16x3 (fp32-equivalent split-bf16 GEMMs) are the gate (|dDER| <= 0.1 at every "
+                   "threshold on a non-degenerate table); bf16 on this variant measures the number format's effect "
+                   "(tests/bf16_der_emulation.py), not parity")
     return out
 
 
