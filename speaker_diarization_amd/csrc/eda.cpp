@@ -11,6 +11,7 @@
 #include "eda.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace sd {
 
@@ -55,8 +56,21 @@ void EdaModel::finalize() {
     for (size_t i = 0; i < bias.size(); ++i) bias[i] = bi.data[i] + bh.data[i];
     *b = arena_.upload(bias);
     *hh = arena_.upload(wh.data);
-    // bf16 mode: a bf16 copy feeds the group-persistent recurrence kernel (lstm.hip).
-    if (cfg_.bf16) (hh == &enc_hh_ ? enc_hh_bf_ : dec_hh_bf_) = upload_packed(arena_, wh.data, 4 * E, E, 1, 1, true).w;
+    // bf16 mode: a bf16 copy feeds the group-persistent recurrence kernel (lstm.hip).  fp32 handles also keep
+    // hi = bf16(W) and lo = bf16(W - hi) for the bf16x3 mode's split recurrence (exact fp32 mode uses neither).
+    (hh == &enc_hh_ ? enc_hh_bf_ : dec_hh_bf_) = upload_packed(arena_, wh.data, 4 * E, E, 1, 1, true).w;
+    if (!cfg_.bf16) {
+      std::vector<float> lo(wh.data.size());
+      for (size_t i = 0; i < lo.size(); ++i) {
+        uint32_t u;
+        std::memcpy(&u, &wh.data[i], 4);
+        u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;   // bf16 round to nearest even (finite weights)
+        float hi;
+        std::memcpy(&hi, &u, 4);
+        lo[i] = wh.data[i] - hi;
+      }
+      (hh == &enc_hh_ ? enc_hh_lo_ : dec_hh_lo_) = upload_packed(arena_, lo, 4 * E, E, 1, 1, true).w;
+    }
   };
   if (plain) {
     dec_ = ld.linear("decoder");
@@ -124,11 +138,13 @@ void EdaModel::forward(const float* feats, int ld_in, int S, int T, const int* l
   // EDA: shuffle -> encoder LSTM (packed) -> decoder LSTM from (h, c)
   gather_rows(X_, S, T, E, perm, lengths, Y_, st);
   conv_gemm(lin(Tens{Y_, false}, rows, E, enc_ih_, enc_b_, Tens{G_, false}, 4 * E), bf, st);
+  // bf16: the bf16 recurrence; bf16x3 (precision 2): the split recurrence; fp32: the exact-f32 step kernel
+  const bool x3 = !bf && gemm_x3();
   lstm_recurrence(G_, S, T, E, 1, enc_hh_, lengths, nullptr, nullptr, nullptr, 0, hT_, cT_, lstm_work_, st,
-                  enc_hh_bf_, lstm_err_.get(0));
+                  bf || x3 ? enc_hh_bf_ : nullptr, lstm_err_.get(0), x3 ? enc_hh_lo_ : nullptr);
   fill_rows(dec_b_, 4 * E, S * NA, Gd_, st);
   lstm_recurrence(Gd_, S, NA, E, 1, dec_hh_, nullptr, hT_, cT_, att_, E, nullptr, nullptr, lstm_work_, st,
-                  dec_hh_bf_, lstm_err_.get(1));
+                  bf || x3 ? dec_hh_bf_ : nullptr, lstm_err_.get(1), x3 ? dec_hh_lo_ : nullptr);
   attractor_scores(X_, S, T, E, att_, NA, lin_w_, lin_b_, probs, act, st);
 }
 

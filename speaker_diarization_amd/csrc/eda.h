@@ -57,7 +57,8 @@ class EdaModel {
   PackedW enc_ih_;
   const float *enc_b_ = nullptr, *enc_hh_ = nullptr;
   const float *dec_b_ = nullptr, *dec_hh_ = nullptr;
-  const void *enc_hh_bf_ = nullptr, *dec_hh_bf_ = nullptr;   // bf16 copies (bf16 mode)
+  const void *enc_hh_bf_ = nullptr, *dec_hh_bf_ = nullptr;   // bf16 copies (bf16 mode; the hi part in fp32 mode)
+  const void *enc_hh_lo_ = nullptr, *dec_hh_lo_ = nullptr;   // bf16(W - hi) (fp32 handles: the bf16x3 recurrence)
   const float *lin_w_ = nullptr, *lin_b_ = nullptr;
   ConvL dec_;   // variant 3: decoder Linear -> sigmoid
 

@@ -402,6 +402,9 @@ void groupnorm_silu(void* y, int S, int T, int C, const float* partial, const fl
 // h0/c0 optional (ndir, B, H); hT/cT optional outputs (ndir, B, H).
 // whh_bf16 (optional, same layout in bf16 bits): bf16-MFMA recurrence (bf16 mode); the
 // cell state, gates and h stay fp32, h is rounded to bf16 only as the MFMA operand.
+// whh_lo (optional, with whh_bf16 = bf16(W) as the hi part): bf16(W - hi), the bf16x3 mode's split
+// recurrence (W_lo h_hi + W_hi h_lo + W_hi h_hi, h exchanged as hi + lo); where the persistent kernel cannot
+// run, the exact-f32 step kernel (never the bf16 one).
 // work: per-handle device scratch of lstm_work_floats(B, H, ndir) floats (the persistent bf16
 // kernel keeps its h exchange and counters there).  host_err (optional, the DEVICE address of a pinned
 // slot of the handle's PinnedFlags): a persistent launch whose poll timed out sets it to 1 from the
@@ -417,7 +420,7 @@ float lstm_granule_probe(int steps, hipStream_t st, int nwg = 4);
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
                      float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16 = nullptr,
-                     int* host_err = nullptr);
+                     int* host_err = nullptr, const void* whh_lo = nullptr);
 
 // ---------------------------------------------------------------- frontend
 // Kaldi fbank (torchaudio.compliance.kaldi.fbank semantics used by

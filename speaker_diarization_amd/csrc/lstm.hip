@@ -216,9 +216,14 @@ constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (25
 // WV (round 5, default for an even MT): 8 waves per workgroup instead of 4 -- two waves per 16-unit tile, each
 // on half of the group's row tiles (tile j * 2 + (wave >> 2)), so every SIMD holds two waves of the step and one's
 // gx loads, transcendentals and stores overlap the other's MFMAs; W slice, counters and exchange are unchanged.
-template <int MT, int WV = 4>
+// X3 (round 6, the bf16x3 mode's recurrence): W_hh and h both as bf16 hi + lo, acc += W_lo h_hi + W_hi h_lo +
+// W_hi h_hi per fragment (the GEMMs' split, fp32-equivalent).  The W_lo rows a wave multiplies (4 gates x its 16
+// units x H) stay in its registers for the whole launch (32 fragments, 128 VGPRs: one wave per SIMD), W_hi in LDS
+// as in bf16 mode; h is published as a hi plane and a lo plane.  MT 1 only (the register budget).
+template <int MT, int WV = 4, bool X3 = false>
 __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
+    const uint16_t* __restrict__ whl,
     const int* __restrict__ lengths, const float* __restrict__ h0, const float* __restrict__ c0,
     float* __restrict__ out, int ldo, float* __restrict__ hT, float* __restrict__ cT,
     uint16_t* __restrict__ hx, int Bp, unsigned* __restrict__ counters, int* __restrict__ err,
@@ -226,6 +231,7 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   constexpr int H = LS_H, BB = 16 * MT, NT = 64 * WV, WPU = WV / 4, MTW = MT / WPU;
   static_assert(WV == 4 || WV == 8, "4 or 8 waves");
   static_assert(MT % WPU == 0, "the row tiles split evenly over the waves of a unit tile");
+  static_assert(!X3 || (MT == 1 && WV == 4), "the split recurrence holds W_lo in registers: one row tile");
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, wt = tid >> 8;
   const int l15 = lane & 15, g = lane >> 4;
@@ -248,12 +254,27 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
           *reinterpret_cast<const uint4*>(wd + (int64_t)(gate * H + 64 * q + j) * H + k8);
     }
   }
-  // h exchange: hx[parity][d][Bp][H] bf16; h_t lives in parity (t + 1) & 1, h_{-1} in 0.
-  constexpr int EB = 2;   // bytes per exchanged value
+  // W_lo fragments of this wave's rows (X3): fragment (gate, k0 / 32) as the MFMA reads W_hi from LDS
+  constexpr int NWL = X3 ? 4 * (H / 32) : 1;
+  bf16x8 wl[NWL];
+  if constexpr (X3) {
+    const uint16_t* wd = whl + (int64_t)d * 4 * H * H;
+#pragma unroll
+    for (int gate = 0; gate < 4; ++gate)
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+        wl[gate * (H / 32) + kc] = *reinterpret_cast<const bf16x8*>(
+            wd + (int64_t)(gate * H + 64 * q + 16 * w + l15) * H + kc * 32 + 8 * g);
+  }
+  // h exchange: hx[parity][part][d][Bp][H] bf16 (part: hi, then lo in X3 mode); h_t lives in parity (t + 1) & 1,
+  // h_{-1} in 0.
+  constexpr int EB = 2;          // bytes per exchanged value
+  constexpr int NP = X3 ? 2 : 1;
   const int64_t plane = (int64_t)ndir * Bp * H;
-  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * plane * EB), 0x00020000);
-  auto hx_off = [&](int parity, int b, int u) {   // byte offset
-    return (uint32_t)(((int64_t)parity * plane + ((int64_t)d * Bp + b) * H + u) * EB);
+  const __amdgpu_buffer_rsrc_t rh =
+      __builtin_amdgcn_make_buffer_rsrc(hx, (short)0, (int)(2 * NP * plane * EB), 0x00020000);
+  auto hx_off = [&](int parity, int b, int u, int part = 0) {   // byte offset
+    return (uint32_t)(((int64_t)(parity * NP + part) * plane + ((int64_t)d * Bp + b) * H + u) * EB);
   };
   float c[MTW][4], hr[MTW][4];
   int len[MTW];
@@ -277,6 +298,11 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     for (int mt = 0; mt < MTW; ++mt) {
       const u32x2_t v = {pack_bf16x2(hr[mt][0], hr[mt][1]), pack_bf16x2(hr[mt][2], hr[mt][3])};
       __builtin_amdgcn_raw_buffer_store_b64(v, rh, hx_off(parity, rb(mt), ub), 0, 16);   // sc1
+      if constexpr (X3) {   // lo = bf16(h - hi), exact residual
+        const u32x2_t l = {pack_bf16x2(hr[mt][0] - __uint_as_float(v[0] << 16), hr[mt][1] - __uint_as_float(v[0] & 0xffff0000u)),
+                           pack_bf16x2(hr[mt][2] - __uint_as_float(v[1] << 16), hr[mt][3] - __uint_as_float(v[1] & 0xffff0000u))};
+        __builtin_amdgcn_raw_buffer_store_b64(l, rh, hx_off(parity, rb(mt), ub, 1), 0, 16);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -323,6 +349,7 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) acc[mt][gate] = floatx4{0.f, 0.f, 0.f, 0.f};
     bf16x8 hfa[MTW][H / 32];
+    bf16x8 hla[X3 ? MTW : 1][X3 ? H / 32 : 1];
     wait_for(4u * (step + 1));   // all 4 quarters published h_{step-1}
     // every h fragment of the step requested at once (one L2 round trip, not one per k-step;
     // s_memtime stamps: 5.1 k of a 10 k-cycle C1 step went to eight serial load -> MFMA waits)
@@ -332,6 +359,12 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
       for (int mt = 0; mt < MTW; ++mt)
         hfa[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                      rh, hx_off(pin, rb(mt), kc * 32 + 8 * g), 0, 16));
+    if constexpr (X3) {
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+        hla[0][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rh, hx_off(pin, rb(0), kc * 32 + 8 * g, 1), 0, 16));
+    }
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MTW];
@@ -340,6 +373,10 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) {
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
+        if constexpr (X3) {   // small terms first, as the split GEMMs
+          acc[0][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[gate * (H / 32) + k0 / 32], hf[0], acc[0][gate], 0, 0, 0);
+          acc[0][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hla[0][k0 / 32], acc[0][gate], 0, 0, 0);
+        }
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt)
           acc[mt][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mt], acc[mt][gate], 0, 0, 0);
@@ -573,21 +610,22 @@ unsigned lstm_spin_limit() {
   return launches++ < n_forced ? v : (1u << 22);
 }
 
-template <int MT, int WV = 4>
+template <int MT, int WV = 4, bool X3 = false>
 void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* whh_bf16, const int* lengths,
                          const float* h0, const float* c0, float* out, int ldo, float* hT, float* cT,
-                         uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st) {
+                         uint16_t* hx, int Bp, unsigned* counters, int* err, int* host_err, hipStream_t st,
+                         const void* whh_lo = nullptr) {
   const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
   static bool attr = false;
   if (!attr) {
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV, X3>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const int groups = ndir * cdiv(B, 16 * MT);
-  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, WV>), dim3(4 * groups), dim3(64 * WV), smem, st, gx, B, T, ndir,
-                     reinterpret_cast<const uint16_t*>(whh_bf16), lengths, h0, c0, out, ldo, hT, cT, hx, Bp,
-                     counters, err, lstm_spin_limit(), host_err);
+  hipLaunchKernelGGL((lstm_group_bf16_kernel<MT, WV, X3>), dim3(4 * groups), dim3(64 * WV), smem, st, gx, B, T,
+                     ndir, reinterpret_cast<const uint16_t*>(whh_bf16), reinterpret_cast<const uint16_t*>(whh_lo),
+                     lengths, h0, c0, out, ldo, hT, cT, hx, Bp, counters, err, lstm_spin_limit(), host_err);
   SD_LAUNCH_CHECK();
 }
 
@@ -595,15 +633,15 @@ void launch_lstm_group_t(const float* gx, int B, int T, int ndir, const void* wh
 // This is the check hipLaunchCooperativeKernel would make (MI355X guide, "Residency and
 // cooperative launch": a plain launch of the same grid has the same residency); a cooperative
 // launch itself is avoided because its queue's teardown crashes rocprofv3's exit path here.
-template <int MT, int WV = 4>
+template <int MT, int WV = 4, bool X3 = false>
 int lstm_group_blocks_per_cu() {
   static int nb = -1;
   if (nb < 0) {
     const size_t smem = sizeof(uint16_t) * 256 * LS_WS;
-    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV>),
+    SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lstm_group_bf16_kernel<MT, WV, X3>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int v = 0;
-    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, WV>, 64 * WV, smem));
+    SD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, lstm_group_bf16_kernel<MT, WV, X3>, 64 * WV, smem));
     nb = v;
   }
   return nb;
@@ -663,7 +701,8 @@ int lstm_group_mt(int B, int ndir) {
 
 // Layout of the persistent kernel's scratch inside the caller's `work`: the double-buffered bf16
 // h exchange, then (16-B aligned) one counter per group and the err word.
-size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
+// (x2: the split recurrence's hi and lo planes)
+size_t lstm_group_hx_bytes(int Bp, int ndir) { return ((size_t)2 * 2 * ndir * Bp * LS_H * 2 + 15) / 16 * 16; }
 
 }  // namespace
 
@@ -737,12 +776,14 @@ int64_t lstm_work_floats(int B, int H, int ndir) {
 
 void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float* whh,
                      const int* lengths, const float* h0, const float* c0, float* out, int ldo,
-                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16, int* host_err) {
+                     float* hT, float* cT, float* work, hipStream_t st, const void* whh_bf16, int* host_err,
+                     const void* whh_lo) {
   SD_CHECK(H % 32 == 0, kErrInvalid, "lstm: H must be a multiple of 32");
+  SD_CHECK(!whh_lo || whh_bf16, kErrInvalid, "lstm: the split recurrence needs W_hh hi and lo");
   static const bool no_seq = getenv("SDIAR_NO_LSTM_SEQ") != nullptr;
   if (whh_bf16 && H == LS_H && !no_seq && (ldo % 4 == 0 || !out)) {
     const int mt = lstm_group_mt(B, ndir);
-    if (mt) {
+    if (mt && (!whh_lo || (mt == 1 && lstm_group_blocks_per_cu<1, 4, true>() >= 1))) {
       const int Bp = cdiv(B, 16 * mt) * 16 * mt;
       const int groups = ndir * cdiv(B, 16 * mt);
       // Exchange buffers + counters live in the caller's per-handle `work` (lstm_work_floats), so
@@ -758,6 +799,11 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
                      4.0 * ((double)B * T * ndir * 4 * H + (double)B * T * ndir * H), st);
       prof.set_steps(T);   // sequential steps (an upper bound with packed lengths: the launch runs max(len))
       int* err = reinterpret_cast<int*>(ctl + (size_t)groups * LS_CNT_STRIDE);
+      if (whh_lo) {
+        launch_lstm_group_t<1, 4, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err,
+                                        host_err, st, whh_lo);
+        return;
+      }
       switch (mt) {
         case 1: launch_lstm_group<1>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
         case 2: launch_lstm_group<2>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err, host_err, st); break;
@@ -771,6 +817,7 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       return;
     }
   }
+  if (whh_lo) whh_bf16 = nullptr;   // the split mode's fallback is the exact-f32 step kernel, not the bf16 one
   const int64_t n = (int64_t)ndir * B * H;
   float* hA = work;
   float* hB = work + n;
