@@ -60,8 +60,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int M = p.B * p.Ho * p.Wo;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  // 1-D grid, XCD-grouped (xcd_remap): the column tiles of one row block are consecutive tiles and run on one
+  // XCD, so its L2 fetches the block's A rows once instead of every XCD fetching them (A is the large operand)
+  const int n_nt = (p.N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / n_nt) * BM;
+  const int n0 = (tile % n_nt) * BN;
 
   // Per-thread A rows (fixed across the k loop).
   int rbh[APASS], rh[APASS], rw[APASS];
@@ -280,7 +284,10 @@ __device__ __forceinline__ int x3_chunk(int r, int c) { return r * kBK + ((c ^ (
 // k-step's MFMAs never wait for its own loads.  LDS: hi + lo tiles of A and B, double-buffered =
 // 2 * 2 * (BM + BN) * 64 B (64 KiB at 128 x 128: two workgroups per CU).
 // Measured on C2 (bf16x3 line): the first form, each wave re-splitting the fp32
-// fragments it read from fp32 tiles, 153 ms; this form 126 ms.
+// fragments it read from fp32 tiles, 153 ms; this form 126 ms.  Also measured, no better: an LDS-DMA-fed form
+// (raw fp32 stages converted in place, 2-4 stage ring: 142-214 ms), every row tile's MFMAs interleaved for the
+// wide tiles too (126.3 ms), the XCD-grouped 1-D grid (127.0 ms; kept: neutral here, it keeps a row block's
+// A reads in one XCD's L2).
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(ConvGemmArgs p) {
   constexpr int TM = BM / 2, TN = BN / 2;
@@ -297,8 +304,12 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(ConvGemmArgs p) {
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int M = p.B * p.Ho * p.Wo;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  // 1-D grid, XCD-grouped (xcd_remap): the column tiles of one row block are consecutive tiles and run on one
+  // XCD, so its L2 fetches the block's A rows once instead of every XCD fetching them (A is the large operand)
+  const int n_nt = (p.N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / n_nt) * BM;
+  const int n0 = (tile % n_nt) * BN;
 
   int rbh[APASS], rh[APASS], rw[APASS];
   const int kq = (tid & 7) * 4;
@@ -421,22 +432,49 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(ConvGemmArgs p) {
       bh[nt] = *reinterpret_cast<const bf16x8*>(b + o);
       bl[nt] = *reinterpret_cast<const bf16x8*>(b + BN * S + o);
     }
-    // per row tile, term-major over the NT column tiles: NT - 1 independent MFMAs between two on the same
-    // accumulator, which sums al·bh, ah·bl, ah·bh in that order
+    if constexpr (NT >= 4) {
+      // per row tile, term-major over the NT column tiles: NT - 1 independent MFMAs between two on the same
+      // accumulator, which sums al·bh, ah·bl, ah·bh in that order
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int o = x3_chunk(wm * TM + mt * 16 + lrow, lk);
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a + o);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + BM * S + o);
+      for (int mt = 0; mt < MT; ++mt) {
+        const int o = x3_chunk(wm * TM + mt * 16 + lrow, lk);
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a + o);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + BM * S + o);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], acc[mt][nt], 0, 0, 0);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], acc[mt][nt], 0, 0, 0);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], acc[mt][nt], 0, 0, 0);
+      }
+    } else {
+      // narrow tiles (NT 1-2): term-major over every (mt, nt), so MT x NT - 1 independent MFMAs separate two
+      // on one accumulator (per row tile they were back to back: 128 x 32 waited on each MFMA's result)
+      bf16x8 ah[MT], al[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int o = x3_chunk(wm * TM + mt * 16 + lrow, lk);
+        ah[mt] = *reinterpret_cast<const bf16x8*>(a + o);
+        al[mt] = *reinterpret_cast<const bf16x8*>(a + BM * S + o);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
     }
   };
 
@@ -494,7 +532,7 @@ template <int BM, int BN>
 void launch_tile(const ConvGemmArgs& p, bool bf16, hipStream_t st) {
   SD_CHECK(!p.a_bf16 && !p.out_bf16 && !p.res_bf16, kErrInvalid, "fp32 conv_gemm takes fp32 tensors");
   const int M = p.B * p.Ho * p.Wo;
-  dim3 grid(cdiv(p.N, BN), cdiv(M, BM));
+  dim3 grid(cdiv(p.N, BN) * cdiv(M, BM));
   if (bf16)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, 1>), grid, dim3(256), 0, st, p);
   else if (t_gemm_x3)
