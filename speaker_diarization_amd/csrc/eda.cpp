@@ -59,18 +59,7 @@ void EdaModel::finalize() {
     // bf16 mode: a bf16 copy feeds the group-persistent recurrence kernel (lstm.hip).  fp32 handles also keep
     // hi = bf16(W) and lo = bf16(W - hi) for the bf16x3 mode's split recurrence (exact fp32 mode uses neither).
     (hh == &enc_hh_ ? enc_hh_bf_ : dec_hh_bf_) = upload_packed(arena_, wh.data, 4 * E, E, 1, 1, true).w;
-    if (!cfg_.bf16) {
-      std::vector<float> lo(wh.data.size());
-      for (size_t i = 0; i < lo.size(); ++i) {
-        uint32_t u;
-        std::memcpy(&u, &wh.data[i], 4);
-        u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;   // bf16 round to nearest even (finite weights)
-        float hi;
-        std::memcpy(&hi, &u, 4);
-        lo[i] = wh.data[i] - hi;
-      }
-      (hh == &enc_hh_ ? enc_hh_lo_ : dec_hh_lo_) = upload_packed(arena_, lo, 4 * E, E, 1, 1, true).w;
-    }
+    if (!cfg_.bf16) (hh == &enc_hh_ ? enc_hh_lo_ : dec_hh_lo_) = upload_bf16_lo(arena_, wh.data);
   };
   if (plain) {
     dec_ = ld.linear("decoder");

@@ -219,7 +219,7 @@ constexpr int LS_CNT_STRIDE = 64;   // unsigned words between group counters (25
 // X3 (round 6, the bf16x3 mode's recurrence): W_hh and h both as bf16 hi + lo, acc += W_lo h_hi + W_hi h_lo +
 // W_hi h_hi per fragment (the GEMMs' split, fp32-equivalent).  The W_lo rows a wave multiplies (4 gates x its 16
 // units x H) stay in its registers for the whole launch (32 fragments, 128 VGPRs: one wave per SIMD), W_hi in LDS
-// as in bf16 mode; h is published as a hi plane and a lo plane.  MT 1 only (the register budget).
+// as in bf16 mode; h is published as a hi plane and a lo plane.  MT <= 2, 4 waves (the register budget).
 template <int MT, int WV = 4, bool X3 = false>
 __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     const float* __restrict__ gx, int B, int T, int ndir, const uint16_t* __restrict__ whh,
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   constexpr int H = LS_H, BB = 16 * MT, NT = 64 * WV, WPU = WV / 4, MTW = MT / WPU;
   static_assert(WV == 4 || WV == 8, "4 or 8 waves");
   static_assert(MT % WPU == 0, "the row tiles split evenly over the waves of a unit tile");
-  static_assert(!X3 || (MT == 1 && WV == 4), "the split recurrence holds W_lo in registers: one row tile");
+  static_assert(!X3 || (MT <= 2 && WV == 4), "the split recurrence holds W_lo in registers: <= 2 row tiles");
   extern __shared__ __attribute__((aligned(16))) uint16_t wsl[];   // [4 gates * 64 units][LS_WS]
   const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, wt = tid >> 8;
   const int l15 = lane & 15, g = lane >> 4;
@@ -362,8 +362,10 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     if constexpr (X3) {
 #pragma unroll
       for (int kc = 0; kc < H / 32; ++kc)
-        hla[0][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rh, hx_off(pin, rb(0), kc * 32 + 8 * g, 1), 0, 16));
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt)
+          hla[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rh, hx_off(pin, rb(mt), kc * 32 + 8 * g, 1), 0, 16));
     }
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
@@ -374,8 +376,11 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
       for (int gate = 0; gate < 4; ++gate) {
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
         if constexpr (X3) {   // small terms first, as the split GEMMs
-          acc[0][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[gate * (H / 32) + k0 / 32], hf[0], acc[0][gate], 0, 0, 0);
-          acc[0][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hla[0][k0 / 32], acc[0][gate], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MTW; ++mt) {
+            acc[mt][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[gate * (H / 32) + k0 / 32], hf[mt], acc[mt][gate], 0, 0, 0);
+            acc[mt][gate] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hla[mt][k0 / 32], acc[mt][gate], 0, 0, 0);
+          }
         }
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt)
@@ -783,7 +788,9 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
   static const bool no_seq = getenv("SDIAR_NO_LSTM_SEQ") != nullptr;
   if (whh_bf16 && H == LS_H && !no_seq && (ldo % 4 == 0 || !out)) {
     const int mt = lstm_group_mt(B, ndir);
-    if (mt && (!whh_lo || (mt == 1 && lstm_group_blocks_per_cu<1, 4, true>() >= 1))) {
+    const bool x3_ok = mt == 1 ? lstm_group_blocks_per_cu<1, 4, true>() >= 1
+                     : mt == 2 ? lstm_group_blocks_per_cu<2, 4, true>() >= 1 : false;
+    if (mt && (!whh_lo || x3_ok)) {
       const int Bp = cdiv(B, 16 * mt) * 16 * mt;
       const int groups = ndir * cdiv(B, 16 * mt);
       // Exchange buffers + counters live in the caller's per-handle `work` (lstm_work_floats), so
@@ -800,8 +807,12 @@ void lstm_recurrence(const float* gx, int B, int T, int H, int ndir, const float
       prof.set_steps(T);   // sequential steps (an upper bound with packed lengths: the launch runs max(len))
       int* err = reinterpret_cast<int*>(ctl + (size_t)groups * LS_CNT_STRIDE);
       if (whh_lo) {
-        launch_lstm_group_t<1, 4, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err,
-                                        host_err, st, whh_lo);
+        if (mt == 1)
+          launch_lstm_group_t<1, 4, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err,
+                                          host_err, st, whh_lo);
+        else
+          launch_lstm_group_t<2, 4, true>(gx, B, T, ndir, whh_bf16, lengths, h0, c0, out, ldo, hT, cT, hx, Bp, ctl, err,
+                                          host_err, st, whh_lo);
         return;
       }
       switch (mt) {

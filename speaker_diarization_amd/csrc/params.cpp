@@ -102,4 +102,17 @@ PackedW upload_packed(DeviceArena& arena, const std::vector<float>& w, int N, in
   return p;
 }
 
+const void* upload_bf16_lo(DeviceArena& arena, const std::vector<float>& w) {
+  std::vector<uint16_t> lo(w.size());
+  for (size_t i = 0; i < w.size(); ++i) {
+    const uint32_t hb = (uint32_t)f2bf_host(w[i]) << 16;
+    float hi;
+    std::memcpy(&hi, &hb, 4);
+    lo[i] = f2bf_host(w[i] - hi);
+  }
+  void* d = arena.alloc(lo.size() * 2);
+  SD_HIP(hipMemcpy(d, lo.data(), lo.size() * 2, hipMemcpyHostToDevice));
+  return d;
+}
+
 }  // namespace sd

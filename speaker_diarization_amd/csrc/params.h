@@ -113,5 +113,7 @@ class ParamStore {
 // Converts a packed fp32 weight to the device layout (bf16 bits when bf16).
 PackedW upload_packed(DeviceArena& arena, const std::vector<float>& w, int N, int Cin, int kh,
                       int kw, bool bf16);
+// bf16(w - bf16(w)) element for element (same layout): the lo part of the bf16x3 split, hi = upload_packed(bf16)
+const void* upload_bf16_lo(DeviceArena& arena, const std::vector<float>& w);
 
 }  // namespace sd

@@ -83,7 +83,9 @@ void TsvadModel::finalize() {
     lstm_ih_ = upload_packed(arena_, wih, 8 * H, (int)wi0.shape[1], 1, 1, cfg_.bf16);
     lstm_b_ = arena_.upload(bias);
     lstm_hh_ = arena_.upload(whh);
-    if (cfg_.bf16) lstm_hh_bf_ = upload_packed(arena_, whh, 2 * 4 * H, H, 1, 1, true).w;
+    // bf16 copy for the bf16 recurrence; fp32 handles keep hi / lo for the bf16x3 mode's split recurrence
+    lstm_hh_bf_ = upload_packed(arena_, whh, 2 * 4 * H, H, 1, 1, true).w;
+    if (!cfg_.bf16) lstm_hh_lo_ = upload_bf16_lo(arena_, whh);
     fc_ = loader().linear("fc");
   }
   auto extra = ps_.unused();
@@ -318,8 +320,10 @@ void TsvadModel::forward(const float* ref, const float* ts, int B, int Tf, int T
     conv_gemm(lin(Tens{X2_, bf}, B * Tl, NS * E, lstm_ih_, lstm_b_, Tens{H_, false}, 8 * Hh), bf, st);
     // SDIAR_LSTM_FP32 (diagnostic, tools/parity_stages.py): the exact-fp32 recurrence in bf16 mode too
     static const bool lstm_fp32 = getenv("SDIAR_LSTM_FP32") != nullptr;
+    const bool x3 = !bf && gemm_x3();   // bf16x3 (precision 2): the split recurrence; fp32: exact step kernel
     lstm_recurrence(H_, B, Tl, Hh, 2, lstm_hh_, nullptr, nullptr, nullptr, Y_, 2 * Hh, nullptr,
-                    nullptr, lstm_work_, st, lstm_fp32 ? nullptr : lstm_hh_bf_, lstm_err_.get(0));
+                    nullptr, lstm_work_, st, (bf && !lstm_fp32) || x3 ? lstm_hh_bf_ : nullptr, lstm_err_.get(0),
+                    x3 ? lstm_hh_lo_ : nullptr);
     ConvGemmArgs f = cam_conv1d(Tens{Y_, false}, B, Tl, 2 * Hh, fc_, 1, 0, 1, Tens{logits, false}, 1);
     f.o_sb = (int64_t)NS * Tl; f.o_sw = 1; f.o_sn = Tl;
     conv_gemm(f, bf, st);

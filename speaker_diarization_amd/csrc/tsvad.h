@@ -79,7 +79,8 @@ class TsvadModel {
   std::vector<ConformerL> conf_;
   PackedW lstm_ih_;
   const float *lstm_b_ = nullptr, *lstm_hh_ = nullptr;
-  const void* lstm_hh_bf_ = nullptr;   // bf16 copy of W_hh (bf16 mode)
+  const void* lstm_hh_bf_ = nullptr;   // bf16 copy of W_hh (bf16 mode; the hi part in fp32 mode)
+  const void* lstm_hh_lo_ = nullptr;   // bf16(W_hh - hi) (fp32 handles: the bf16x3 split recurrence)
   ConvL fc_;
 
   // CAM++ trunk of a large batch as two window slices, the second on side_ (fork / join events on the
