@@ -69,7 +69,7 @@ WORKLOADS = {
 # dense TFLOP/s (MI355X_MICROARCH.md); bf16x3 = the bf16 peak over its 3 MFMAs per fp32-equivalent product
 PEAKS = {"bf16": 2500.0, "f32": 157.3, "bf16x3": 2500.0 / 3}
 HBM_PEAK = 8000.0                        # GB/s
-ATTN_KERNELS = ("mha_block", "attention_bf16", "attention_f32")   # fused block first (C2 conformer)
+ATTN_KERNELS = ("mha_block", "attention_bf16", "attention_bf16x3", "attention_f32")   # fused block first (C2)
 
 
 def parse(argv=None):
@@ -162,7 +162,9 @@ def roofline_of(name, st, traffic=None):
     kernel's algorithmic work sits closer to (max(flops/peak_flops,
     bytes/peak_bw) over the measured time), and `achieved` is quoted in that roof's unit."""
     secs = st["ms"] * 1e-3
-    dt = "f32" if name.endswith("f32") else "bf16"
+    # f32 MFMA peak for exact-f32 kernels; the bf16 peak / 3 for bf16x3 kernels (their flops are the fp32
+    # products; each costs three bf16 MFMA products); else bf16
+    dt = "f32" if name.endswith("f32") else "bf16x3" if name.endswith("bf16x3") else "bf16"
     tf = st["flops"] / secs / 1e12 if st["flops"] > 0 else 0.0
     gbs = st["bytes"] / secs / 1e9
     f_mfma, f_hbm = tf / PEAKS[dt], gbs / HBM_PEAK
