@@ -43,6 +43,87 @@ constexpr int kLdsF = kBK + 2;    // fp32 row stride (34 words: conflict-free 16
 
 thread_local bool t_gemm_x3 = false;
 
+// LDS-staged fp32 epilogue (round 6): the accumulator tile goes to LDS (BM x (BN + 4) floats), then each thread
+// owns one 4-column group of rows r0, r0 + 256 / (BN / 4), ...: per-channel alpha / beta loaded once, the rows'
+// residuals fetched before any store (res may alias out: the in-place residual adds), float4 stores along the
+// output rows.  The per-element form it replaces (a 64-B piece per 16 lanes, a divide chain per row, a scalar
+// alpha / beta load per element) took 45 % of the bf16x3 GEMM time on C2.
+// General outputs (strided, gated) keep a per-element loop over the staged tile.
+template <int BM, int BN, int MT, int NT>
+__device__ __forceinline__ void staged_epilogue_f32(const ConvGemmArgs& p, const floatx4 (&acc)[MT][NT], float* Cs,
+                                                    int m0, int n0, int M) {
+  constexpr int TM = BM / 2, TN = BN / 2, CLD = BN + 4, CPR = BN / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, lrow = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(wm * TM + mt * 16 + lk * 4 + r) * CLD + wn * TN + nt * 16 + lrow] = acc[mt][nt][r];
+  __syncthreads();
+  float* const outp = reinterpret_cast<float*>(p.out);
+  const bool lin = out_rows_linear(p);
+  if (lin && p.o_sn == 1 && (p.o_sw & 3) == 0 && !p.gate && (!p.res || (p.res_ld & 3) == 0)) {
+    constexpr int RPI = 256 / CPR, ITER = BM / RPI;
+    const int cg = tid % CPR, r0 = tid / CPR, n = n0 + cg * 4;
+    if (n >= p.N) return;
+    const bool full = n + 3 < p.N;
+    float al[4], be[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = full || n + u < p.N;
+      al[u] = (p.alpha && ok) ? p.alpha[n + u] : 1.f;
+      be[u] = (p.beta && ok) ? p.beta[n + u] : 0.f;
+    }
+    float4 rv[ITER];
+    if (p.res) {
+      const float* rbase = reinterpret_cast<const float*>(p.res);
+#pragma unroll
+      for (int i = 0; i < ITER; ++i) {
+        const int m = m0 + r0 + i * RPI;
+        rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M) {
+          const float* r = rbase + (int64_t)m * p.res_ld + n;
+          if (full) rv[i] = *reinterpret_cast<const float4*>(r);
+          else {
+            rv[i].x = r[0];
+            if (n + 1 < p.N) rv[i].y = r[1];
+            if (n + 2 < p.N) rv[i].z = r[2];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int row = r0 + i * RPI, m = m0 + row;
+      if (m >= M) break;
+      const float4 c4 = *reinterpret_cast<const float4*>(Cs + row * CLD + cg * 4);
+      float v[4] = {c4.x, c4.y, c4.z, c4.w};
+      const float r4[4] = {p.res ? rv[i].x : 0.f, p.res ? rv[i].y : 0.f, p.res ? rv[i].z : 0.f, p.res ? rv[i].w : 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u] * al[u] + be[u] + r4[u], p.act);
+      const int64_t o = (int64_t)m * p.o_sw + n;
+      if (full) *reinterpret_cast<float4*>(outp + o) = make_float4(v[0], v[1], v[2], v[3]);
+      else
+        for (int u = 0; u < 4 && n + u < p.N; ++u) outp[o + u] = v[u];
+    }
+    return;
+  }
+  for (int q = tid; q < BM * BN; q += 256) {
+    const int row = q / BN, col = q % BN, m = m0 + row, n = n0 + col;
+    if (m >= M || n >= p.N) continue;
+    const int wo = m % p.Wo, t = m / p.Wo, ho = t % p.Ho, b = t / p.Ho;
+    float v = Cs[row * CLD + col];
+    if (p.alpha) v *= p.alpha[n];
+    if (p.beta) v += p.beta[n];
+    if (p.res) v += reinterpret_cast<const float*>(p.res)[(int64_t)m * p.res_ld + n];
+    v = apply_act(v, p.act);
+    if (p.gate) v *= p.gate[((int64_t)b * p.gate_nseg + wo / p.gate_seg) * p.N + n];
+    outp[(int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw + (int64_t)n * p.o_sn] = v;
+  }
+}
+
 // MODE 0: exact f32 MFMA, 1: bf16 (fp32 activations converted on staging); bf16x3: conv_gemm_x3_kernel
 template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
@@ -52,8 +133,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
   constexpr int APASS = BM / 32;
   using LdsT = typename std::conditional<BF16, uint16_t, float>::type;
   constexpr int LDS_STRIDE = BF16 ? kLdsBf : kLdsF;
-  __shared__ __attribute__((aligned(16))) LdsT As[2][BM * LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) LdsT Bs[2][BN * LDS_STRIDE];
+  // one array (As then Bs) so the exact-f32 epilogue can stage its tile over both
+  __shared__ __attribute__((aligned(16))) LdsT smem[2 * (BM + BN) * LDS_STRIDE];
+  LdsT (*const As)[BM * LDS_STRIDE] = reinterpret_cast<LdsT (*)[BM * LDS_STRIDE]>(smem);
+  LdsT (*const Bs)[BN * LDS_STRIDE] = reinterpret_cast<LdsT (*)[BN * LDS_STRIDE]>(smem + 2 * BM * LDS_STRIDE);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -234,7 +317,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs p) {
     __syncthreads();
   }
 
-  // Epilogue.
+  // Epilogue: staged through LDS in exact-f32 mode (the tile fits the fp32 operand buffers)
+  if constexpr (!BF16 && (int)sizeof(smem) >= BM * (BN + 4) * 4) {
+    staged_epilogue_f32<BM, BN, MT, NT>(p, acc, reinterpret_cast<float*>(smem), m0, n0, M);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -488,37 +575,14 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(ConvGemmArgs p) {
     if (kt + 1 < KT) store_tile(buf ^ 1, st);
     __syncthreads();
   }
-
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * TM + mt * 16 + lk * 4 + r;
-      if (m >= M) continue;
-      const int wo = m % p.Wo;
-      const int t = m / p.Wo;
-      const int ho = t % p.Ho;
-      const int b = t / p.Ho;
-      const int64_t obase = (int64_t)b * p.o_sb + (int64_t)ho * p.o_sh + (int64_t)wo * p.o_sw;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int n = n0 + wn * TN + nt * 16 + lrow;
-        if (n >= p.N) continue;
-        float v = acc[mt][nt][r];
-        if (p.alpha) v *= p.alpha[n];
-        if (p.beta) v += p.beta[n];
-        if (p.res) v += reinterpret_cast<const float*>(p.res)[(int64_t)m * p.res_ld + n];
-        v = apply_act(v, p.act);
-        if (p.gate) v *= p.gate[((int64_t)b * p.gate_nseg + wo / p.gate_seg) * p.N + n];
-        reinterpret_cast<float*>(p.out)[obase + (int64_t)n * p.o_sn] = v;
-      }
-    }
-  }
+  staged_epilogue_f32<BM, BN, MT, NT>(p, acc, reinterpret_cast<float*>(smx), m0, n0, M);
 }
 
 template <int BM, int BN>
 void launch_x3(const ConvGemmArgs& p, dim3 grid, hipStream_t st) {
-  constexpr int kBytes = 2 * (2 * BM + 2 * BN) * kBK * (int)sizeof(uint16_t);   // 2 buffers x (hi+lo of A, B)
+  constexpr int kRing = 2 * (2 * BM + 2 * BN) * kBK * (int)sizeof(uint16_t);   // 2 buffers x (hi+lo of A, B)
+  constexpr int kEpi = BM * (BN + 4) * (int)sizeof(float);                      // the staged epilogue tile
+  constexpr int kBytes = kRing > kEpi ? kRing : kEpi;
   static bool attr = [] {
     SD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<BM, BN>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, kBytes));
