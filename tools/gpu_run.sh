@@ -12,7 +12,7 @@
 #                                      -> <outdir>/kernel_stats_<name>.csv
 #   pmc:<name>:<counters>:<bench args> one rocprofv3 --pmc pass -> <outdir>/pmc_<name>.csv
 #   py:<name>:<script> [args]          python3 <script> [args] -> <outdir>/<name>.log
-# Environment variables given before the command apply to every step (e.g. SDIAR_LSTM_WV=4).
+# Environment variables given before the command apply to every step (e.g. SDIAR_CAM_ONE_STREAM=1).
 set -uo pipefail
 OUT=$1; shift
 mkdir -p "$OUT"
