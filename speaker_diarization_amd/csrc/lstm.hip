@@ -257,6 +257,22 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   // W_lo fragments of this wave's rows (X3): fragment (gate, k0 / 32) as the MFMA reads W_hi from LDS
   constexpr int NWL = X3 ? 4 * (H / 32) : 1;
   bf16x8 wl[NWL];
+  // REGW: the wave's W_hi fragments (4 gates x its 16 units x H: 32 fragments, 128 VGPRs) stay in registers for
+  // the launch, so a step's MFMA chain reads no LDS -- one row tile on 4 waves (C1 / C3: 6.71-6.81 -> 6.45-6.54 ms
+  // per recording, recurrence 5.92-6.02 -> 5.66-5.70 ms) and two row tiles on 8 waves (two waves per SIMD; C2
+  // 25.35-25.65 -> 25.32-25.43 ms).  Not in the split mode: there it cost C1 9.0 -> 12.0 ms (W_lo already
+  // holds 128 registers)
+  constexpr bool REGW = !X3 && ((MT == 1 && WV == 4) || (MT == 2 && WV == 8));
+  bf16x8 wr[REGW ? 4 * (H / 32) : 1];
+  if constexpr (REGW) {
+    const uint16_t* wd = whh + (int64_t)d * 4 * H * H;
+#pragma unroll
+    for (int gate = 0; gate < 4; ++gate)
+#pragma unroll
+      for (int kc = 0; kc < H / 32; ++kc)
+        wr[gate * (H / 32) + kc] = *reinterpret_cast<const bf16x8*>(
+            wd + (int64_t)(gate * H + 64 * q + 16 * w + l15) * H + kc * 32 + 8 * g);
+  }
   if constexpr (X3) {
     const uint16_t* wd = whl + (int64_t)d * 4 * H * H;
 #pragma unroll
@@ -374,7 +390,9 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
       for (int mt = 0; mt < MTW; ++mt) hf[mt] = hfa[mt][k0 / 32];
 #pragma unroll
       for (int gate = 0; gate < 4; ++gate) {
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
+        bf16x8 wf;
+        if constexpr (REGW) wf = wr[gate * (H / 32) + k0 / 32];
+        else wf = *reinterpret_cast<const bf16x8*>(&wsl[(gate * 64 + 16 * w + l15) * LS_WS + k0 + 8 * g]);
         if constexpr (X3) {   // small terms first, as the split GEMMs
 #pragma unroll
           for (int mt = 0; mt < MTW; ++mt) {
