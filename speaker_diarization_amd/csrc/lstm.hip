@@ -383,6 +383,9 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
           hla[mt][kc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                        rh, hx_off(pin, rb(mt), kc * 32 + 8 * g, 1), 0, 16));
     }
+    // keep every load above issued together: left alone, the scheduler sinks them next to their MFMAs when the
+    // registers are tight (the register-resident W_hh), two in flight at a time -- 8 serial L2 round trips
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MTW];
