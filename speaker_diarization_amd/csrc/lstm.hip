@@ -385,7 +385,8 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
     }
     // keep every load above issued together: left alone, the scheduler sinks them next to their MFMAs when the
     // registers are tight (the register-resident W_hh), two in flight at a time -- 8 serial L2 round trips
-    __builtin_amdgcn_sched_barrier(0);
+    // (C1 recurrence 5.8-6.0 -> 5.3-5.6 ms).  Not in the split mode, whose 16 loads then cost C1 9.0 -> 10.3 ms.
+    if constexpr (!X3) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k0 = 0; k0 < H; k0 += 32) {
       bf16x8 hf[MTW];
