@@ -204,6 +204,28 @@ def test_tsvad_v1_large_batch_uses_wide_gemm_paths(gpu):
     assert err < BF16_ATOL
 
 
+def test_tsvad_bf16x3_two_row_tile_recurrence(gpu):
+    """B = 520 windows: more than 512 BiLSTM sequences per direction, so the persistent recurrence runs two row
+    tiles per group (co-residency: 4 x 2 x ceil(B / 16) workgroups must fit the CUs) -- in bf16x3 mode the
+    split kernel lstm_group_bf16_kernel<2, 4, true>.  Its logits against the same forward in exact fp32 (the
+    step kernel) within the fp32 bound."""
+    cfg = _cfg(1, 6)
+    sd = to_torch(tsvad_state_dict(cfg, seed=41))
+    B = 520
+    x, ts = tsvad_inputs(B, 598, 150, seed=42)
+    xd, tsd = torch.from_numpy(x).to(gpu), torch.from_numpy(ts).to(gpu)
+    outs = {}
+    for prec in ("fp32", "bf16x3"):
+        m = TSVADModel(cfg, device=gpu, precision=prec, max_batch=B)
+        m.load_state_dict(sd)
+        outs[prec] = m.forward(xd, tsd, 150).cpu().numpy()
+        del m
+        torch.cuda.empty_cache()
+    err = np.abs(outs["bf16x3"] - outs["fp32"]).max()
+    print(f"B={B} bf16x3 vs fp32: max|logit diff| = {err:.3e}")
+    assert np.isfinite(outs["bf16x3"]).all() and err < FP32_ATOL
+
+
 @pytest.mark.parametrize("variant", [0, 1])
 def test_tsvad_repeated_forward_bit_identical(gpu, variant):
     """Repeated forwards on one handle (its workspaces, LSTM exchange buffers and counters reused) give
