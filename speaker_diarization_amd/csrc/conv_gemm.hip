@@ -64,7 +64,9 @@ __device__ __forceinline__ void staged_epilogue_f32(const ConvGemmArgs& p, const
   __syncthreads();
   float* const outp = reinterpret_cast<float*>(p.out);
   const bool lin = out_rows_linear(p);
-  if (lin && p.o_sn == 1 && (p.o_sw & 3) == 0 && !p.gate && (!p.res || (p.res_ld & 3) == 0)) {
+  // float4 rows: unit column stride, 4-float row strides and 16-B aligned base pointers
+  if (lin && p.o_sn == 1 && (p.o_sw & 3) == 0 && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0 && !p.gate &&
+      (!p.res || ((p.res_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))) {
     constexpr int RPI = 256 / CPR, ITER = BM / RPI;
     const int cg = tid % CPR, r0 = tid / CPR, n = n0 + cg * 4;
     if (n >= p.N) return;
