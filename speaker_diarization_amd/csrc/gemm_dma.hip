@@ -264,9 +264,13 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(ConvGemmArgs p) {
   __syncthreads();
 
   const bool lin = out_rows_linear(p);
-  const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0;
+  // 4-column vector stores: unit column stride, 4-element row strides, base pointers aligned for the vector width
+  // (16 B fp32, 8 B bf16; split-K slabs are whole allocations)
+  const bool vec = lin && p.o_sn == 1 && (p.o_sw & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(p.out) & (p.out_bf16 ? 7 : 15)) == 0;
   constexpr int CPR = BN / 4;
-  if (vec && !p.gate && (!p.res || (!p.res_bf16 && (p.res_ld & 3) == 0))) {
+  if (vec && !p.gate &&
+      (!p.res || (!p.res_bf16 && (p.res_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))) {
     // Fast epilogue (row-major output): each thread owns one 4-column group, so the
     // per-channel alpha/beta are loaded once, and all residual rows are fetched before
     // any store (res may alias out: the in-place residual add of the encoders).
