@@ -244,8 +244,14 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   const int ub = 64 * q + 16 * w + 4 * g;       // first of this lane's 4 units
   auto rb = [&](int j) { return b0 + (j * WPU + wt) * 16 + l15; };   // batch row of the lane in its j-th tile
 
-  // W slice -> LDS: slice row (gate, j) = W_hh row gate*H + 64q + j.
-  {
+  // REGW: the wave's W_hi fragments (4 gates x its 16 units x H: 32 fragments, 128 VGPRs) stay in registers for
+  // the launch, so a step's MFMA chain reads no LDS -- one row tile on 4 waves (C1 / C3: 6.71-6.81 -> 6.45-6.54 ms
+  // per recording, recurrence 5.92-6.02 -> 5.66-5.70 ms) and two row tiles on 8 waves (two waves per SIMD; C2
+  // 25.35-25.65 -> 25.32-25.43 ms).  Not in the split mode: there it cost C1 9.0 -> 12.0 ms (W_lo already
+  // holds 128 registers)
+  constexpr bool REGW = !X3 && ((MT == 1 && WV == 4) || (MT == 2 && WV == 8));
+  // W slice -> LDS (the layouts that read W_hi from LDS): slice row (gate, j) = W_hh row gate*H + 64q + j.
+  if constexpr (!REGW) {
     const uint16_t* wd = whh + (int64_t)d * 4 * H * H;
     for (int i = tid; i < 256 * (H / 8); i += NT) {
       const int row = i / (H / 8), k8 = (i % (H / 8)) * 8;
@@ -257,12 +263,6 @@ __global__ __launch_bounds__(64 * WV) void lstm_group_bf16_kernel(
   // W_lo fragments of this wave's rows (X3): fragment (gate, k0 / 32) as the MFMA reads W_hi from LDS
   constexpr int NWL = X3 ? 4 * (H / 32) : 1;
   bf16x8 wl[NWL];
-  // REGW: the wave's W_hi fragments (4 gates x its 16 units x H: 32 fragments, 128 VGPRs) stay in registers for
-  // the launch, so a step's MFMA chain reads no LDS -- one row tile on 4 waves (C1 / C3: 6.71-6.81 -> 6.45-6.54 ms
-  // per recording, recurrence 5.92-6.02 -> 5.66-5.70 ms) and two row tiles on 8 waves (two waves per SIMD; C2
-  // 25.35-25.65 -> 25.32-25.43 ms).  Not in the split mode: there it cost C1 9.0 -> 12.0 ms (W_lo already
-  // holds 128 registers)
-  constexpr bool REGW = !X3 && ((MT == 1 && WV == 4) || (MT == 2 && WV == 8));
   bf16x8 wr[REGW ? 4 * (H / 32) : 1];
   if constexpr (REGW) {
     const uint16_t* wd = whh + (int64_t)d * 4 * H * H;
