@@ -61,3 +61,16 @@ def test_checker_finds_the_round5_branch_pattern(tmp_path):
     assert all(re.search(r"mha_block_kernelILi\d+ELi4E", f[0]) for f in found), {f[0] for f in found}
     # and it is the taken-edge read the round-5 schedule had: an AGPR read a few wait states after the MFMA
     assert any(f[5] == "v_accvgpr_read_b32" and f[7] <= 2 for f in found)
+
+
+def test_checker_flags_write_after_write_and_taken_edges():
+    """Synthetic instruction lists: a VALU overwrite of an MFMA destination inside its window is reported (the
+    MFMA's later write-back would clobber it), a far one is not, and a read on a branch target is followed."""
+    mf = ("v_mfma_f32_16x16x32_bf16", "v[0:3], v[4:7], v[8:11], v[0:3]")
+    waw = [mf, ("v_mov_b32_e32", "v2, 0xff800000"), ("s_endpgm", "")]
+    assert isa_hazards.check_function("waw", waw, {})
+    late = [mf, ("s_nop", "7"), ("v_mov_b32_e32", "v2, 0xff800000"), ("s_endpgm", "")]
+    assert not isa_hazards.check_function("late", late, {})
+    taken = [mf, ("s_cbranch_vccnz", "L1"), ("s_nop", "7"), ("s_endpgm", ""), ("v_add_f32_e32", "v12, v3, v3"),
+             ("s_endpgm", "")]
+    assert isa_hazards.check_function("taken", taken, {"L1": 4})

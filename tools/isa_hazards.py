@@ -13,7 +13,9 @@ path of a uniform branch:
 
 This checker follows every path (fall-through and branch targets) from each MFMA and reports a read of any of its
 destination registers by a VALU / memory instruction before that register's measured wait states (each
-instruction counts one, s_nop N counts N + 1; need_for()), unless the register was overwritten first.
+instruction counts one, s_nop N counts N + 1; need_for()), unless the register was overwritten first -- and, as
+a write-after-write hazard, a VALU write of a destination register inside the same window (the MFMA's own late
+write-back would land on top of it; the RAW thresholds are used for it, the WAW ones were not probed).
     python tools/isa_hazards.py [object files ...]      (default: speaker_diarization_amd/lib/obj/*.o)
 Exit status 1 if any hazard is found."""
 from __future__ import annotations
@@ -140,6 +142,8 @@ def check_function(name, ins, labels, max_paths=20000):
                 mj, oj = ins[j]
                 if is_reader(mj):
                     hit = [r for r in sources(mj, oj) & live if ws < need_of[r]]
+                    if not hit and mj.startswith("v_"):   # WAW: a VALU overwrite inside the MFMA's window
+                        hit = [r for r in dests(mj, oj) & live if ws < need_of[r]]
                     if hit:
                         found.append((name, i, mn, ops, j, mj, oj, ws))
                         break
@@ -172,7 +176,7 @@ def main(argv):
             total += check_function(name, ins, labels)
     for name, i, mn, ops, j, mj, oj, ws in total:
         print(f"HAZARD {name}: [{i}] {mn} {ops}  ->  [{j}] {mj} {oj}  after {ws} wait states")
-    print(f"{len(objs)} objects, {kernels} functions, {len(total)} MFMA-result reads below the measured wait states")
+    print(f"{len(objs)} objects, {kernels} functions, {len(total)} MFMA-result reads / overwrites below the measured wait states")
     return 1 if total else 0
 
 
